@@ -1,0 +1,267 @@
+#!/usr/bin/env python3
+"""bench.py -- SMA param-bucket reduce on MI355X (BASELINE.json metric).
+
+A "step" is one ModelManager.trySynchronise (lockAny -> synchronise ->
+unlockAny, ModelManager.java:293-353) over the full flat parameter buffer of
+the workload, with every input already resident in HBM:
+
+  N = 1 : configs[2] (C3) -- ResNet-50 fp32 parameters (n = 25,557,032),
+          8 replicas on one MI355X, alpha 0.1, momentum 0.9: the fused kernel.
+  N > 1 : the same 8 replicas per GPU on each of N GPUs (weak scaling):
+          kernel A + RCCL all-reduce over xGMI + kernel B per GPU.
+
+value = algorithmic bytes moved by all ranks / max-over-ranks wall time of
+exactly K steps ((12R+8+8m)n per step at G = 1, and
+(12R+8)n + (12+8m)n per GPU at G > 1; the all-reduce is reported apart).
+
+Run:  python bench.py [--gpus N --steps K --warmup W]
+      python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+METRIC = "GB/s device-resident SMA param-bucket reduce (ResNet-50, 8 replicas)"
+HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+XGMI_PEAK_GBS = 7 * 153.0  # per GPU, 7 links
+SEED = 20190701
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def parse():
+    p = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=50)
+    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--model", choices=["resnet50", "lenet"], default="resnet50")
+    p.add_argument("--replicas", type=int, default=8, help="replicas per GPU")
+    p.add_argument("--alpha", type=float, default=0.1)
+    p.add_argument("--momentum", type=float, default=0.9)
+    p.add_argument("--block", type=int, default=256)
+    p.add_argument("--blocks-per-cu", type=int, default=0)
+    p.add_argument("--policy", type=int, default=1, help="0 plain, 1 nontemporal loads/stores")
+    p.add_argument("--unroll", type=int, default=1)
+    p.add_argument("--bucket-mb", type=float, default=0.0, help="G>1 pipeline bucket (MB of fp32), 0 = one")
+    p.add_argument("--force-split", action="store_true", help="use kernel A + all-reduce + B even at G=1")
+    p.add_argument("--cpu-seconds", type=float, default=10.0)
+    p.add_argument("--cpu-elements", type=int, default=1 << 22)
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-staged", action="store_true")
+    p.add_argument("--no-copy-ceiling", action="store_true")
+    p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
+                   help="PMC-derived HBM bytes per launch (written by scripts/pmc_traffic.py)")
+    return p.parse_args()
+
+
+def alg_bytes(n, R, momentum, G):
+    m = 1 if momentum > 0 else 0
+    if G == 1:
+        return (12 * R + 8 + 8 * m) * n, (12 * R + 8 + 8 * m) * n
+    a = (12 * R + 8) * n
+    return a + (12 + 8 * m) * n, a
+
+
+def cpu_baseline(args, n_full):
+    """The reference's call sequence (memset, memcpy + 3 saxpy per replica,
+    momentum, apply) on OpenBLAS, 1 thread bound to core 0 like TheCPU.bind(0)
+    (clib-multigpu/CPU.c:39-52, BLAS.c:32), on a bounded sample."""
+    from oracle import oracle as O
+    n = min(args.cpu_elements, n_full)
+    lib = O.blas_open()
+    O.blas_set_threads(1)
+    st = O.make_state(n, 1, args.replicas, args.alpha, args.momentum)
+    O.bind_core(0)
+    try:
+        O.sma_step_blas(st)  # warm
+        steps, t0 = 0, O.now()
+        while True:
+            O.sma_step_blas(st)
+            steps += 1
+            el = O.now() - t0
+            if el >= args.cpu_seconds:
+                break
+    finally:
+        O.unbind()
+    b, _ = alg_bytes(n, args.replicas, args.momentum, 1)
+    return {"value": round(b * steps / el / 1e9, 3), "unit": "GB/s", "cores": 1, "kind": "port",
+            "sample": f"{n} fp32 elements x {args.replicas} replicas, momentum {args.momentum}, {steps} steps "
+                      f"in {el:.1f} s; reference BLAS call sequence (sma.c:13-231) on OpenBLAS "
+                      f"({os.path.basename(lib)}), 1 thread pinned to core 0, same algorithmic-bytes formula"}
+
+
+def main():
+    args = parse()
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: launch N>1 with torch.distributed.run")
+
+    import torch
+    import torch.distributed as dist
+
+    from crossbow_amd import SYNC_BSP, UPDATE_SMA, TheGPU, _lib
+    from crossbow_amd.variables import MODELS, register
+
+    torch.cuda.set_device(local_rank)
+    if world > 1:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+
+    gpu = TheGPU()
+    uid = None
+    if world > 1:
+        obj = [gpu.unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(obj, src=0)
+        uid = obj[0]
+    gpu.init_rank(local_rank, world, rank, uid)
+
+    shapes = MODELS[args.model]()
+    n = register(gpu, shapes)
+    gpu.setUpdateModelType(UPDATE_SMA)
+    gpu.setEamsgdAlpha(args.alpha)
+    gpu.setMomentum(args.momentum, 0)
+    gpu.setModelManager(args.replicas, SYNC_BSP)
+    gpu.set_kernel_config(args.block, args.blocks_per_cu, args.policy, args.unroll)
+    if args.bucket_mb > 0:
+        gpu.set_bucket_elements(int(args.bucket_mb * (1 << 20) / 4))
+    if args.force_split:
+        gpu.set_force_split(True)
+    gpu.fill_synthetic(SEED)
+    gpu.set_timing(True)
+
+    clock = 0
+
+    def step():
+        nonlocal clock
+        clock += 1
+        gpu.lockAny()
+        gpu.synchronise(0, clock, 0, False)
+        gpu.unlockAny()
+
+    for _ in range(args.warmup):
+        step()
+    gpu.wait()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    gpu.wait()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    if world > 1:
+        dist.barrier()
+        t = torch.tensor([el], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+
+    G = world
+    split = G > 1 or args.force_split
+    step_bytes, kernel_bytes = alg_bytes(n, args.replicas, args.momentum, 2 if split else 1)
+    kern = gpu.timing_history(_lib.T_KERNEL)[-args.steps:]
+    steps_ms = gpu.timing_history(_lib.T_STEP)[-args.steps:]
+    kern_ms = statistics.mean(kern)
+    result = {
+        "metric": METRIC,
+        "value": round(step_bytes * G * args.steps / el / 1e9, 2),
+        "unit": "GB/s",
+        "n_gpus": G,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(el * 1e3 / args.steps, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "fp32",
+        "data": "synthetic (splitmix64 -> Box-Muller, BASELINE.md 2.3), generated on device",
+        "config": {
+            "workload": f"{args.model}-params SMA reduce+correct, {args.replicas} replicas/GPU x {G} GPU",
+            "elements": n,
+            "replicas_per_gpu": args.replicas,
+            "alpha": args.alpha,
+            "momentum": args.momentum,
+            "bytes_per_step_per_gpu": step_bytes,
+            "parallelism": f"sma-dp{G}",
+            "pipeline": "fused" if not split else "accumulate+rccl-allreduce+apply",
+            "kernel_config": dict(block=args.block, blocks_per_cu=args.blocks_per_cu, policy=args.policy,
+                                  unroll=args.unroll, bucket_mb=args.bucket_mb),
+        },
+    }
+    kname = "sma_fused_kernel" if not split else "sma_accumulate_kernel"
+    achieved = kernel_bytes / (kern_ms * 1e-3) / 1e9
+    traffic = None
+    try:
+        with open(args.traffic_json) as f:
+            tj = json.load(f)
+        key = f"{kname}/{args.model}/R{args.replicas}/m{1 if args.momentum > 0 else 0}"
+        traffic = tj.get(key, {}).get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        pass
+    result["roofline"] = {"bound": "hbm", "kernel": kname, "achieved": round(achieved, 1),
+                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                          "traffic": traffic, "alg_bytes_per_launch": kernel_bytes,
+                          "launch_ms_mean": round(kern_ms, 4), "launch_ms_median": round(statistics.median(kern), 4),
+                          "launches": len(kern)}
+    result["step_ms_device_median"] = round(statistics.median(steps_ms), 4)
+    if split:
+        ar = gpu.timing_history(_lib.T_ALLREDUCE)[-args.steps:]
+        ap = gpu.timing_history(_lib.T_APPLY)[-args.steps:]
+        ar_ms = statistics.median(ar)
+        algbw = 4 * n / (ar_ms * 1e-3) / 1e9
+        busbw = algbw * 2 * (G - 1) / G if G > 1 else 0.0
+        result["allreduce"] = {"ms_median": round(ar_ms, 4), "algbw_GBs": round(algbw, 1),
+                               "busbw_GBs": round(busbw, 1), "xgmi_peak_GBs": XGMI_PEAK_GBS,
+                               "apply_ms_median": round(statistics.median(ap), 4)}
+
+    if rank == 0 and world == 1:
+        if not args.no_copy_ceiling:
+            result["copy_ceiling_GBs"] = round(gpu.bench_copy(1 << 30, 20), 1)
+        if not args.no_staged:
+            # Host-staged rate (north_star): pinned H2D of z, last, s_i, w_i,
+            # the step, pinned D2H of z, last, w_i.  Reported, never `value`.
+            samples = []
+            for _ in range(3):
+                gpu.stage_in()
+                step()
+                gpu.stage_out()
+                gpu.wait()
+                samples.append(gpu.last_timing(0))
+            t = sorted(samples, key=lambda x: x[_lib.T_H2D] + x[_lib.T_KERNEL] + x[_lib.T_D2H])[1]
+            m = 1 if args.momentum > 0 else 0
+            h2d = (2 * args.replicas + 1 + m) * 4 * n
+            d2h = (args.replicas + 1 + m) * 4 * n
+            tot = (t[_lib.T_H2D] + t[_lib.T_KERNEL] + t[_lib.T_D2H]) * 1e-3
+            result["host_staged"] = {
+                "h2d_ms": round(t[_lib.T_H2D], 3), "kernel_ms": round(t[_lib.T_KERNEL], 4),
+                "d2h_ms": round(t[_lib.T_D2H], 3),
+                "h2d_GBs": round(h2d / (t[_lib.T_H2D] * 1e-3) / 1e9, 2),
+                "d2h_GBs": round(d2h / (t[_lib.T_D2H] * 1e-3) / 1e9, 2),
+                "end_to_end_GBs": round(step_bytes / tot / 1e9, 2),
+            }
+        if not args.no_cpu_baseline:
+            result["cpu_baseline"] = cpu_baseline(args, n)
+        else:
+            result["cpu_baseline"] = None
+
+    gpu.free()
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,98 @@
+"""Build the native pieces of crossbow_amd in-tree.
+
+* ``crossbow_amd/libcrossbow_sma.so``  -- the C-ABI library (hipcc, gfx950):
+  csrc/context.hip + csrc/sma_kernels.hip, linked against RCCL.
+* ``crossbow_amd/libGPU.so``           -- the JNI shim exporting Crossbow's
+  ``TheGPU`` model-path natives; built only where ``jni.h`` exists (there is
+  no JDK in this image).
+
+Usage: ``python -m crossbow_amd.build [--force]``.
+"""
+from __future__ import annotations
+
+import glob
+import os
+import shutil
+import subprocess
+import sys
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(PKG)
+CSRC = os.path.join(PKG, "csrc")
+LIB = os.path.join(PKG, "libcrossbow_sma.so")
+JNI_LIB = os.path.join(PKG, "libGPU.so")
+ARCH = "gfx950"
+
+
+def _hipcc() -> str:
+    for c in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", shutil.which("hipcc")):
+        if c and os.path.exists(c):
+            return c
+    raise RuntimeError("hipcc not found: the MI355X library needs ROCm's hipcc")
+
+
+def _sources():
+    return [os.path.join(CSRC, "context.hip"), os.path.join(CSRC, "sma_kernels.hip")]
+
+
+def _deps():
+    return _sources() + [os.path.join(CSRC, "sma_internal.h"), os.path.join(ROOT, "include", "crossbow_sma.h")]
+
+
+def _stale(target: str, deps) -> bool:
+    if not os.path.exists(target):
+        return True
+    t = os.path.getmtime(target)
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def build_lib(force: bool = False, verbose: bool = False) -> str:
+    if not force and not _stale(LIB, _deps()):
+        return LIB
+    tmp = LIB + ".tmp"
+    cmd = [_hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wall",
+           "-I", os.path.join(ROOT, "include"), "-o", tmp] + _sources() + ["-lrccl", "-lpthread"]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    subprocess.run(cmd, check=True)
+    os.replace(tmp, LIB)
+    return LIB
+
+
+def find_jni_include():
+    cands = []
+    jh = os.environ.get("JAVA_HOME")
+    if jh:
+        cands.append(os.path.join(jh, "include"))
+    cands += glob.glob("/usr/lib/jvm/*/include")
+    for c in cands:
+        if os.path.exists(os.path.join(c, "jni.h")):
+            return c
+    return None
+
+
+def build_jni(force: bool = False, verbose: bool = False):
+    """Build libGPU.so (the JNI drop-in) when a JDK is present; else None."""
+    inc = find_jni_include()
+    if inc is None:
+        return None
+    src = os.path.join(CSRC, "jni", "TheGPU_jni.c")
+    if not force and not _stale(JNI_LIB, [src, LIB]):
+        return JNI_LIB
+    cmd = ["gcc", "-O2", "-fPIC", "-shared", "-I", inc, "-I", os.path.join(inc, "linux"),
+           "-I", os.path.join(ROOT, "include"), "-o", JNI_LIB, src, "-L", PKG, "-lcrossbow_sma",
+           "-Wl,-rpath,$ORIGIN"]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    subprocess.run(cmd, check=True)
+    return JNI_LIB
+
+
+def build(force: bool = False, verbose: bool = False) -> str:
+    lib = build_lib(force, verbose)
+    build_jni(force, verbose)
+    return lib
+
+
+if __name__ == "__main__":
+    print(build(force="--force" in sys.argv, verbose=True))

@@ -1,0 +1,1439 @@
+// context.hip -- execution context, model manager and SMA orchestration
+// behind the C-ABI of include/crossbow_sma.h.
+//
+// MI355X-first restatement of the reference's native runtime for the model
+// path: crossbowExecutionContext (clib-multigpu/executioncontext.c), the model
+// manager (modelmanager.c), the model buffers (model.c, databuffer.c), solver
+// configuration (solverconfiguration.c) and the SMA synchronisation
+// (synch/sma.c, synch/common.c).  Differences by design:
+//   * one device arena per GPU (one hipMalloc) holding the base model and every
+//     replica buffer, instead of ~5 cudaMallocs per model;
+//   * the SMA step is one fused kernel at G = 1 and kernel A + RCCL all-reduce
+//     + kernel B at G > 1 (optionally bucketed and pipelined), instead of
+//     3R+3 cuBLAS saxpys, R+4 copies and three cudaDeviceSynchronize;
+//   * the Phase-D "copy base to replicas" decision travels with the all-reduce
+//     (control block) instead of a host-side count;
+//   * errors return codes; the JNI shim turns them back into exit(1).
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <pthread.h>
+#include <sys/stat.h>
+#include <sys/types.h>
+#include <fcntl.h>
+#include <unistd.h>
+#include <errno.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "../../include/crossbow_sma.h"
+#include "sma_internal.h"
+
+namespace {
+
+thread_local std::string g_last_error;
+
+int fail(int code, const char *fmt, ...) {
+  char buf[1024];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  g_last_error = buf;
+  return code;
+}
+
+#define HIP_TRY(call)                                                                              \
+  do {                                                                                             \
+    hipError_t e_ = (call);                                                                        \
+    if (e_ != hipSuccess)                                                                          \
+      return fail(CBX_ERR_HIP, "%s:%d %s: %s", __FILE__, __LINE__, #call, hipGetErrorString(e_)); \
+  } while (0)
+
+#define NCCL_TRY(call)                                                                             \
+  do {                                                                                             \
+    ncclResult_t r_ = (call);                                                                      \
+    if (r_ != ncclSuccess)                                                                         \
+      return fail(CBX_ERR_RCCL, "%s:%d %s: %s", __FILE__, __LINE__, #call, ncclGetErrorString(r_)); \
+  } while (0)
+
+#define TRY(expr)            \
+  do {                       \
+    int rc_ = (expr);        \
+    if (rc_ < 0) return rc_; \
+  } while (0)
+
+// ---------------------------------------------------------------------------
+// Solver configuration, clib-multigpu/solverconfiguration.{h,c}
+// ---------------------------------------------------------------------------
+enum LrPolicy { LR_FIXED = 0, LR_INV, LR_STEP, LR_MULTISTEP, LR_EXP, LR_CLR, LR_LSR };
+
+struct SolverConf {
+  float alpha = 0.5f;  // solverconfiguration.c:17
+  int tau = 1;
+  LrPolicy policy = LR_FIXED;
+  float learningRate = 0.0f;
+  double gamma = 0.0;
+  double power = 0.0;
+  int size = 0;
+  std::vector<int> steps;
+  int step = 0;
+  int warmuptasks = 0;
+  float momentum = 0.0f;
+  int momentumMethod = 0;
+  float weightDecay = 0.0f;
+  float baseModelMomentum = 0.0f;
+  unsigned copy = 0;  // `_copy`, solverconfiguration.h:41-52
+
+  // crossbowSolverConfGetLearningRate, solverconfiguration.c:116-162.
+  int learning_rate(int task, float *out) {
+    float rate = 0.0f;
+    switch (policy) {
+      case LR_FIXED: rate = learningRate; break;
+      case LR_INV: rate = learningRate * (float)std::pow(1.0 + gamma * (double)(task + 1), -power); break;
+      case LR_STEP:
+        if (size <= 0) return fail(CBX_ERR_STATE, "step learning-rate policy with size 0");
+        rate = learningRate * (float)std::pow(gamma, std::floor((double)((task + 1) / size)));
+        break;
+      case LR_MULTISTEP:
+        if (step < (int)steps.size() && (task + 1) >= steps[step]) {
+          step++;
+          copy = 1;  // signal Phase D (solverconfiguration.c:133)
+        }
+        rate = learningRate * (float)std::pow(gamma, (double)step);
+        break;
+      case LR_LSR:
+        if (warmuptasks <= 0) return fail(CBX_ERR_STATE, "LSR policy without warm-up tasks");
+        if (task < warmuptasks) {
+          rate = (learningRate * (float)task) / (float)warmuptasks;
+        } else {
+          if (step < (int)steps.size() && (task + 1) >= steps[step]) {
+            step++;
+            copy = 1;  // solverconfiguration.c:147
+          }
+          rate = learningRate * (float)std::pow(gamma, (double)step);
+        }
+        break;
+      case LR_EXP: rate = learningRate * (float)std::pow(gamma, (double)(task + 1)); break;
+      default: return fail(CBX_ERR_UNSUPPORTED, "learning-rate policy %d unsupported", (int)policy);
+    }
+    *out = rate;
+    return CBX_OK;
+  }
+};
+
+// ---------------------------------------------------------------------------
+// Model definition (theModel before the manager exists), model.c:8-200
+// ---------------------------------------------------------------------------
+struct Variable {
+  int64_t offset_bytes;
+  int64_t bytes;
+  int64_t elements;
+};
+
+struct ModelDef {
+  bool defined = false;
+  int ops = 0;
+  int64_t bytes = 0;       // setModel size (sum of capacities)
+  int64_t offset = 0;      // model.c:151 running offset
+  int64_t elements = 0;    // model.c:153
+  int wpc = 0;
+  int type = 0;            // update model type
+  SolverConf conf;
+  std::map<std::pair<int, int>, Variable> vars;  // (op id, order) -> variable
+  std::vector<int> count_per_op;
+  std::vector<float> host;  // initial values (PIN host buffer of theModel->data)
+};
+
+struct Replica {
+  int id = 0;
+  int g = 0;          // global device index (id % G)
+  int local = -1;     // local device slot, -1 if in another process
+  int slot = 0;       // replica slot within its device
+  int clock = 0;
+  int updates = 0;
+  SolverConf conf;
+  pthread_mutex_t lock;
+  hipEvent_t updated = nullptr;
+};
+
+enum TimingEv { EV_START = 0, EV_A, EV_AR, EV_B, EV_H2D0, EV_H2D1, EV_D2H0, EV_D2H1, EV_COUNT };
+
+struct Device {
+  int hip_id = 0;
+  int g = 0;  // global device index
+  hipStream_t stream = nullptr;
+  ncclComm_t comm = nullptr;
+  int num_cus = 256;
+  // Arena: [base data][base gradient(ctrl+acc)][base diff(ctrl+D)][base last]
+  //        then per replica [data][diff][last][gradient].
+  char *arena = nullptr;
+  char *host = nullptr;  // pinned mirror, same layout (lazy)
+  size_t arena_bytes = 0;
+  size_t stride = 0;  // bytes per buffer slot
+  std::vector<int> replicas;  // global ids, increasing
+  hipEvent_t base_updated = nullptr, accumulated = nullptr, synched = nullptr;
+  hipEvent_t ev[EV_COUNT] = {};
+  bool ev_valid[EV_COUNT] = {};
+  // Per-step timing ring: events {START, A, AR, B} of the last kRing steps,
+  // so a benchmark reads every launch of its timed region afterwards without
+  // a host synchronisation between steps.
+  static constexpr int kRing = 1024;
+  std::vector<hipEvent_t> ring;
+  std::vector<char> ring_split;
+  int ring_pos = 0;
+  int ring_count = 0;
+};
+
+}  // namespace
+
+struct cbx_context {
+  std::vector<Device> devs;
+  int G = 1;           // global device count (ranks)
+  bool per_rank = false;
+  ModelDef model;
+  bool manager = false;
+  int R = 0;           // replicas per device
+  int size = 0;        // R * G
+  int sync_type = CBX_SYNC_BSP;
+  std::vector<Replica *> replicas;  // global id -> replica (all ids; remote ones have local = -1)
+  std::vector<int> locked;
+  int64_t n = 0;       // model elements
+  int64_t n4 = 0;      // padded float4 count
+  bool has_last = false;
+  unsigned long long version = 0;
+  bool timing = false;
+  cbx::LaunchConfig cfg;
+  int64_t bucket_elems = 0;
+  bool force_split = false;
+  bool last_step_split = false;
+};
+
+namespace {
+
+// ---------------------------------------------------------------------------
+// Arena layout helpers
+// ---------------------------------------------------------------------------
+constexpr int kBaseSlots = 4;     // data, gradient, diff, last
+constexpr int kReplicaSlots = 4;  // data, diff, last, gradient
+constexpr size_t kAlign = 2u << 20;
+
+size_t slot_index_base(int kind) {
+  switch (kind) {
+    case CBX_BUF_DATA: return 0;
+    case CBX_BUF_GRADIENT: return 1;
+    case CBX_BUF_DIFF: return 2;
+    default: return 3;
+  }
+}
+
+size_t slot_index_replica(int slot, int kind) {
+  size_t k;
+  switch (kind) {
+    case CBX_BUF_DATA: k = 0; break;
+    case CBX_BUF_DIFF: k = 1; break;
+    case CBX_BUF_LAST: k = 2; break;
+    default: k = 3; break;
+  }
+  return kBaseSlots + (size_t)slot * kReplicaSlots + k;
+}
+
+// Byte offset of the model data inside a slot: acc and D carry a 256-byte
+// control block in front (sma_internal.h).
+size_t data_offset(bool ctrl) { return ctrl ? (size_t)cbx::kCtrlFloats * sizeof(float) : 0; }
+
+float *slot_ptr(char *arena, const Device &d, size_t slot, bool ctrl) {
+  return reinterpret_cast<float *>(arena + slot * d.stride + data_offset(ctrl));
+}
+
+bool base_has(const cbx_context *c, int kind) { return kind != CBX_BUF_LAST || c->has_last; }
+
+float *base_dev(const cbx_context *c, const Device &d, int kind) {
+  const bool ctrl = (kind == CBX_BUF_GRADIENT || kind == CBX_BUF_DIFF);
+  return slot_ptr(d.arena, d, slot_index_base(kind), ctrl);
+}
+
+float *base_ctrl(const Device &d, int kind) {
+  return reinterpret_cast<float *>(d.arena + slot_index_base(kind) * d.stride);
+}
+
+float *replica_dev(const Device &d, const Replica &r, int kind) {
+  return slot_ptr(d.arena, d, slot_index_replica(r.slot, kind), false);
+}
+
+float *base_host(const Device &d, int kind) {
+  const bool ctrl = (kind == CBX_BUF_GRADIENT || kind == CBX_BUF_DIFF);
+  return slot_ptr(d.host, d, slot_index_base(kind), ctrl);
+}
+
+float *replica_host(const Device &d, const Replica &r, int kind) {
+  return slot_ptr(d.host, d, slot_index_replica(r.slot, kind), false);
+}
+
+int check_ctx(cbx_context *c) {
+  if (!c) return fail(CBX_ERR_INVALID, "null context");
+  return CBX_OK;
+}
+
+int check_manager(cbx_context *c) {
+  TRY(check_ctx(c));
+  if (!c->manager) return fail(CBX_ERR_STATE, "model manager not created (call cbx_set_model_manager)");
+  return CBX_OK;
+}
+
+int check_replica(cbx_context *c, int id, bool need_local) {
+  TRY(check_manager(c));
+  if (id < 0 || id >= c->size) return fail(CBX_ERR_INVALID, "replica id %d out of range [0, %d)", id, c->size);
+  if (need_local && c->replicas[id]->local < 0)
+    return fail(CBX_ERR_INVALID, "replica %d lives in another process (device %d)", id, c->replicas[id]->g);
+  return CBX_OK;
+}
+
+int local_of(cbx_context *c, int g) {
+  for (size_t k = 0; k < c->devs.size(); ++k)
+    if (c->devs[k].g == g) return (int)k;
+  return -1;
+}
+
+int gfx950_device_count(int *count) {
+  int n = 0;
+  *count = 0;
+  hipError_t e = hipGetDeviceCount(&n);
+  if (e != hipSuccess || n <= 0) {
+    (void)hipGetLastError();
+    return CBX_OK;
+  }
+  int k = 0;
+  for (int i = 0; i < n; ++i) {
+    hipDeviceProp_t p;
+    if (hipGetDeviceProperties(&p, i) != hipSuccess) continue;
+    if (std::strncmp(p.gcnArchName, "gfx950", 6) == 0) ++k;
+  }
+  *count = k;
+  return CBX_OK;
+}
+
+int open_device(Device &d, int hip_id, int g) {
+  int total = 0;
+  hipError_t ce = hipGetDeviceCount(&total);
+  if (ce != hipSuccess) {
+    (void)hipGetLastError();
+    return fail(CBX_ERR_NO_DEVICE, "no MI355X visible: %s", hipGetErrorString(ce));
+  }
+  if (hip_id < 0 || hip_id >= total) return fail(CBX_ERR_NO_DEVICE, "device %d not visible (%d devices)", hip_id, total);
+  hipDeviceProp_t p;
+  HIP_TRY(hipGetDeviceProperties(&p, hip_id));
+  if (std::strncmp(p.gcnArchName, "gfx950", 6) != 0)
+    return fail(CBX_ERR_NO_DEVICE, "device %d is %s, this library is built for gfx950 (MI355X) only", hip_id,
+                p.gcnArchName);
+  d.hip_id = hip_id;
+  d.g = g;
+  d.num_cus = p.multiProcessorCount;
+  HIP_TRY(hipSetDevice(hip_id));
+  // executioncontext.c:324: one non-blocking model-synchronisation stream.
+  HIP_TRY(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
+  HIP_TRY(hipEventCreateWithFlags(&d.base_updated, hipEventDisableTiming));
+  HIP_TRY(hipEventCreateWithFlags(&d.accumulated, hipEventDisableTiming));
+  HIP_TRY(hipEventCreateWithFlags(&d.synched, hipEventDisableTiming));
+  for (int k = 0; k < EV_COUNT; ++k) HIP_TRY(hipEventCreate(&d.ev[k]));
+  return CBX_OK;
+}
+
+void close_device(Device &d) {
+  if (d.stream == nullptr && d.arena == nullptr) return;
+  (void)hipSetDevice(d.hip_id);
+  if (d.stream) (void)hipStreamSynchronize(d.stream);
+  if (d.comm) (void)ncclCommDestroy(d.comm);
+  if (d.arena) (void)hipFree(d.arena);
+  if (d.host) (void)hipHostFree(d.host);
+  if (d.base_updated) (void)hipEventDestroy(d.base_updated);
+  if (d.accumulated) (void)hipEventDestroy(d.accumulated);
+  if (d.synched) (void)hipEventDestroy(d.synched);
+  for (int k = 0; k < EV_COUNT; ++k)
+    if (d.ev[k]) (void)hipEventDestroy(d.ev[k]);
+  for (hipEvent_t e : d.ring) (void)hipEventDestroy(e);
+  if (d.stream) (void)hipStreamDestroy(d.stream);
+  d = Device();
+}
+
+// Record a timing event when timing is enabled.  Step events (START..B) go
+// to the current ring slot, staging events to the fixed ones.
+int mark(cbx_context *c, Device &d, int ev) {
+  if (!c->timing) return CBX_OK;
+  if (ev <= EV_B && !d.ring.empty()) {
+    HIP_TRY(hipEventRecord(d.ring[(size_t)d.ring_pos * 4 + ev], d.stream));
+    return CBX_OK;
+  }
+  HIP_TRY(hipEventRecord(d.ev[ev], d.stream));
+  d.ev_valid[ev] = true;
+  return CBX_OK;
+}
+
+void ring_advance(cbx_context *c, Device &d, bool split) {
+  if (!c->timing || d.ring.empty()) return;
+  d.ring_split[d.ring_pos] = split ? 1 : 0;
+  d.ring_pos = (d.ring_pos + 1) % Device::kRing;
+  if (d.ring_count < Device::kRing) d.ring_count++;
+}
+
+// Elapsed ms between events a and b of ring slot `slot` (-1 if absent).
+int ring_span(Device &d, int slot, int a, int b, float *out) {
+  *out = -1.0f;
+  HIP_TRY(hipEventSynchronize(d.ring[(size_t)slot * 4 + b]));
+  HIP_TRY(hipEventElapsedTime(out, d.ring[(size_t)slot * 4 + a], d.ring[(size_t)slot * 4 + b]));
+  return CBX_OK;
+}
+
+// ---------------------------------------------------------------------------
+// SMA step, clib-multigpu/synch/sma.c:13-231
+// ---------------------------------------------------------------------------
+int build_args(cbx_context *c, Device &d, int first, cbx::SmaArgs &a, int *copies) {
+  std::memset(&a, 0, sizeof(a));
+  int k = 0;
+  int cp = 0;
+  for (int id : d.replicas) {  // increasing id order, sma.c:69
+    if (id < first || !c->locked[id]) continue;
+    if (k >= cbx::kMaxReplicas)
+      return fail(CBX_ERR_UNSUPPORTED, "more than %d locked replicas on one device", cbx::kMaxReplicas);
+    Replica &r = *c->replicas[id];
+    a.s[k] = reinterpret_cast<const cbx::v4f *>(replica_dev(d, r, CBX_BUF_DIFF));
+    a.w[k] = reinterpret_cast<cbx::v4f *>(replica_dev(d, r, CBX_BUF_DATA));
+    if (r.conf.copy) cp++;  // sma.c:113-120
+    ++k;
+  }
+  a.nrep = k;
+  a.z = reinterpret_cast<cbx::v4f *>(base_dev(c, d, CBX_BUF_DATA));
+  a.last = c->has_last ? reinterpret_cast<cbx::v4f *>(base_dev(c, d, CBX_BUF_LAST)) : nullptr;
+  a.acc = reinterpret_cast<cbx::v4f *>(base_dev(c, d, CBX_BUF_GRADIENT));
+  a.D = reinterpret_cast<const cbx::v4f *>(base_dev(c, d, CBX_BUF_DIFF));
+  a.ctrl_out = base_ctrl(d, CBX_BUF_GRADIENT);
+  a.ctrl_in = base_ctrl(d, CBX_BUF_DIFF);
+  a.n4 = c->n4;
+  a.alpha = c->model.conf.alpha;  // sma.c:33, theModel's conf
+  a.copies = (float)cp;
+  *copies = cp;
+  return CBX_OK;
+}
+
+cbx::SmaArgs offset_args(const cbx::SmaArgs &a, int64_t start4, int64_t len4) {
+  cbx::SmaArgs b = a;
+  for (int r = 0; r < a.nrep; ++r) {
+    b.s[r] = a.s[r] + start4;
+    b.w[r] = a.w[r] + start4;
+  }
+  b.z = a.z + start4;
+  if (a.last) b.last = a.last + start4;
+  b.acc = a.acc + start4;
+  b.D = a.D + start4;
+  b.n4 = len4;
+  return b;
+}
+
+int sma_step(cbx_context *c, int first) {
+  const bool mom = c->has_last && c->model.conf.momentum > 0;  // sma.c:150 (base conf)
+  std::vector<cbx::SmaArgs> args(c->devs.size());
+  int copies_total = 0;
+  for (size_t k = 0; k < c->devs.size(); ++k) {
+    int cp = 0;
+    TRY(build_args(c, c->devs[k], first, args[k], &cp));
+    copies_total += cp;
+  }
+
+  if (c->G == 1 && c->force_split && c->devs[0].comm == nullptr) {
+    Device &d = c->devs[0];
+    HIP_TRY(hipSetDevice(d.hip_id));
+    int dev = d.hip_id;
+    NCCL_TRY(ncclCommInitAll(&d.comm, 1, &dev));
+  }
+  if (c->G == 1 && !c->force_split) {
+    // Single GPU: Phase B is the identity, so A + C (+ D) fuse into one pass.
+    Device &d = c->devs[0];
+    HIP_TRY(hipSetDevice(d.hip_id));
+    HIP_TRY(hipStreamWaitEvent(d.stream, d.base_updated, 0));  // sma.c:63
+    cbx::LaunchConfig cfg = c->cfg;
+    cfg.num_cus = d.num_cus;
+    TRY(mark(c, d, EV_START));
+    HIP_TRY(cbx::launch_sma_fused(args[0], mom, copies_total > 0, cfg, d.stream));
+    TRY(mark(c, d, EV_A));
+    TRY(mark(c, d, EV_B));
+    ring_advance(c, d, false);
+    c->last_step_split = false;
+  } else {
+    // G > 1: kernel A, grouped RCCL all-reduce of acc (+ control block),
+    // kernel B; optionally per bucket so A(k+1) overlaps all-reduce(k).
+    const int64_t pad = cbx::kPadFloat4;
+    int64_t b4 = c->bucket_elems > 0 ? ((c->bucket_elems / 4 + pad - 1) / pad) * pad : c->n4;
+    if (b4 <= 0 || b4 > c->n4) b4 = c->n4;
+    const int64_t nb = (c->n4 + b4 - 1) / b4;
+    for (size_t k = 0; k < c->devs.size(); ++k) {
+      Device &d = c->devs[k];
+      HIP_TRY(hipSetDevice(d.hip_id));
+      HIP_TRY(hipStreamWaitEvent(d.stream, d.base_updated, 0));
+      TRY(mark(c, d, EV_START));
+    }
+    for (int64_t b = 0; b < nb; ++b) {
+      const int64_t start = b * b4;
+      const int64_t len = std::min(b4, c->n4 - start);
+      for (size_t k = 0; k < c->devs.size(); ++k) {
+        Device &d = c->devs[k];
+        HIP_TRY(hipSetDevice(d.hip_id));
+        cbx::LaunchConfig cfg = c->cfg;
+        cfg.num_cus = d.num_cus;
+        HIP_TRY(cbx::launch_sma_accumulate(offset_args(args[k], start, len), b == 0, cfg, d.stream));
+        if (b == nb - 1) {
+          TRY(mark(c, d, EV_A));
+          HIP_TRY(hipEventRecord(d.accumulated, d.stream));  // sma.c:127
+        }
+      }
+      // common.c:14-54: grouped all-reduce, fp32 sum.  Bucket 0 also carries
+      // the control block that sits right in front of the data.
+      NCCL_TRY(ncclGroupStart());
+      for (size_t k = 0; k < c->devs.size(); ++k) {
+        Device &d = c->devs[k];
+        HIP_TRY(hipSetDevice(d.hip_id));
+        const float *src = base_dev(c, d, CBX_BUF_GRADIENT) + start * 4;
+        float *dst = base_dev(c, d, CBX_BUF_DIFF) + start * 4;
+        size_t count = (size_t)len * 4;
+        if (b == 0) {
+          src -= cbx::kCtrlFloats;
+          dst -= cbx::kCtrlFloats;
+          count += cbx::kCtrlFloats;
+        }
+        NCCL_TRY(ncclAllReduce(src, dst, count, ncclFloat, ncclSum, d.comm, d.stream));
+      }
+      NCCL_TRY(ncclGroupEnd());
+      for (size_t k = 0; k < c->devs.size(); ++k) {
+        Device &d = c->devs[k];
+        HIP_TRY(hipSetDevice(d.hip_id));
+        if (b == nb - 1) TRY(mark(c, d, EV_AR));
+        cbx::LaunchConfig cfg = c->cfg;
+        cfg.num_cus = d.num_cus;
+        HIP_TRY(cbx::launch_sma_apply(offset_args(args[k], start, len), mom, cfg, d.stream));
+      }
+    }
+    for (size_t k = 0; k < c->devs.size(); ++k) {
+      Device &d = c->devs[k];
+      HIP_TRY(hipSetDevice(d.hip_id));
+      TRY(mark(c, d, EV_B));
+      ring_advance(c, d, true);
+    }
+    c->last_step_split = true;
+  }
+
+  // Events the unchanged scheduler waits on: synched / base->updated
+  // (sma.c:177,204) and replica->updated (sma.c:115,222).
+  for (size_t k = 0; k < c->devs.size(); ++k) {
+    Device &d = c->devs[k];
+    HIP_TRY(hipSetDevice(d.hip_id));
+    HIP_TRY(hipEventRecord(d.synched, d.stream));
+    HIP_TRY(hipEventRecord(d.base_updated, d.stream));
+    for (int id : d.replicas) {
+      if (id < first || !c->locked[id]) continue;
+      HIP_TRY(hipEventRecord(c->replicas[id]->updated, d.stream));
+      c->replicas[id]->conf.copy = 0;  // sma.c:220 (a no-op unless a copy happened)
+    }
+  }
+  return CBX_OK;
+}
+
+// ---------------------------------------------------------------------------
+// Checkpoint helpers, databuffer.c:215-259, model.c:396-416
+// ---------------------------------------------------------------------------
+int write_file(const std::string &path, const void *data, size_t bytes) {
+  int fd = open(path.c_str(), O_WRONLY | O_CREAT | O_TRUNC, 0644);
+  if (fd < 0) return fail(CBX_ERR_IO, "failed to open %s: %s", path.c_str(), strerror(errno));
+  size_t done = 0;
+  while (done < bytes) {
+    ssize_t w = write(fd, (const char *)data + done, bytes - done);
+    if (w <= 0) {
+      close(fd);
+      return fail(CBX_ERR_IO, "%zu/%zu bytes written to %s", done, bytes, path.c_str());
+    }
+    done += (size_t)w;
+  }
+  close(fd);
+  return CBX_OK;
+}
+
+int read_file(const std::string &path, void *data, size_t bytes) {
+  int fd = open(path.c_str(), O_RDONLY);
+  if (fd < 0) return fail(CBX_ERR_IO, "failed to open %s: %s", path.c_str(), strerror(errno));
+  size_t done = 0;
+  while (done < bytes) {
+    ssize_t r = read(fd, (char *)data + done, bytes - done);
+    if (r <= 0) {
+      close(fd);
+      return fail(CBX_ERR_IO, "%zu/%zu bytes read from %s", done, bytes, path.c_str());
+    }
+    done += (size_t)r;
+  }
+  close(fd);
+  return CBX_OK;
+}
+
+std::string fmt(const char *f, ...) {
+  char buf[4096];
+  va_list ap;
+  va_start(ap, f);
+  vsnprintf(buf, sizeof(buf), f, ap);
+  va_end(ap);
+  return buf;
+}
+
+int store_buffer(const float *dev, size_t bytes, const std::string &path, std::vector<char> &tmp) {
+  tmp.resize(bytes);
+  HIP_TRY(hipMemcpy(tmp.data(), dev, bytes, hipMemcpyDeviceToHost));
+  return write_file(path, tmp.data(), bytes);
+}
+
+int load_buffer(float *dev, size_t bytes, const std::string &path, std::vector<char> &tmp) {
+  tmp.resize(bytes);
+  TRY(read_file(path, tmp.data(), bytes));
+  HIP_TRY(hipMemcpy(dev, tmp.data(), bytes, hipMemcpyHostToDevice));
+  return CBX_OK;
+}
+
+int alloc_host_mirror(cbx_context *c) {
+  for (Device &d : c->devs) {
+    if (d.host) continue;
+    HIP_TRY(hipSetDevice(d.hip_id));
+    HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&d.host), d.arena_bytes, hipHostMallocDefault));
+    std::memset(d.host, 0, d.arena_bytes);
+  }
+  return CBX_OK;
+}
+
+}  // namespace
+
+// ===========================================================================
+// C-ABI
+// ===========================================================================
+extern "C" {
+
+int cbx_abi_version(void) { return CBX_ABI_VERSION; }
+
+const char *cbx_last_error(void) { return g_last_error.c_str(); }
+
+int cbx_device_count(int *count) {
+  if (!count) return fail(CBX_ERR_INVALID, "null count");
+  return gfx950_device_count(count);
+}
+
+int cbx_init(cbx_context **out, const int *devices, int ndevices) {
+  if (!out || !devices || ndevices <= 0) return fail(CBX_ERR_INVALID, "cbx_init: need at least one device");
+  *out = nullptr;
+  cbx_context *c = new cbx_context();
+  c->G = ndevices;
+  c->devs.resize(ndevices);
+  for (int k = 0; k < ndevices; ++k) {
+    int rc = open_device(c->devs[k], devices[k], k);
+    if (rc < 0) {
+      std::string msg = g_last_error;
+      cbx_free(c);
+      return fail(rc, "%s", msg.c_str());
+    }
+  }
+  if (ndevices > 1) {
+    // executioncontext.c:185-201: ncclCommInitAll over the selected devices;
+    // communicators are indexed by rank (selected-device order).
+    std::vector<ncclComm_t> comms(ndevices);
+    std::vector<int> ids(devices, devices + ndevices);
+    ncclResult_t r = ncclCommInitAll(comms.data(), ndevices, ids.data());
+    if (r != ncclSuccess) {
+      cbx_free(c);
+      return fail(CBX_ERR_RCCL, "ncclCommInitAll: %s", ncclGetErrorString(r));
+    }
+    for (int k = 0; k < ndevices; ++k) c->devs[k].comm = comms[k];
+  }
+  *out = c;
+  return CBX_OK;
+}
+
+int cbx_get_unique_id(unsigned char unique_id[128]) {
+  static_assert(sizeof(ncclUniqueId) == 128, "RCCL unique id size");
+  ncclUniqueId id;
+  NCCL_TRY(ncclGetUniqueId(&id));
+  std::memcpy(unique_id, &id, sizeof(id));
+  return CBX_OK;
+}
+
+int cbx_init_rank(cbx_context **out, int device, int nranks, int rank, const unsigned char unique_id[128]) {
+  if (!out || nranks <= 0 || rank < 0 || rank >= nranks) return fail(CBX_ERR_INVALID, "cbx_init_rank: bad rank");
+  *out = nullptr;
+  cbx_context *c = new cbx_context();
+  c->G = nranks;
+  c->per_rank = true;
+  c->devs.resize(1);
+  int rc = open_device(c->devs[0], device, rank);
+  if (rc < 0) {
+    std::string msg = g_last_error;
+    cbx_free(c);
+    return fail(rc, "%s", msg.c_str());
+  }
+  if (nranks > 1) {
+    if (!unique_id) {
+      cbx_free(c);
+      return fail(CBX_ERR_INVALID, "cbx_init_rank: unique id required for %d ranks", nranks);
+    }
+    ncclUniqueId id;
+    std::memcpy(&id, unique_id, sizeof(id));
+    ncclResult_t r = ncclCommInitRank(&c->devs[0].comm, nranks, id, rank);
+    if (r != ncclSuccess) {
+      cbx_free(c);
+      return fail(CBX_ERR_RCCL, "ncclCommInitRank: %s", ncclGetErrorString(r));
+    }
+  }
+  *out = c;
+  return CBX_OK;
+}
+
+int cbx_free(cbx_context *c) {
+  if (!c) return CBX_OK;
+  for (Device &d : c->devs) close_device(d);
+  for (Replica *r : c->replicas) {
+    if (!r) continue;
+    if (r->updated) (void)hipEventDestroy(r->updated);
+    pthread_mutex_destroy(&r->lock);
+    delete r;
+  }
+  delete c;
+  return CBX_OK;
+}
+
+// ---- model registration ---------------------------------------------------
+int cbx_set_model(cbx_context *c, int variables, int bytes) {
+  TRY(check_ctx(c));
+  if (c->manager) return fail(CBX_ERR_STATE, "model already finalised");
+  if (variables <= 0 || bytes <= 0) return fail(CBX_ERR_INVALID, "setModel(%d, %d)", variables, bytes);
+  c->model = ModelDef();
+  c->model.defined = true;
+  c->model.ops = variables;
+  c->model.bytes = bytes;
+  c->model.count_per_op.assign(variables, 0);
+  c->model.host.assign((size_t)(bytes + 3) / 4, 0.0f);
+  return CBX_OK;
+}
+
+int cbx_set_model_variable(cbx_context *c, int id, int order, int ndims, const int *shape, int capacity) {
+  TRY(check_ctx(c));
+  ModelDef &m = c->model;
+  if (!m.defined) return fail(CBX_ERR_STATE, "setModelVariable before setModel");
+  if (c->manager) return fail(CBX_ERR_STATE, "model already finalised");
+  if (id < 0 || id >= m.ops) return fail(CBX_ERR_INVALID, "variable op %d out of range [0, %d)", id, m.ops);
+  if (ndims < 0 || (ndims > 0 && !shape) || capacity < 0) return fail(CBX_ERR_INVALID, "bad variable shape");
+  // model.c:127-157: the next variable of op `id` must have order count+1.
+  if (order != m.count_per_op[id] + 1)
+    return fail(CBX_ERR_INVALID, "invalid model variable order (ndx=%d, ord=%d)", id, m.count_per_op[id] + 1);
+  int64_t elements = 1;
+  for (int k = 0; k < ndims; ++k) elements *= shape[k];
+  if (m.offset + capacity > m.bytes)
+    return fail(CBX_ERR_INVALID, "variable overflows the model (%lld + %d > %lld)", (long long)m.offset, capacity,
+                (long long)m.bytes);
+  m.vars[{id, order}] = Variable{m.offset, capacity, elements};
+  m.count_per_op[id]++;
+  m.offset += capacity;
+  m.elements += elements;
+  return CBX_OK;
+}
+
+int cbx_set_model_variable_buffer(cbx_context *c, int id, int order, const void *src) {
+  TRY(check_ctx(c));
+  auto it = c->model.vars.find({id, order});
+  if (it == c->model.vars.end()) return fail(CBX_ERR_INVALID, "model variable not found (id %d, order %d)", id, order);
+  if (!src) return fail(CBX_ERR_INVALID, "null variable buffer");
+  // executioncontext.c:1583-1590 -> databuffer.c:80-84: copy into the pinned
+  // host image of theModel; it reaches the device at setModelManager.
+  std::memcpy(reinterpret_cast<char *>(c->model.host.data()) + it->second.offset_bytes, src,
+              (size_t)it->second.bytes);
+  return CBX_OK;
+}
+
+int cbx_set_model_work_per_clock(cbx_context *c, int wpc) {
+  TRY(check_ctx(c));
+  c->model.wpc = wpc;
+  return CBX_OK;
+}
+
+int cbx_set_update_model_type(cbx_context *c, int type) {
+  TRY(check_ctx(c));
+  if (type < 0 || type > 7) return fail(CBX_ERR_INVALID, "Invalid update model type");  // executioncontext.c:1623
+  c->model.type = type;
+  return CBX_OK;
+}
+
+// ---- solver ---------------------------------------------------------------
+int cbx_set_learning_rate_decay_policy_fixed(cbx_context *c, float rate) {
+  TRY(check_ctx(c));
+  c->model.conf.policy = LR_FIXED;
+  c->model.conf.learningRate = rate;
+  return CBX_OK;
+}
+
+int cbx_set_learning_rate_decay_policy_inv(cbx_context *c, float rate, double gamma, double power) {
+  TRY(check_ctx(c));
+  c->model.conf.policy = LR_INV;
+  c->model.conf.learningRate = rate;
+  c->model.conf.gamma = gamma;
+  c->model.conf.power = power;
+  return CBX_OK;
+}
+
+int cbx_set_learning_rate_decay_policy_step(cbx_context *c, float rate, double gamma, int size) {
+  TRY(check_ctx(c));
+  c->model.conf.policy = LR_STEP;
+  c->model.conf.learningRate = rate;
+  c->model.conf.gamma = gamma;
+  c->model.conf.size = size;
+  return CBX_OK;
+}
+
+int cbx_set_learning_rate_decay_policy_multistep(cbx_context *c, float rate, double gamma, int warmuptasks,
+                                                  int nsteps, const int *steps) {
+  TRY(check_ctx(c));
+  if (nsteps < 0 || (nsteps > 0 && !steps)) return fail(CBX_ERR_INVALID, "bad multistep schedule");
+  SolverConf &s = c->model.conf;
+  s.policy = warmuptasks > 0 ? LR_LSR : LR_MULTISTEP;  // executioncontext.c:1690
+  s.learningRate = rate;
+  s.gamma = gamma;
+  s.warmuptasks = warmuptasks;
+  s.steps.assign(steps, steps + nsteps);
+  return CBX_OK;
+}
+
+int cbx_set_learning_rate_decay_policy_exp(cbx_context *c, float rate, double gamma) {
+  TRY(check_ctx(c));
+  c->model.conf.policy = LR_EXP;
+  c->model.conf.learningRate = rate;
+  c->model.conf.gamma = gamma;
+  return CBX_OK;
+}
+
+int cbx_set_base_model_momentum(cbx_context *c, float m) {
+  TRY(check_ctx(c));
+  c->model.conf.baseModelMomentum = m;  // stored, never used natively (sma.c:152)
+  return CBX_OK;
+}
+
+int cbx_set_momentum(cbx_context *c, float m, int method) {
+  TRY(check_ctx(c));
+  if (method != 0 && method != 1) return fail(CBX_ERR_INVALID, "Invalid momentum type");
+  c->model.conf.momentum = m;
+  c->model.conf.momentumMethod = method;
+  return CBX_OK;
+}
+
+int cbx_set_weight_decay(cbx_context *c, float decay) {
+  TRY(check_ctx(c));
+  c->model.conf.weightDecay = decay;
+  return CBX_OK;
+}
+
+int cbx_set_eamsgd_alpha(cbx_context *c, float alpha) {
+  TRY(check_ctx(c));
+  c->model.conf.alpha = alpha;
+  return CBX_OK;
+}
+
+int cbx_set_eamsgd_tau(cbx_context *c, int tau) {
+  TRY(check_ctx(c));
+  c->model.conf.tau = tau;
+  return CBX_OK;
+}
+
+// ---- model manager --------------------------------------------------------
+int cbx_set_model_manager(cbx_context *c, int replicas, int type) {
+  TRY(check_ctx(c));
+  if (c->manager) return fail(CBX_ERR_STATE, "model manager already created");
+  if (!c->model.defined) return fail(CBX_ERR_STATE, "setModelManager before setModel");
+  if (type != CBX_SYNC_BSP && type != CBX_SYNC_SSP && type != CBX_SYNC_ASP)
+    return fail(CBX_ERR_INVALID, "illegal synchronisation type %d", type);
+  if (replicas <= 0) return fail(CBX_ERR_INVALID, "need at least one replica per device");
+  if (replicas > cbx::kMaxReplicas) return fail(CBX_ERR_UNSUPPORTED, "at most %d replicas per device", cbx::kMaxReplicas);
+  ModelDef &m = c->model;
+  if (m.elements <= 0) {
+    // A model registered as raw bytes (no variables): every 4 bytes are a float.
+    m.elements = m.bytes / 4;
+  }
+  if ((int64_t)m.elements * 4 > m.bytes) return fail(CBX_ERR_INVALID, "model elements exceed model bytes");
+
+  c->n = m.elements;
+  const int64_t pad = cbx::kPadFloat4;
+  c->n4 = ((c->n + 3) / 4 + pad - 1) / pad * pad;
+  if (c->n4 * 16 + 4096 >= (int64_t)1 << 32)
+    return fail(CBX_ERR_UNSUPPORTED, "model of %lld elements exceeds the 4 GiB per-buffer kernel offset range",
+                (long long)c->n);
+  // model.c:116-120: `last` exists iff momentum > 0 (theModel's conf).
+  c->has_last = m.conf.momentum > 0;
+  c->R = replicas;
+  c->size = replicas * c->G;
+  c->sync_type = type;
+
+  // Replicas round-robin over devices: replica j*G + g on device g.
+  c->replicas.assign(c->size, nullptr);
+  c->locked.assign(c->size, 0);
+  for (int i = 0; i < c->size; ++i) {
+    Replica *r = new Replica();
+    r->id = i;
+    r->g = i % c->G;
+    r->local = local_of(c, r->g);
+    r->slot = i / c->G;
+    r->conf = m.conf;  // crossbowSolverConfReplicate (model.c:265)
+    pthread_mutex_init(&r->lock, nullptr);
+    c->replicas[i] = r;
+  }
+
+  const size_t data_bytes = (size_t)c->n4 * 16 + (size_t)cbx::kCtrlFloats * sizeof(float);
+  const size_t stride = (data_bytes + kAlign - 1) / kAlign * kAlign;
+  for (Device &d : c->devs) {
+    HIP_TRY(hipSetDevice(d.hip_id));
+    d.stride = stride;
+    d.arena_bytes = stride * (size_t)(kBaseSlots + kReplicaSlots * replicas);
+    hipError_t e = hipMalloc(reinterpret_cast<void **>(&d.arena), d.arena_bytes);
+    if (e != hipSuccess)
+      return fail(CBX_ERR_HIP, "hipMalloc(%zu) for the model arena: %s", d.arena_bytes, hipGetErrorString(e));
+    HIP_TRY(hipMemsetAsync(d.arena, 0, d.arena_bytes, d.stream));
+    d.replicas.clear();
+    for (int i = 0; i < c->size; ++i)
+      if (c->replicas[i]->g == d.g) d.replicas.push_back(i);
+    // executioncontext.c:1741: push theModel's initial values, then every
+    // base model and replica starts as a copy of it (modelmanager.c:28-64).
+    float *z = base_dev(c, d, CBX_BUF_DATA);
+    HIP_TRY(hipMemcpyAsync(z, m.host.data(), (size_t)c->n * 4, hipMemcpyHostToDevice, d.stream));
+    for (int id : d.replicas) {
+      Replica &r = *c->replicas[id];
+      HIP_TRY(hipMemcpyAsync(replica_dev(d, r, CBX_BUF_DATA), z, (size_t)c->n * 4, hipMemcpyDeviceToDevice, d.stream));
+      HIP_TRY(hipEventCreateWithFlags(&r.updated, hipEventDisableTiming));
+    }
+    HIP_TRY(hipEventRecord(d.base_updated, d.stream));
+    HIP_TRY(hipStreamSynchronize(d.stream));
+  }
+  c->manager = true;
+  return CBX_OK;
+}
+
+// ---- barrier path ---------------------------------------------------------
+int cbx_lock_any(cbx_context *c) {
+  TRY(check_manager(c));
+  // modelmanager.c:212-231: trylock every replica this process owns.
+  int count = 0, local = 0;
+  for (int i = 0; i < c->size; ++i) {
+    c->locked[i] = 0;
+    Replica *r = c->replicas[i];
+    if (r->local < 0) continue;
+    ++local;
+    if (pthread_mutex_trylock(&r->lock) == 0) {
+      c->locked[i] = 1;
+      ++count;
+    }
+  }
+  if (c->sync_type == CBX_SYNC_BSP) {
+    // executioncontext.c:2199-2205
+    if (count != local) {
+      for (int i = 0; i < c->size; ++i)
+        if (c->locked[i]) {
+          pthread_mutex_unlock(&c->replicas[i]->lock);
+          c->locked[i] = 0;
+        }
+      return fail(CBX_ERR_BARRIER, "failed to lock all GPU model replicas at synchronisation barrier");
+    }
+    return c->size;
+  }
+  return count;
+}
+
+int cbx_merge(cbx_context *c, int pull, int *first_out) {
+  (void)pull;
+  TRY(check_manager(c));
+  if (!first_out) return fail(CBX_ERR_INVALID, "null merge result");
+  // executioncontext.c:2219-2245
+  int N = 0;
+  for (int i = 0; i < c->size; ++i)
+    if (c->locked[i]) N += c->replicas[i]->updates;
+  *first_out = -1;
+  if (N == 0) return CBX_OK;
+  if (c->size == 1) {
+    *first_out = 0;
+    return CBX_OK;
+  }
+  int first = 0;
+  for (; first < c->size; ++first)
+    if (c->locked[first]) break;
+  *first_out = first;
+  return CBX_OK;
+}
+
+int cbx_synchronise(cbx_context *c, int first, int clock, int autotune, int push) {
+  (void)push;
+  TRY(check_manager(c));
+  if (first < 0 || first > c->size) return fail(CBX_ERR_INVALID, "first replica %d out of range", first);
+  // executioncontext.c:2287-2315: SYNCHRONOUSEAMSGD (3) routes to SMA because
+  // ELASTIC_AVERAGE is #undef'd; SMA is 7.  The other update models are not
+  // this library's path.
+  const int type = c->model.type;
+  if (type != CBX_UPDATE_SMA && type != CBX_UPDATE_SYNCHRONOUSEAMSGD)
+    return fail(CBX_ERR_UNSUPPORTED, "update model %d is not the SMA path", type);
+  TRY(sma_step(c, first));
+  if (autotune < 0) TRY(cbx_del_model(c));
+  if (autotune > 0) TRY(cbx_add_model(c));
+  // modelmanager.c:259-265: clock of every locked replica.
+  for (int i = 0; i < c->size; ++i)
+    if (c->locked[i]) {
+      c->replicas[i]->clock = clock;
+      c->replicas[i]->updates = 0;
+    }
+  return CBX_OK;
+}
+
+int cbx_unlock_any(cbx_context *c) {
+  TRY(check_manager(c));
+  int count = 0;
+  for (int i = 0; i < c->size; ++i)
+    if (c->locked[i]) {
+      pthread_mutex_unlock(&c->replicas[i]->lock);
+      c->locked[i] = 0;
+      ++count;
+    }
+  return count;
+}
+
+// ---- checkpoint -----------------------------------------------------------
+int cbx_checkpoint_model(cbx_context *c, const char *dir) {
+  TRY(check_manager(c));
+  if (!dir) return fail(CBX_ERR_INVALID, "null checkpoint directory");
+  // executioncontext.c:2340-2350: dir/%06llu, a new version per call.
+  std::string path = fmt("%s/%06llu", dir, ++c->version);
+  if (mkdir(path.c_str(), 0777) < 0 && !(c->per_rank && errno == EEXIST))
+    return fail(CBX_ERR_IO, "Failed to create directory %s", path.c_str());
+  TRY(cbx_wait(c));
+  std::vector<char> tmp;
+  const size_t bytes = (size_t)c->n * 4;
+  for (Device &d : c->devs) {
+    HIP_TRY(hipSetDevice(d.hip_id));
+    // modelmanager.c:306-343, model.c:396-405
+    std::string prefix = fmt("%s/gpu-%02d-theModel", path.c_str(), d.g);
+    TRY(store_buffer(base_dev(c, d, CBX_BUF_DATA), bytes, prefix + "-data.dat", tmp));
+    if (c->has_last) TRY(store_buffer(base_dev(c, d, CBX_BUF_LAST), bytes, prefix + "-last.dat", tmp));
+    for (int id : d.replicas) {
+      Replica &r = *c->replicas[id];
+      std::string rp = fmt("%s/gpu-%02d-replica-%03d", path.c_str(), d.g, id);
+      TRY(store_buffer(replica_dev(d, r, CBX_BUF_DATA), bytes, rp + "-data.dat", tmp));
+      if (c->has_last) TRY(store_buffer(replica_dev(d, r, CBX_BUF_LAST), bytes, rp + "-last.dat", tmp));
+    }
+  }
+  return CBX_OK;
+}
+
+int cbx_override_model_data(cbx_context *c, const char *dir) {
+  TRY(check_manager(c));
+  if (!dir) return CBX_OK;  // GPU.c:1169: a null directory is a no-op
+  TRY(cbx_wait(c));
+  std::vector<char> tmp;
+  const size_t bytes = (size_t)c->n * 4;
+  for (Device &d : c->devs) {
+    HIP_TRY(hipSetDevice(d.hip_id));
+    // modelmanager.c:267-304
+    std::string prefix = fmt("%s/gpu-%02d-theModel", dir, d.g);
+    TRY(load_buffer(base_dev(c, d, CBX_BUF_DATA), bytes, prefix + "-data.dat", tmp));
+    if (c->has_last) TRY(load_buffer(base_dev(c, d, CBX_BUF_LAST), bytes, prefix + "-last.dat", tmp));
+    for (int id : d.replicas) {
+      Replica &r = *c->replicas[id];
+      std::string rp = fmt("%s/gpu-%02d-replica-%03d", dir, d.g, id);
+      TRY(load_buffer(replica_dev(d, r, CBX_BUF_DATA), bytes, rp + "-data.dat", tmp));
+      if (c->has_last) TRY(load_buffer(replica_dev(d, r, CBX_BUF_LAST), bytes, rp + "-last.dat", tmp));
+    }
+  }
+  return CBX_OK;
+}
+
+int cbx_add_model(cbx_context *c) {
+  TRY(check_manager(c));
+  return fail(CBX_ERR_UNSUPPORTED, "autotune addModel is not implemented (DESIGN.md, out of scope for round 1)");
+}
+
+int cbx_del_model(cbx_context *c) {
+  TRY(check_manager(c));
+  return fail(CBX_ERR_UNSUPPORTED, "autotune delModel is not implemented (DESIGN.md, out of scope for round 1)");
+}
+
+// ---- task-side replica access ---------------------------------------------
+int cbx_replica_lock(cbx_context *c, int id) {
+  TRY(check_replica(c, id, true));
+  pthread_mutex_lock(&c->replicas[id]->lock);
+  return CBX_OK;
+}
+
+int cbx_replica_unlock(cbx_context *c, int id) {
+  TRY(check_replica(c, id, true));
+  pthread_mutex_unlock(&c->replicas[id]->lock);
+  return CBX_OK;
+}
+
+int cbx_replica_task_done(cbx_context *c, int id) {
+  TRY(check_replica(c, id, true));
+  c->replicas[id]->updates++;
+  return CBX_OK;
+}
+
+int cbx_replica_clock(cbx_context *c, int id) {
+  TRY(check_replica(c, id, false));
+  return c->replicas[id]->clock;
+}
+
+int cbx_replica_learning_rate(cbx_context *c, int id, int task, float *rate) {
+  TRY(check_replica(c, id, false));
+  if (!rate) return fail(CBX_ERR_INVALID, "null rate");
+  return c->replicas[id]->conf.learning_rate(task, rate);
+}
+
+int cbx_replica_get_copy(cbx_context *c, int id) {
+  TRY(check_replica(c, id, false));
+  return (int)c->replicas[id]->conf.copy;
+}
+
+int cbx_replica_set_copy(cbx_context *c, int id, int flag) {
+  TRY(check_replica(c, id, false));
+  c->replicas[id]->conf.copy = flag ? 1u : 0u;
+  return CBX_OK;
+}
+
+int cbx_replica_device(cbx_context *c, int id) {
+  TRY(check_replica(c, id, false));
+  return c->replicas[id]->g;
+}
+
+int cbx_replica_is_local(cbx_context *c, int id) {
+  TRY(check_replica(c, id, false));
+  return c->replicas[id]->local >= 0 ? 1 : 0;
+}
+
+int cbx_num_replicas(cbx_context *c) {
+  TRY(check_manager(c));
+  return c->size;
+}
+
+int cbx_num_devices(cbx_context *c) {
+  TRY(check_ctx(c));
+  return c->G;
+}
+
+int cbx_num_local_devices(cbx_context *c) {
+  TRY(check_ctx(c));
+  return (int)c->devs.size();
+}
+
+int cbx_local_device_index(cbx_context *c, int local) {
+  TRY(check_ctx(c));
+  if (local < 0 || local >= (int)c->devs.size()) return fail(CBX_ERR_INVALID, "local device %d out of range", local);
+  return c->devs[local].g;
+}
+
+long long cbx_model_elements(cbx_context *c) {
+  if (!c) return fail(CBX_ERR_INVALID, "null context");
+  return c->manager ? (long long)c->n : (long long)c->model.elements;
+}
+
+// ---- buffers --------------------------------------------------------------
+static int replica_ptr(cbx_context *c, int id, int kind, float **p, Device **dev) {
+  TRY(check_replica(c, id, true));
+  if (kind < CBX_BUF_DATA || kind > CBX_BUF_LAST) return fail(CBX_ERR_INVALID, "bad buffer kind %d", kind);
+  if (kind == CBX_BUF_LAST && !c->has_last) return fail(CBX_ERR_INVALID, "no momentum buffer (momentum == 0)");
+  Replica &r = *c->replicas[id];
+  Device &d = c->devs[r.local];
+  *p = replica_dev(d, r, kind);
+  if (dev) *dev = &d;
+  return CBX_OK;
+}
+
+static int base_ptr(cbx_context *c, int g, int kind, float **p, Device **dev) {
+  TRY(check_manager(c));
+  if (kind < CBX_BUF_DATA || kind > CBX_BUF_LAST) return fail(CBX_ERR_INVALID, "bad buffer kind %d", kind);
+  if (!base_has(c, kind)) return fail(CBX_ERR_INVALID, "no momentum buffer (momentum == 0)");
+  int k = local_of(c, g);
+  if (k < 0) return fail(CBX_ERR_INVALID, "device %d is not driven by this process", g);
+  *p = base_dev(c, c->devs[k], kind);
+  if (dev) *dev = &c->devs[k];
+  return CBX_OK;
+}
+
+int cbx_replica_buffer(cbx_context *c, int id, int kind, void **dev_ptr) {
+  float *p = nullptr;
+  TRY(replica_ptr(c, id, kind, &p, nullptr));
+  *dev_ptr = p;
+  return CBX_OK;
+}
+
+int cbx_base_buffer(cbx_context *c, int g, int kind, void **dev_ptr) {
+  float *p = nullptr;
+  TRY(base_ptr(c, g, kind, &p, nullptr));
+  *dev_ptr = p;
+  return CBX_OK;
+}
+
+static int copy_io(cbx_context *c, Device *d, void *dst, const void *src, size_t bytes, hipMemcpyKind kind) {
+  if (bytes != (size_t)c->n * 4)
+    return fail(CBX_ERR_INVALID, "buffer is %lld bytes, got %zu", (long long)c->n * 4, bytes);
+  HIP_TRY(hipSetDevice(d->hip_id));
+  HIP_TRY(hipStreamSynchronize(d->stream));
+  HIP_TRY(hipMemcpy(dst, src, bytes, kind));
+  return CBX_OK;
+}
+
+int cbx_replica_write(cbx_context *c, int id, int kind, const void *src, size_t bytes) {
+  float *p = nullptr;
+  Device *d = nullptr;
+  TRY(replica_ptr(c, id, kind, &p, &d));
+  return copy_io(c, d, p, src, bytes, hipMemcpyHostToDevice);
+}
+
+int cbx_replica_read(cbx_context *c, int id, int kind, void *dst, size_t bytes) {
+  float *p = nullptr;
+  Device *d = nullptr;
+  TRY(replica_ptr(c, id, kind, &p, &d));
+  return copy_io(c, d, dst, p, bytes, hipMemcpyDeviceToHost);
+}
+
+int cbx_base_write(cbx_context *c, int g, int kind, const void *src, size_t bytes) {
+  float *p = nullptr;
+  Device *d = nullptr;
+  TRY(base_ptr(c, g, kind, &p, &d));
+  return copy_io(c, d, p, src, bytes, hipMemcpyHostToDevice);
+}
+
+int cbx_base_read(cbx_context *c, int g, int kind, void *dst, size_t bytes) {
+  float *p = nullptr;
+  Device *d = nullptr;
+  TRY(base_ptr(c, g, kind, &p, &d));
+  return copy_io(c, d, dst, p, bytes, hipMemcpyDeviceToHost);
+}
+
+// ---- staging --------------------------------------------------------------
+int cbx_stage_in(cbx_context *c) {
+  TRY(check_manager(c));
+  TRY(alloc_host_mirror(c));
+  const size_t bytes = (size_t)c->n * 4;
+  for (Device &d : c->devs) {
+    HIP_TRY(hipSetDevice(d.hip_id));
+    TRY(mark(c, d, EV_H2D0));
+    HIP_TRY(hipMemcpyAsync(base_dev(c, d, CBX_BUF_DATA), base_host(d, CBX_BUF_DATA), bytes, hipMemcpyHostToDevice, d.stream));
+    if (c->has_last)
+      HIP_TRY(hipMemcpyAsync(base_dev(c, d, CBX_BUF_LAST), base_host(d, CBX_BUF_LAST), bytes, hipMemcpyHostToDevice, d.stream));
+    for (int id : d.replicas) {
+      Replica &r = *c->replicas[id];
+      HIP_TRY(hipMemcpyAsync(replica_dev(d, r, CBX_BUF_DIFF), replica_host(d, r, CBX_BUF_DIFF), bytes, hipMemcpyHostToDevice, d.stream));
+      HIP_TRY(hipMemcpyAsync(replica_dev(d, r, CBX_BUF_DATA), replica_host(d, r, CBX_BUF_DATA), bytes, hipMemcpyHostToDevice, d.stream));
+    }
+    TRY(mark(c, d, EV_H2D1));
+  }
+  return CBX_OK;
+}
+
+int cbx_stage_out(cbx_context *c) {
+  TRY(check_manager(c));
+  TRY(alloc_host_mirror(c));
+  const size_t bytes = (size_t)c->n * 4;
+  for (Device &d : c->devs) {
+    HIP_TRY(hipSetDevice(d.hip_id));
+    TRY(mark(c, d, EV_D2H0));
+    HIP_TRY(hipMemcpyAsync(base_host(d, CBX_BUF_DATA), base_dev(c, d, CBX_BUF_DATA), bytes, hipMemcpyDeviceToHost, d.stream));
+    if (c->has_last)
+      HIP_TRY(hipMemcpyAsync(base_host(d, CBX_BUF_LAST), base_dev(c, d, CBX_BUF_LAST), bytes, hipMemcpyDeviceToHost, d.stream));
+    for (int id : d.replicas) {
+      Replica &r = *c->replicas[id];
+      HIP_TRY(hipMemcpyAsync(replica_host(d, r, CBX_BUF_DATA), replica_dev(d, r, CBX_BUF_DATA), bytes, hipMemcpyDeviceToHost, d.stream));
+    }
+    TRY(mark(c, d, EV_D2H1));
+  }
+  return CBX_OK;
+}
+
+int cbx_replica_host_buffer(cbx_context *c, int id, int kind, void **host_ptr) {
+  float *p = nullptr;
+  TRY(replica_ptr(c, id, kind, &p, nullptr));
+  TRY(alloc_host_mirror(c));
+  Replica &r = *c->replicas[id];
+  *host_ptr = replica_host(c->devs[r.local], r, kind);
+  return CBX_OK;
+}
+
+int cbx_base_host_buffer(cbx_context *c, int g, int kind, void **host_ptr) {
+  float *p = nullptr;
+  Device *d = nullptr;
+  TRY(base_ptr(c, g, kind, &p, &d));
+  TRY(alloc_host_mirror(c));
+  *host_ptr = base_host(*d, kind);
+  return CBX_OK;
+}
+
+int cbx_wait(cbx_context *c) {
+  TRY(check_ctx(c));
+  for (Device &d : c->devs) {
+    HIP_TRY(hipSetDevice(d.hip_id));
+    HIP_TRY(hipStreamSynchronize(d.stream));
+  }
+  return CBX_OK;
+}
+
+// ---- measurement ----------------------------------------------------------
+int cbx_set_timing(cbx_context *c, int enable) {
+  TRY(check_ctx(c));
+  c->timing = enable != 0;
+  for (Device &d : c->devs) {
+    for (int k = 0; k < EV_COUNT; ++k) d.ev_valid[k] = false;
+    d.ring_pos = 0;
+    d.ring_count = 0;
+    if (c->timing && d.ring.empty()) {
+      HIP_TRY(hipSetDevice(d.hip_id));
+      d.ring.resize((size_t)Device::kRing * 4, nullptr);
+      d.ring_split.assign(Device::kRing, 0);
+      for (hipEvent_t &e : d.ring) HIP_TRY(hipEventCreate(&e));
+    }
+  }
+  return CBX_OK;
+}
+
+int cbx_last_timing(cbx_context *c, int local, float *ms) {
+  TRY(check_ctx(c));
+  if (local < 0 || local >= (int)c->devs.size() || !ms) return fail(CBX_ERR_INVALID, "bad timing query");
+  Device &d = c->devs[local];
+  HIP_TRY(hipSetDevice(d.hip_id));
+  for (int k = 0; k < CBX_T_COUNT; ++k) ms[k] = -1.0f;
+  if (d.ring_count > 0) {
+    const int slot = (d.ring_pos + Device::kRing - 1) % Device::kRing;
+    TRY(ring_span(d, slot, EV_START, EV_A, &ms[CBX_T_KERNEL]));
+    if (d.ring_split[slot]) {
+      TRY(ring_span(d, slot, EV_A, EV_AR, &ms[CBX_T_ALLREDUCE]));
+      TRY(ring_span(d, slot, EV_AR, EV_B, &ms[CBX_T_APPLY]));
+    }
+    TRY(ring_span(d, slot, EV_START, EV_B, &ms[CBX_T_STEP]));
+  }
+  auto span = [&](int a, int b, float *out) -> int {
+    if (!d.ev_valid[a] || !d.ev_valid[b]) return CBX_OK;
+    HIP_TRY(hipEventSynchronize(d.ev[b]));
+    HIP_TRY(hipEventElapsedTime(out, d.ev[a], d.ev[b]));
+    return CBX_OK;
+  };
+  TRY(span(EV_H2D0, EV_H2D1, &ms[CBX_T_H2D]));
+  TRY(span(EV_D2H0, EV_D2H1, &ms[CBX_T_D2H]));
+  return CBX_OK;
+}
+
+int cbx_timing_history(cbx_context *c, int local, int which, float *ms, int max) {
+  TRY(check_ctx(c));
+  if (local < 0 || local >= (int)c->devs.size() || !ms || max < 0) return fail(CBX_ERR_INVALID, "bad history query");
+  if (which != CBX_T_KERNEL && which != CBX_T_ALLREDUCE && which != CBX_T_APPLY && which != CBX_T_STEP)
+    return fail(CBX_ERR_INVALID, "history covers kernel / all-reduce / apply / step only");
+  Device &d = c->devs[local];
+  HIP_TRY(hipSetDevice(d.hip_id));
+  const int count = std::min(max, d.ring_count);
+  for (int k = 0; k < count; ++k) {
+    const int slot = (d.ring_pos + Device::kRing - count + k) % Device::kRing;
+    int a = EV_START, b = EV_A;
+    if (which == CBX_T_ALLREDUCE) { a = EV_A; b = EV_AR; }
+    if (which == CBX_T_APPLY) { a = EV_AR; b = EV_B; }
+    if (which == CBX_T_STEP) { a = EV_START; b = EV_B; }
+    if ((which == CBX_T_ALLREDUCE || which == CBX_T_APPLY) && !d.ring_split[slot]) {
+      ms[k] = -1.0f;
+      continue;
+    }
+    TRY(ring_span(d, slot, a, b, &ms[k]));
+  }
+  return count;
+}
+
+int cbx_set_kernel_config(cbx_context *c, int block, int blocks_per_cu, int policy, int unroll) {
+  TRY(check_ctx(c));
+  if (block < 64 || block > 512 || block % 64 != 0) return fail(CBX_ERR_INVALID, "block must be 64..512, multiple of 64");
+  if (unroll != 1 && unroll != 2) return fail(CBX_ERR_INVALID, "unroll must be 1 or 2");
+  if (policy != 0 && policy != 1) return fail(CBX_ERR_INVALID, "policy must be 0 or 1");
+  if (blocks_per_cu < 0) return fail(CBX_ERR_INVALID, "blocks_per_cu must be >= 0");
+  if ((int64_t)block * unroll > cbx::kPadFloat4 || cbx::kPadFloat4 % ((int64_t)block * unroll) != 0)
+    return fail(CBX_ERR_INVALID, "block*unroll must divide %lld", (long long)cbx::kPadFloat4);
+  c->cfg.block = block;
+  c->cfg.blocks_per_cu = blocks_per_cu;
+  c->cfg.policy = policy;
+  c->cfg.unroll = unroll;
+  return CBX_OK;
+}
+
+int cbx_set_bucket_elements(cbx_context *c, long long bucket_elements) {
+  TRY(check_ctx(c));
+  if (bucket_elements < 0) return fail(CBX_ERR_INVALID, "negative bucket size");
+  c->bucket_elems = bucket_elements;
+  return CBX_OK;
+}
+
+int cbx_set_force_split(cbx_context *c, int force) {
+  TRY(check_ctx(c));
+  c->force_split = force != 0;
+  return CBX_OK;
+}
+
+int cbx_fill_synthetic(cbx_context *c, unsigned long long seed) {
+  TRY(check_manager(c));
+  const int64_t n = c->n;
+  for (Device &d : c->devs) {
+    HIP_TRY(hipSetDevice(d.hip_id));
+    // Buffer ids as in oracle/sma_oracle.h: z 0, last 1, s_i 16+2i, w_i 17+2i.
+    float *z = base_dev(c, d, CBX_BUF_DATA);
+    HIP_TRY(cbx::launch_fill_normal(z, n, seed ^ 0ULL, 0.05f, nullptr, d.stream));
+    if (c->has_last) HIP_TRY(cbx::launch_fill_normal(base_dev(c, d, CBX_BUF_LAST), n, seed ^ 1ULL, 0.001f, nullptr, d.stream));
+    for (int id : d.replicas) {
+      Replica &r = *c->replicas[id];
+      float *s = replica_dev(d, r, CBX_BUF_DIFF);
+      HIP_TRY(cbx::launch_fill_normal(s, n, seed ^ (unsigned long long)(16 + 2 * id), 0.01f, z, d.stream));
+      HIP_TRY(cbx::launch_fill_normal(replica_dev(d, r, CBX_BUF_DATA), n, seed ^ (unsigned long long)(17 + 2 * id),
+                                      0.001f, s, d.stream));
+    }
+    HIP_TRY(hipStreamSynchronize(d.stream));
+  }
+  return CBX_OK;
+}
+
+int cbx_bench_copy(cbx_context *c, size_t bytes, int iters, float *gbps) {
+  TRY(check_ctx(c));
+  if (!gbps || iters <= 0 || bytes < 16) return fail(CBX_ERR_INVALID, "bad copy benchmark arguments");
+  Device &d = c->devs[0];
+  HIP_TRY(hipSetDevice(d.hip_id));
+  const int64_t n4 = (int64_t)(bytes / 16);
+  cbx::v4f *a = nullptr, *b = nullptr;
+  HIP_TRY(hipMalloc(reinterpret_cast<void **>(&a), (size_t)n4 * 16));
+  hipError_t e = hipMalloc(reinterpret_cast<void **>(&b), (size_t)n4 * 16);
+  if (e != hipSuccess) {
+    (void)hipFree(a);
+    return fail(CBX_ERR_HIP, "hipMalloc: %s", hipGetErrorString(e));
+  }
+  cbx::LaunchConfig cfg = c->cfg;
+  cfg.num_cus = d.num_cus;
+  int rc = CBX_OK;
+  float ms = 0.0f;
+  do {
+    if (hipMemsetAsync(a, 0, (size_t)n4 * 16, d.stream) != hipSuccess) { rc = fail(CBX_ERR_HIP, "memset"); break; }
+    for (int k = 0; k < 3 && rc == CBX_OK; ++k)
+      if (cbx::launch_copy(b, a, n4, cfg, d.stream) != hipSuccess) rc = fail(CBX_ERR_HIP, "copy launch");
+    if (rc != CBX_OK) break;
+    if (hipEventRecord(d.ev[EV_H2D0], d.stream) != hipSuccess) { rc = fail(CBX_ERR_HIP, "event"); break; }
+    for (int k = 0; k < iters && rc == CBX_OK; ++k) {
+      hipError_t le = (k & 1) ? cbx::launch_copy(a, b, n4, cfg, d.stream) : cbx::launch_copy(b, a, n4, cfg, d.stream);
+      if (le != hipSuccess) rc = fail(CBX_ERR_HIP, "copy launch: %s", hipGetErrorString(le));
+    }
+    if (rc != CBX_OK) break;
+    if (hipEventRecord(d.ev[EV_H2D1], d.stream) != hipSuccess) { rc = fail(CBX_ERR_HIP, "event"); break; }
+    if (hipEventSynchronize(d.ev[EV_H2D1]) != hipSuccess) { rc = fail(CBX_ERR_HIP, "sync"); break; }
+    if (hipEventElapsedTime(&ms, d.ev[EV_H2D0], d.ev[EV_H2D1]) != hipSuccess) { rc = fail(CBX_ERR_HIP, "elapsed"); break; }
+    *gbps = (float)(2.0 * (double)n4 * 16.0 * iters / (ms * 1e-3) / 1e9);
+  } while (0);
+  d.ev_valid[EV_H2D0] = d.ev_valid[EV_H2D1] = false;
+  (void)hipFree(a);
+  (void)hipFree(b);
+  return rc;
+}
+
+}  // extern "C"

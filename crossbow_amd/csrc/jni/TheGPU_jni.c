@@ -1,0 +1,191 @@
+/*
+ * TheGPU_jni.c -- JNI shim exporting Crossbow's TheGPU model-path natives on
+ * top of libcrossbow_sma.so.  Built by crossbow_amd/build.py only where a JDK
+ * provides jni.h (none in this image).
+ *
+ * Signatures follow clib-multigpu/uk_ac_imperial_lsds_crossbow_device_TheGPU.h
+ * (e.g. synchronise (IIIZ)I at :636-640).  Like the reference (static theGPU,
+ * GPU.c:12) the context is process-global, and like the reference every
+ * failure prints to stderr and exits (debug.h:37-57).
+ */
+#include <jni.h>
+
+#include <stdio.h>
+#include <stdlib.h>
+
+#include "crossbow_sma.h"
+
+static cbx_context *theGPU = NULL;
+
+static jint fatal_or (int rc) {
+	if (rc < 0) {
+		fprintf (stderr, "error: %s\n", cbx_last_error ());
+		exit (1);
+	}
+	return (jint) rc;
+}
+
+#define NATIVE(ret, name) JNIEXPORT ret JNICALL Java_uk_ac_imperial_lsds_crossbow_device_TheGPU_##name
+
+/* GPU.c:21-63.  Thread-count / core-offset arguments configure the reference's
+ * task and callback handler threads, which are not on this path. */
+NATIVE(jint, init) (JNIEnv *env, jobject obj, jintArray devices, jint streams, jint callbacks,
+		jint tasks, jint cboffset, jint tkoffset) {
+	(void) obj; (void) streams; (void) callbacks; (void) tasks; (void) cboffset; (void) tkoffset;
+	if (theGPU) {
+		fprintf (stderr, "error: GPU execution context already initialised\n");
+		exit (1);
+	}
+	jsize argc = (*env)->GetArrayLength (env, devices);
+	jint *argv = (*env)->GetIntArrayElements (env, devices, 0);
+	int rc = cbx_init (&theGPU, (const int *) argv, (int) argc);
+	(*env)->ReleaseIntArrayElements (env, devices, argv, JNI_ABORT);
+	return fatal_or (rc);
+}
+
+NATIVE(jint, free) (JNIEnv *env, jobject obj) {
+	(void) env; (void) obj;
+	int rc = cbx_free (theGPU);
+	theGPU = NULL;
+	return fatal_or (rc);
+}
+
+NATIVE(jint, setModel) (JNIEnv *env, jobject obj, jint variables, jint size) {
+	(void) env; (void) obj;
+	return fatal_or (cbx_set_model (theGPU, variables, size));
+}
+
+NATIVE(jint, setModelVariable) (JNIEnv *env, jobject obj, jint id, jint order, jintArray dims, jint capacity) {
+	(void) obj;
+	jsize argc = (*env)->GetArrayLength (env, dims);
+	jint *argv = (*env)->GetIntArrayElements (env, dims, 0);
+	int rc = cbx_set_model_variable (theGPU, id, order, (int) argc, (const int *) argv, capacity);
+	(*env)->ReleaseIntArrayElements (env, dims, argv, JNI_ABORT);
+	return fatal_or (rc);
+}
+
+NATIVE(jint, setModelVariableBuffer) (JNIEnv *env, jobject obj, jint id, jint order, jobject buffer) {
+	(void) obj;
+	return fatal_or (cbx_set_model_variable_buffer (theGPU, id, order, (*env)->GetDirectBufferAddress (env, buffer)));
+}
+
+NATIVE(jint, setModelWorkPerClock) (JNIEnv *env, jobject obj, jint wpc) {
+	(void) env; (void) obj;
+	return fatal_or (cbx_set_model_work_per_clock (theGPU, wpc));
+}
+
+NATIVE(jint, setUpdateModelType) (JNIEnv *env, jobject obj, jint type) {
+	(void) env; (void) obj;
+	return fatal_or (cbx_set_update_model_type (theGPU, type));
+}
+
+NATIVE(jint, setLearningRateDecayPolicyFixed) (JNIEnv *env, jobject obj, jfloat rate) {
+	(void) env; (void) obj;
+	return fatal_or (cbx_set_learning_rate_decay_policy_fixed (theGPU, rate));
+}
+
+NATIVE(jint, setLearningRateDecayPolicyInv) (JNIEnv *env, jobject obj, jfloat rate, jdouble gamma, jdouble power) {
+	(void) env; (void) obj;
+	return fatal_or (cbx_set_learning_rate_decay_policy_inv (theGPU, rate, gamma, power));
+}
+
+NATIVE(jint, setLearningRateDecayPolicyStep) (JNIEnv *env, jobject obj, jfloat rate, jdouble gamma, jint size) {
+	(void) env; (void) obj;
+	return fatal_or (cbx_set_learning_rate_decay_policy_step (theGPU, rate, gamma, size));
+}
+
+NATIVE(jint, setLearningRateDecayPolicyMultiStep) (JNIEnv *env, jobject obj, jfloat rate, jdouble gamma,
+		jint warmup, jintArray steps) {
+	(void) obj;
+	jsize argc = (*env)->GetArrayLength (env, steps);
+	jint *argv = (*env)->GetIntArrayElements (env, steps, 0);
+	int rc = cbx_set_learning_rate_decay_policy_multistep (theGPU, rate, gamma, warmup, (int) argc, (const int *) argv);
+	(*env)->ReleaseIntArrayElements (env, steps, argv, JNI_ABORT);
+	return fatal_or (rc);
+}
+
+NATIVE(jint, setLearningRateDecayPolicyExp) (JNIEnv *env, jobject obj, jfloat rate, jdouble gamma) {
+	(void) env; (void) obj;
+	return fatal_or (cbx_set_learning_rate_decay_policy_exp (theGPU, rate, gamma));
+}
+
+NATIVE(jint, setBaseModelMomentum) (JNIEnv *env, jobject obj, jfloat momentum) {
+	(void) env; (void) obj;
+	return fatal_or (cbx_set_base_model_momentum (theGPU, momentum));
+}
+
+NATIVE(jint, setMomentum) (JNIEnv *env, jobject obj, jfloat momentum, jint method) {
+	(void) env; (void) obj;
+	return fatal_or (cbx_set_momentum (theGPU, momentum, method));
+}
+
+NATIVE(jint, setWeightDecay) (JNIEnv *env, jobject obj, jfloat decay) {
+	(void) env; (void) obj;
+	return fatal_or (cbx_set_weight_decay (theGPU, decay));
+}
+
+NATIVE(jint, setEamsgdAlpha) (JNIEnv *env, jobject obj, jfloat alpha) {
+	(void) env; (void) obj;
+	return fatal_or (cbx_set_eamsgd_alpha (theGPU, alpha));
+}
+
+NATIVE(jint, setEamsgdTau) (JNIEnv *env, jobject obj, jint tau) {
+	(void) env; (void) obj;
+	return fatal_or (cbx_set_eamsgd_tau (theGPU, tau));
+}
+
+NATIVE(jint, setModelManager) (JNIEnv *env, jobject obj, jint replicas, jint type) {
+	(void) env; (void) obj;
+	return fatal_or (cbx_set_model_manager (theGPU, replicas, type));
+}
+
+/* GPU.c:1113-1120; executioncontext.c:2199-2205 exits when BSP cannot lock all. */
+NATIVE(jint, lockAny) (JNIEnv *env, jobject obj) {
+	(void) env; (void) obj;
+	return fatal_or (cbx_lock_any (theGPU));
+}
+
+NATIVE(jint, merge) (JNIEnv *env, jobject obj, jboolean pull) {
+	(void) env; (void) obj;
+	int first = -1;
+	fatal_or (cbx_merge (theGPU, pull == JNI_TRUE ? 1 : 0, &first));
+	return (jint) first;
+}
+
+NATIVE(jint, synchronise) (JNIEnv *env, jobject obj, jint first, jint clock, jint autotune, jboolean push) {
+	(void) env; (void) obj;
+	return fatal_or (cbx_synchronise (theGPU, first, clock, autotune, push == JNI_TRUE ? 1 : 0));
+}
+
+NATIVE(jint, unlockAny) (JNIEnv *env, jobject obj) {
+	(void) env; (void) obj;
+	return fatal_or (cbx_unlock_any (theGPU));
+}
+
+NATIVE(jint, checkpointModel) (JNIEnv *env, jobject obj, jstring dir) {
+	(void) obj;
+	const char *path = (*env)->GetStringUTFChars (env, dir, NULL);
+	int rc = cbx_checkpoint_model (theGPU, path);
+	(*env)->ReleaseStringUTFChars (env, dir, path);
+	return fatal_or (rc);
+}
+
+NATIVE(jint, overrideModelData) (JNIEnv *env, jobject obj, jstring dir) {
+	(void) obj;
+	if ((*env)->IsSameObject (env, dir, NULL))
+		return 0; /* GPU.c:1169 */
+	const char *path = (*env)->GetStringUTFChars (env, dir, NULL);
+	int rc = cbx_override_model_data (theGPU, path);
+	(*env)->ReleaseStringUTFChars (env, dir, path);
+	return fatal_or (rc);
+}
+
+NATIVE(jint, addModel) (JNIEnv *env, jobject obj) {
+	(void) env; (void) obj;
+	return fatal_or (cbx_add_model (theGPU));
+}
+
+NATIVE(jint, delModel) (JNIEnv *env, jobject obj) {
+	(void) env; (void) obj;
+	return fatal_or (cbx_del_model (theGPU));
+}

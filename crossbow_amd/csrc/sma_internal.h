@@ -1,0 +1,73 @@
+// sma_internal.h -- kernel arguments and launchers shared by the SMA kernels
+// (sma_kernels.hip) and the execution context (context.hip).  Not part of the
+// C-ABI; see include/crossbow_sma.h for that.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+namespace cbx {
+
+// Replicas per device handled by one launch (kernarg holds 2 pointers each).
+constexpr int kMaxReplicas = 64;
+// Unrolled (register-resident) replica chunk inside the kernels.
+constexpr int kChunk = 8;
+// Base-model momentum, hard-coded at clib-multigpu/synch/sma.c:152.
+constexpr float kBaseMomentum = 0.9f;
+
+typedef float v4f __attribute__((ext_vector_type(4)));
+
+// One kernel argument block for every SMA kernel.  All buffers are fp32
+// arrays of n4 float4s (the flat model buffer, clib-multigpu/model.c:127-157,
+// padded to a multiple of kPadFloat4; the pad is zero and stays zero).  The
+// acc / D buffers are preceded by a 256-byte control block whose first float
+// counts this device's Phase-D copy requests; it is summed by the all-reduce
+// together with the first bucket, so kernel B learns "copy on any device"
+// without a host round trip.
+struct SmaArgs {
+  const v4f *s[kMaxReplicas];  // replica snapshots   (replica->diff)
+  v4f *w[kMaxReplicas];        // replica parameters  (replica->data)
+  v4f *z;                      // base model          (base->data)
+  v4f *last;                   // base momentum       (base->last), may be null
+  v4f *acc;                    // Phase A output      (base->gradient)
+  const v4f *D;                // Phase B output      (base->diff)
+  float *ctrl_out;             // acc control block   (kernel A writes)
+  const float *ctrl_in;        // D control block     (kernel B reads)
+  int64_t n4;                  // float4s in the launch's range (multiple of kPadFloat4)
+  float alpha;                 // conf->alpha (sma.c:33)
+  float copies;                // Phase D requests on this device (kernel A)
+  int nrep;                    // locked replicas on this device, id order
+  int pad_;
+};
+
+// Buffers are padded to this many float4s so every trip of every kernel is
+// full (block * unroll <= 1024) and no bounds checks sit in the inner loop.
+constexpr int64_t kPadFloat4 = 1024;
+// Control block in front of acc / D, in floats (256 bytes keeps data aligned).
+constexpr int64_t kCtrlFloats = 64;
+
+struct LaunchConfig {
+  int block = 256;         // threads per workgroup
+  int blocks_per_cu = 0;   // 0: one trip per thread; >0: grid-stride, this many WGs per CU
+  int policy = 1;          // 0 plain, 1 nontemporal global loads/stores
+  int unroll = 1;          // float4s per thread per trip (1 or 2)
+  int num_cus = 256;
+};
+
+// Fused 1-GPU step: Phase A + (identity) B + C (+ D when copy).
+hipError_t launch_sma_fused(const SmaArgs &a, bool momentum, bool copy,
+                            const LaunchConfig &cfg, hipStream_t stream);
+// Multi-GPU kernel A: Phase A only, writes acc and the control slot.
+hipError_t launch_sma_accumulate(const SmaArgs &a, bool write_ctrl,
+                                 const LaunchConfig &cfg, hipStream_t stream);
+// Multi-GPU kernel B: Phase C (+ D, gated by the reduced control slot).
+hipError_t launch_sma_apply(const SmaArgs &a, bool momentum,
+                            const LaunchConfig &cfg, hipStream_t stream);
+// Synthetic normal fill.
+hipError_t launch_fill_normal(float *out, int64_t n, uint64_t seed, float sigma,
+                              const float *mean, hipStream_t stream);
+// Float4 copy used to measure the HBM ceiling on the box.
+hipError_t launch_copy(v4f *dst, const v4f *src, int64_t n4, const LaunchConfig &cfg,
+                       hipStream_t stream);
+
+}  // namespace cbx

@@ -1,0 +1,385 @@
+// sma_kernels.hip -- HIP kernels of the SMA step for CDNA4 (gfx950).
+//
+// The reference runs the step as 3R+3 cuBLAS saxpy calls, R+4 copies/memsets
+// and 3 host-blocking syncs per GPU (clib-multigpu/synch/sma.c:13-231), moving
+// (44R+48)n bytes.  Here one streaming pass reads every input once and writes
+// every output once:
+//
+//   fused (1 GPU)     reads z, last, s_i, w_i  writes w_i, z, last   (12R+8+8m)n B
+//   accumulate (A)    reads z, s_i, w_i        writes w_i, acc       (12R+8)n B
+//   apply (B)         reads D, z, last         writes z, last (, w)  (12+8m)n B
+//
+// The work is an fp32 AXPY/reduce at ~0.1 flop/byte: HBM-bound, no MFMA.  Each
+// lane moves 16-byte float4s (1 KiB per wave instruction), every load of a trip
+// is issued before the first arithmetic, and the per-replica partial sum stays
+// in registers -- no LDS is needed because no element is re-read.
+//
+// Arithmetic is the reference's, bit for bit: cuBLAS saxpy y := fma(a, x, y)
+// in fp32 and the same operation order, so 1-GPU results equal the oracle's.
+#include "sma_internal.h"
+
+namespace cbx {
+namespace {
+
+template <int P>
+__device__ __forceinline__ v4f ld(const v4f *p) {
+  if constexpr (P == 1) {
+    return __builtin_nontemporal_load(p);
+  } else {
+    return *p;
+  }
+}
+
+template <int P>
+__device__ __forceinline__ void st(v4f *p, v4f v) {
+  if constexpr (P == 1) {
+    __builtin_nontemporal_store(v, p);
+  } else {
+    *p = v;
+  }
+}
+
+// Uniform (SGPR) base + 32-bit lane byte offset: lets the compiler use the
+// global_load/store "saddr + voffset" form, one VGPR per address instead of a
+// 64-bit pair per stream (18+ streams per lane at R = 8).
+template <int P>
+__device__ __forceinline__ v4f ldo(const v4f *base, uint32_t off) {
+  return ld<P>(reinterpret_cast<const v4f *>(reinterpret_cast<const char *>(base) + off));
+}
+
+template <int P>
+__device__ __forceinline__ void sto(v4f *base, uint32_t off, v4f v) {
+  st<P>(reinterpret_cast<v4f *>(reinterpret_cast<char *>(base) + off), v);
+}
+
+__device__ __forceinline__ v4f vfma(v4f a, v4f b, v4f c) {
+  return __builtin_elementwise_fma(a, b, c);
+}
+
+// ---------------------------------------------------------------------------
+// Fused 1-GPU step.  R >= 0 replicas fully unrolled (R <= kChunk); R == -1
+// takes a.nrep and walks the replicas in register-resident chunks of kChunk.
+// Per element (sma.c):
+//   d   = fma(-1, z, s_i)              :79-90
+//   w_i = fma(-alpha, d, w_i)          :93-99
+//   acc = fma(+alpha, d, acc)          :102-107   (acc starts at +0, :66)
+//   D   = acc                          common.c:3-57 with one rank
+//   D   = fma(0.9, last, D); last = D  :148-166 (if momentum > 0)
+//   z   = fma(1, D, z)                 :168-174
+//   w_i = z                            :185-227 (if any replica asked to copy)
+// ---------------------------------------------------------------------------
+template <int R, bool MOM, bool COPY, int P, int U>
+__global__ __launch_bounds__(512) void sma_fused_kernel(const SmaArgs a) {
+  constexpr int RR = (R > 0) ? R : kChunk;
+  const uint32_t trip = gridDim.x * blockDim.x * U;
+  const uint32_t n4 = (uint32_t)a.n4;
+  const v4f al = a.alpha;
+  const v4f nal = -a.alpha;
+  const v4f mb = kBaseMomentum;
+  const v4f one = 1.0f;
+  const v4f mone = -1.0f;
+  for (uint32_t base = blockIdx.x * blockDim.x * U + threadIdx.x; base < n4; base += trip) {
+    v4f zv[U], lv[U], acc[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t i = (base + u * blockDim.x) * 16u;
+      zv[u] = ldo<P>(a.z, i);
+      if constexpr (MOM) lv[u] = ldo<P>(a.last, i);
+      acc[u] = 0.0f;
+    }
+    const int nrep = (R >= 0) ? R : a.nrep;
+    for (int c = 0; c < nrep; c += RR) {
+      v4f sv[U][RR], wv[U][RR];
+#pragma unroll
+      for (int r = 0; r < RR; ++r) {
+        if (R < 0 && c + r >= nrep) break;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const uint32_t i = (base + u * blockDim.x) * 16u;
+          sv[u][r] = ldo<P>(a.s[c + r], i);
+          if constexpr (!COPY) wv[u][r] = ldo<P>(a.w[c + r], i);
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < RR; ++r) {
+        if (R < 0 && c + r >= nrep) break;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const v4f d = vfma(mone, zv[u], sv[u][r]);
+          if constexpr (!COPY) wv[u][r] = vfma(nal, d, wv[u][r]);
+          acc[u] = vfma(al, d, acc[u]);
+        }
+      }
+      if constexpr (!COPY) {
+#pragma unroll
+        for (int r = 0; r < RR; ++r) {
+          if (R < 0 && c + r >= nrep) break;
+#pragma unroll
+          for (int u = 0; u < U; ++u) sto<P>(a.w[c + r], (base + u * blockDim.x) * 16u, wv[u][r]);
+        }
+      }
+      if constexpr (R >= 0) break;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t i = (base + u * blockDim.x) * 16u;
+      v4f D = acc[u];
+      if constexpr (MOM) {
+        D = vfma(mb, lv[u], D);
+        sto<P>(a.last, i, D);
+      }
+      zv[u] = vfma(one, D, zv[u]);
+      sto<P>(a.z, i, zv[u]);
+    }
+    if constexpr (COPY) {
+      for (int r = 0; r < nrep; ++r) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) sto<P>(a.w[r], (base + u * blockDim.x) * 16u, zv[u]);
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Kernel A (G > 1): Phase A on this device's locked replicas -> acc.
+// ---------------------------------------------------------------------------
+template <int R, int P, int U>
+__global__ __launch_bounds__(512) void sma_accumulate_kernel(const SmaArgs a) {
+  constexpr int RR = (R > 0) ? R : kChunk;
+  if (a.ctrl_out != nullptr && blockIdx.x == 0 && threadIdx.x < kCtrlFloats)
+    a.ctrl_out[threadIdx.x] = (threadIdx.x == 0) ? a.copies : 0.0f;
+  const uint32_t trip = gridDim.x * blockDim.x * U;
+  const uint32_t n4 = (uint32_t)a.n4;
+  const v4f al = a.alpha;
+  const v4f nal = -a.alpha;
+  const v4f mone = -1.0f;
+  for (uint32_t base = blockIdx.x * blockDim.x * U + threadIdx.x; base < n4; base += trip) {
+    v4f zv[U], acc[U];
+    const int nrep = (R >= 0) ? R : a.nrep;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      acc[u] = 0.0f;
+      if (nrep > 0) zv[u] = ldo<P>(a.z, (base + u * blockDim.x) * 16u);
+    }
+    for (int c = 0; c < nrep; c += RR) {
+      v4f sv[U][RR], wv[U][RR];
+#pragma unroll
+      for (int r = 0; r < RR; ++r) {
+        if (R < 0 && c + r >= nrep) break;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const uint32_t i = (base + u * blockDim.x) * 16u;
+          sv[u][r] = ldo<P>(a.s[c + r], i);
+          wv[u][r] = ldo<P>(a.w[c + r], i);
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < RR; ++r) {
+        if (R < 0 && c + r >= nrep) break;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const v4f d = vfma(mone, zv[u], sv[u][r]);
+          wv[u][r] = vfma(nal, d, wv[u][r]);
+          acc[u] = vfma(al, d, acc[u]);
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < RR; ++r) {
+        if (R < 0 && c + r >= nrep) break;
+#pragma unroll
+        for (int u = 0; u < U; ++u) sto<P>(a.w[c + r], (base + u * blockDim.x) * 16u, wv[u][r]);
+      }
+      if constexpr (R >= 0) break;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) sto<P>(a.acc, (base + u * blockDim.x) * 16u, acc[u]);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Kernel B (G > 1): Phase C on the all-reduced D, then Phase D when the
+// reduced control block says any device had a copy request.
+// ---------------------------------------------------------------------------
+template <bool MOM, int P, int U>
+__global__ __launch_bounds__(512) void sma_apply_kernel(const SmaArgs a) {
+  const bool copy = a.ctrl_in[0] > 0.0f;
+  const uint32_t trip = gridDim.x * blockDim.x * U;
+  const uint32_t n4 = (uint32_t)a.n4;
+  const v4f mb = kBaseMomentum;
+  const v4f one = 1.0f;
+  for (uint32_t base = blockIdx.x * blockDim.x * U + threadIdx.x; base < n4; base += trip) {
+    v4f Dv[U], zv[U], lv[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t i = (base + u * blockDim.x) * 16u;
+      Dv[u] = ldo<P>(a.D, i);
+      zv[u] = ldo<P>(a.z, i);
+      if constexpr (MOM) lv[u] = ldo<P>(a.last, i);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t i = (base + u * blockDim.x) * 16u;
+      if constexpr (MOM) {
+        Dv[u] = vfma(mb, lv[u], Dv[u]);
+        sto<P>(a.last, i, Dv[u]);
+      }
+      zv[u] = vfma(one, Dv[u], zv[u]);
+      sto<P>(a.z, i, zv[u]);
+    }
+    if (copy) {
+      for (int r = 0; r < a.nrep; ++r) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) sto<P>(a.w[r], (base + u * blockDim.x) * 16u, zv[u]);
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Synthetic inputs: splitmix64 -> Box-Muller in double.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
+  uint64_t z = x + 0x9E3779B97F4A7C15ULL;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+  return z ^ (z >> 31);
+}
+
+__global__ __launch_bounds__(256) void fill_normal_kernel(float *out, int64_t n, uint64_t seed, float sigma,
+                                                          const float *mean) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += stride) {
+    const uint64_t x = splitmix64(seed + (uint64_t)(2 * k) * 0x9E3779B97F4A7C15ULL);
+    const uint64_t y = splitmix64(seed + (uint64_t)(2 * k + 1) * 0x9E3779B97F4A7C15ULL);
+    const double u1 = (double)((x >> 11) + 1) * (1.0 / 9007199254740992.0);
+    const double u2 = (double)(y >> 11) * (1.0 / 9007199254740992.0);
+    const float v = (float)((double)sigma * (sqrt(-2.0 * log(u1)) * cos(6.283185307179586 * u2)));
+    out[k] = mean ? (mean[k] + v) : v;
+  }
+}
+
+template <int P>
+__global__ __launch_bounds__(512) void copy_kernel(v4f *dst, const v4f *src, int64_t n4) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) st<P>(dst + i, ld<P>(src + i));
+}
+
+// Grid for a range of n4 float4s (a multiple of block*unroll).
+inline dim3 grid_for(int64_t n4, const LaunchConfig &cfg) {
+  const int64_t per_block = (int64_t)cfg.block * cfg.unroll;
+  int64_t blocks = (n4 + per_block - 1) / per_block;
+  if (cfg.blocks_per_cu > 0) {
+    const int64_t cap = (int64_t)cfg.num_cus * cfg.blocks_per_cu;
+    if (blocks > cap) blocks = cap;
+  }
+  if (blocks < 1) blocks = 1;
+  return dim3((unsigned)blocks);
+}
+
+template <int R, bool MOM, bool COPY, int P>
+hipError_t fused_u(const SmaArgs &a, const LaunchConfig &cfg, hipStream_t s) {
+  const dim3 g = grid_for(a.n4, cfg);
+  if (cfg.unroll == 2)
+    hipLaunchKernelGGL((sma_fused_kernel<R, MOM, COPY, P, 2>), g, dim3(cfg.block), 0, s, a);
+  else
+    hipLaunchKernelGGL((sma_fused_kernel<R, MOM, COPY, P, 1>), g, dim3(cfg.block), 0, s, a);
+  return hipGetLastError();
+}
+
+template <bool MOM, bool COPY, int P>
+hipError_t fused_r(const SmaArgs &a, const LaunchConfig &cfg, hipStream_t s) {
+  switch (a.nrep) {
+    case 0: return fused_u<0, MOM, COPY, P>(a, cfg, s);
+    case 1: return fused_u<1, MOM, COPY, P>(a, cfg, s);
+    case 2: return fused_u<2, MOM, COPY, P>(a, cfg, s);
+    case 3: return fused_u<3, MOM, COPY, P>(a, cfg, s);
+    case 4: return fused_u<4, MOM, COPY, P>(a, cfg, s);
+    case 5: return fused_u<5, MOM, COPY, P>(a, cfg, s);
+    case 6: return fused_u<6, MOM, COPY, P>(a, cfg, s);
+    case 7: return fused_u<7, MOM, COPY, P>(a, cfg, s);
+    case 8: return fused_u<8, MOM, COPY, P>(a, cfg, s);
+    default: return fused_u<-1, MOM, COPY, P>(a, cfg, s);
+  }
+}
+
+template <int R, int P>
+hipError_t acc_u(const SmaArgs &a, const LaunchConfig &cfg, hipStream_t s) {
+  const dim3 g = grid_for(a.n4, cfg);
+  if (cfg.unroll == 2)
+    hipLaunchKernelGGL((sma_accumulate_kernel<R, P, 2>), g, dim3(cfg.block), 0, s, a);
+  else
+    hipLaunchKernelGGL((sma_accumulate_kernel<R, P, 1>), g, dim3(cfg.block), 0, s, a);
+  return hipGetLastError();
+}
+
+template <int P>
+hipError_t acc_r(const SmaArgs &a, const LaunchConfig &cfg, hipStream_t s) {
+  switch (a.nrep) {
+    case 0: return acc_u<0, P>(a, cfg, s);
+    case 1: return acc_u<1, P>(a, cfg, s);
+    case 2: return acc_u<2, P>(a, cfg, s);
+    case 3: return acc_u<3, P>(a, cfg, s);
+    case 4: return acc_u<4, P>(a, cfg, s);
+    case 5: return acc_u<5, P>(a, cfg, s);
+    case 6: return acc_u<6, P>(a, cfg, s);
+    case 7: return acc_u<7, P>(a, cfg, s);
+    case 8: return acc_u<8, P>(a, cfg, s);
+    default: return acc_u<-1, P>(a, cfg, s);
+  }
+}
+
+template <bool MOM, int P>
+hipError_t apply_u(const SmaArgs &a, const LaunchConfig &cfg, hipStream_t s) {
+  const dim3 g = grid_for(a.n4, cfg);
+  if (cfg.unroll == 2)
+    hipLaunchKernelGGL((sma_apply_kernel<MOM, P, 2>), g, dim3(cfg.block), 0, s, a);
+  else
+    hipLaunchKernelGGL((sma_apply_kernel<MOM, P, 1>), g, dim3(cfg.block), 0, s, a);
+  return hipGetLastError();
+}
+
+}  // namespace
+
+hipError_t launch_sma_fused(const SmaArgs &a, bool momentum, bool copy, const LaunchConfig &cfg,
+                            hipStream_t stream) {
+  if (cfg.policy == 1) {
+    if (momentum) return copy ? fused_r<true, true, 1>(a, cfg, stream) : fused_r<true, false, 1>(a, cfg, stream);
+    return copy ? fused_r<false, true, 1>(a, cfg, stream) : fused_r<false, false, 1>(a, cfg, stream);
+  }
+  if (momentum) return copy ? fused_r<true, true, 0>(a, cfg, stream) : fused_r<true, false, 0>(a, cfg, stream);
+  return copy ? fused_r<false, true, 0>(a, cfg, stream) : fused_r<false, false, 0>(a, cfg, stream);
+}
+
+hipError_t launch_sma_accumulate(const SmaArgs &a, bool write_ctrl, const LaunchConfig &cfg,
+                                 hipStream_t stream) {
+  SmaArgs b = a;
+  if (!write_ctrl) b.ctrl_out = nullptr;
+  return cfg.policy == 1 ? acc_r<1>(b, cfg, stream) : acc_r<0>(b, cfg, stream);
+}
+
+hipError_t launch_sma_apply(const SmaArgs &a, bool momentum, const LaunchConfig &cfg, hipStream_t stream) {
+  if (cfg.policy == 1) return momentum ? apply_u<true, 1>(a, cfg, stream) : apply_u<false, 1>(a, cfg, stream);
+  return momentum ? apply_u<true, 0>(a, cfg, stream) : apply_u<false, 0>(a, cfg, stream);
+}
+
+hipError_t launch_fill_normal(float *out, int64_t n, uint64_t seed, float sigma, const float *mean,
+                              hipStream_t stream) {
+  int64_t blocks = (n + 255) / 256;
+  if (blocks > 8192) blocks = 8192;
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL(fill_normal_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, out, n, seed, sigma, mean);
+  return hipGetLastError();
+}
+
+hipError_t launch_copy(v4f *dst, const v4f *src, int64_t n4, const LaunchConfig &cfg, hipStream_t stream) {
+  LaunchConfig c = cfg;
+  c.unroll = 1;
+  const dim3 g = grid_for(n4, c);
+  if (cfg.policy == 1)
+    hipLaunchKernelGGL((copy_kernel<1>), g, dim3(c.block), 0, stream, dst, src, n4);
+  else
+    hipLaunchKernelGGL((copy_kernel<0>), g, dim3(c.block), 0, stream, dst, src, n4);
+  return hipGetLastError();
+}
+
+}  // namespace cbx

@@ -1,0 +1,270 @@
+"""Python mirror of Crossbow's ``TheGPU`` model-path natives.
+
+Same method names, argument meaning and call order as
+``src/main/java/uk/ac/imperial/lsds/crossbow/device/TheGPU.java:268-354``,
+bound to ``libcrossbow_sma.so`` through its C-ABI (include/crossbow_sma.h)
+instead of JNI.  Where the reference would print and ``exit(1)``
+(clib-multigpu/debug.h:37-57) these methods raise :class:`CbxError`.
+
+Extra helpers (snake_case) expose what the Java side reaches only through
+other natives: buffer upload/download, pinned staging and timing.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Iterable, Optional, Sequence
+
+import numpy as np
+
+from . import _lib
+from ._lib import CbxError, check  # noqa: F401
+
+
+def _ptr(a: np.ndarray) -> ctypes.c_void_p:
+    return ctypes.c_void_p(a.ctypes.data)
+
+
+class TheGPU:
+    """One execution context (the reference's process-global ``theGPU``)."""
+
+    def __init__(self):
+        self._L = _lib.load()
+        self._ctx = ctypes.c_void_p()
+
+    # ---- lifecycle ------------------------------------------------------
+    @staticmethod
+    def device_count() -> int:
+        n = ctypes.c_int(0)
+        check(_lib.load().cbx_device_count(ctypes.byref(n)))
+        return n.value
+
+    def init(self, devices: Sequence[int]) -> int:
+        """TheGPU.init (GPU.c:21-63): one process drives ``devices``."""
+        arr = (ctypes.c_int * len(devices))(*devices)
+        return check(self._L.cbx_init(ctypes.byref(self._ctx), arr, len(devices)))
+
+    @staticmethod
+    def unique_id() -> bytes:
+        buf = (ctypes.c_ubyte * 128)()
+        check(_lib.load().cbx_get_unique_id(buf))
+        return bytes(buf)
+
+    def init_rank(self, device: int, nranks: int, rank: int, unique_id: Optional[bytes]) -> int:
+        """One process per GPU: rank ``rank`` of ``nranks`` drives ``device``."""
+        uid = None
+        if unique_id is not None:
+            uid = (ctypes.c_ubyte * 128).from_buffer_copy(unique_id)
+        return check(self._L.cbx_init_rank(ctypes.byref(self._ctx), device, nranks, rank, uid))
+
+    def free(self) -> int:
+        if self._ctx:
+            rc = self._L.cbx_free(self._ctx)
+            self._ctx = ctypes.c_void_p()
+            return check(rc)
+        return 0
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.free()
+
+    @property
+    def ctx(self):
+        return self._ctx
+
+    # ---- model registration (Model.GPURegister, Model.java:338-371) -------
+    def setModel(self, variables: int, size: int) -> int:
+        return check(self._L.cbx_set_model(self._ctx, variables, size))
+
+    def setModelVariable(self, id: int, order: int, shape: Sequence[int], capacity: int) -> int:
+        arr = (ctypes.c_int * max(1, len(shape)))(*shape)
+        return check(self._L.cbx_set_model_variable(self._ctx, id, order, len(shape), arr, capacity))
+
+    def setModelVariableBuffer(self, id: int, order: int, buffer) -> int:
+        a = np.ascontiguousarray(np.frombuffer(memoryview(buffer), dtype=np.uint8))
+        return check(self._L.cbx_set_model_variable_buffer(self._ctx, id, order, _ptr(a)))
+
+    def setModelWorkPerClock(self, wpc: int) -> int:
+        return check(self._L.cbx_set_model_work_per_clock(self._ctx, wpc))
+
+    def setUpdateModelType(self, type: int) -> int:
+        return check(self._L.cbx_set_update_model_type(self._ctx, type))
+
+    # ---- solver (SolverConf.GPURegister, SolverConf.java:355-409) ----------
+    def setLearningRateDecayPolicyFixed(self, rate: float) -> int:
+        return check(self._L.cbx_set_learning_rate_decay_policy_fixed(self._ctx, rate))
+
+    def setLearningRateDecayPolicyInv(self, rate: float, gamma: float, power: float) -> int:
+        return check(self._L.cbx_set_learning_rate_decay_policy_inv(self._ctx, rate, gamma, power))
+
+    def setLearningRateDecayPolicyStep(self, rate: float, gamma: float, step: int) -> int:
+        return check(self._L.cbx_set_learning_rate_decay_policy_step(self._ctx, rate, gamma, step))
+
+    def setLearningRateDecayPolicyMultiStep(self, rate: float, gamma: float, warmup: int, steps: Sequence[int]) -> int:
+        arr = (ctypes.c_int * max(1, len(steps)))(*steps)
+        return check(self._L.cbx_set_learning_rate_decay_policy_multistep(self._ctx, rate, gamma, warmup,
+                                                                           len(steps), arr))
+
+    def setLearningRateDecayPolicyExp(self, rate: float, gamma: float) -> int:
+        return check(self._L.cbx_set_learning_rate_decay_policy_exp(self._ctx, rate, gamma))
+
+    def setBaseModelMomentum(self, momentum: float) -> int:
+        return check(self._L.cbx_set_base_model_momentum(self._ctx, momentum))
+
+    def setMomentum(self, momentum: float, method: int = 0) -> int:
+        return check(self._L.cbx_set_momentum(self._ctx, momentum, method))
+
+    def setWeightDecay(self, decay: float) -> int:
+        return check(self._L.cbx_set_weight_decay(self._ctx, decay))
+
+    def setEamsgdAlpha(self, alpha: float) -> int:
+        return check(self._L.cbx_set_eamsgd_alpha(self._ctx, alpha))
+
+    def setEamsgdTau(self, tau: int) -> int:
+        return check(self._L.cbx_set_eamsgd_tau(self._ctx, tau))
+
+    # ---- model manager / barrier path -------------------------------------
+    def setModelManager(self, size: int, type: int) -> int:
+        return check(self._L.cbx_set_model_manager(self._ctx, size, type))
+
+    def lockAny(self) -> int:
+        return check(self._L.cbx_lock_any(self._ctx))
+
+    def merge(self, pull: bool) -> int:
+        first = ctypes.c_int(-1)
+        check(self._L.cbx_merge(self._ctx, 1 if pull else 0, ctypes.byref(first)))
+        return first.value
+
+    def synchronise(self, first: int, clock: int, autotune: int, push: bool) -> int:
+        return check(self._L.cbx_synchronise(self._ctx, first, clock, autotune, 1 if push else 0))
+
+    def unlockAny(self) -> int:
+        return check(self._L.cbx_unlock_any(self._ctx))
+
+    def checkpointModel(self, directory: str) -> int:
+        return check(self._L.cbx_checkpoint_model(self._ctx, directory.encode()))
+
+    def overrideModelData(self, directory: Optional[str]) -> int:
+        return check(self._L.cbx_override_model_data(self._ctx, directory.encode() if directory else None))
+
+    def addModel(self) -> int:
+        return check(self._L.cbx_add_model(self._ctx))
+
+    def delModel(self) -> int:
+        return check(self._L.cbx_del_model(self._ctx))
+
+    # ---- task-side replica access -----------------------------------------
+    def replica_lock(self, id: int) -> None:
+        check(self._L.cbx_replica_lock(self._ctx, id))
+
+    def replica_unlock(self, id: int) -> None:
+        check(self._L.cbx_replica_unlock(self._ctx, id))
+
+    def replica_task_done(self, id: int) -> None:
+        check(self._L.cbx_replica_task_done(self._ctx, id))
+
+    def replica_clock(self, id: int) -> int:
+        return check(self._L.cbx_replica_clock(self._ctx, id))
+
+    def replica_learning_rate(self, id: int, task: int) -> float:
+        r = ctypes.c_float(0.0)
+        check(self._L.cbx_replica_learning_rate(self._ctx, id, task, ctypes.byref(r)))
+        return r.value
+
+    def replica_copy(self, id: int) -> int:
+        return check(self._L.cbx_replica_get_copy(self._ctx, id))
+
+    def set_replica_copy(self, id: int, flag: bool) -> None:
+        check(self._L.cbx_replica_set_copy(self._ctx, id, 1 if flag else 0))
+
+    def replica_device(self, id: int) -> int:
+        return check(self._L.cbx_replica_device(self._ctx, id))
+
+    def replica_is_local(self, id: int) -> bool:
+        return bool(check(self._L.cbx_replica_is_local(self._ctx, id)))
+
+    def num_replicas(self) -> int:
+        return check(self._L.cbx_num_replicas(self._ctx))
+
+    def num_devices(self) -> int:
+        return check(self._L.cbx_num_devices(self._ctx))
+
+    def local_devices(self) -> Iterable[int]:
+        k = check(self._L.cbx_num_local_devices(self._ctx))
+        return [check(self._L.cbx_local_device_index(self._ctx, j)) for j in range(k)]
+
+    def elements(self) -> int:
+        return check(self._L.cbx_model_elements(self._ctx))
+
+    def local_replicas(self) -> Sequence[int]:
+        return [i for i in range(self.num_replicas()) if self.replica_is_local(i)]
+
+    # ---- buffers -----------------------------------------------------------
+    def replica_write(self, id: int, kind: int, values: np.ndarray) -> None:
+        a = np.ascontiguousarray(values, dtype=np.float32)
+        check(self._L.cbx_replica_write(self._ctx, id, kind, _ptr(a), a.nbytes))
+
+    def replica_read(self, id: int, kind: int) -> np.ndarray:
+        a = np.empty(self.elements(), dtype=np.float32)
+        check(self._L.cbx_replica_read(self._ctx, id, kind, _ptr(a), a.nbytes))
+        return a
+
+    def base_write(self, device: int, kind: int, values: np.ndarray) -> None:
+        a = np.ascontiguousarray(values, dtype=np.float32)
+        check(self._L.cbx_base_write(self._ctx, device, kind, _ptr(a), a.nbytes))
+
+    def base_read(self, device: int, kind: int) -> np.ndarray:
+        a = np.empty(self.elements(), dtype=np.float32)
+        check(self._L.cbx_base_read(self._ctx, device, kind, _ptr(a), a.nbytes))
+        return a
+
+    def replica_host_view(self, id: int, kind: int) -> np.ndarray:
+        p = ctypes.c_void_p()
+        check(self._L.cbx_replica_host_buffer(self._ctx, id, kind, ctypes.byref(p)))
+        return np.ctypeslib.as_array(ctypes.cast(p, ctypes.POINTER(ctypes.c_float)), shape=(self.elements(),))
+
+    def base_host_view(self, device: int, kind: int) -> np.ndarray:
+        p = ctypes.c_void_p()
+        check(self._L.cbx_base_host_buffer(self._ctx, device, kind, ctypes.byref(p)))
+        return np.ctypeslib.as_array(ctypes.cast(p, ctypes.POINTER(ctypes.c_float)), shape=(self.elements(),))
+
+    def stage_in(self) -> None:
+        check(self._L.cbx_stage_in(self._ctx))
+
+    def stage_out(self) -> None:
+        check(self._L.cbx_stage_out(self._ctx))
+
+    def wait(self) -> None:
+        check(self._L.cbx_wait(self._ctx))
+
+    # ---- measurement -------------------------------------------------------
+    def set_timing(self, enable: bool) -> None:
+        check(self._L.cbx_set_timing(self._ctx, 1 if enable else 0))
+
+    def last_timing(self, local: int = 0) -> np.ndarray:
+        ms = (ctypes.c_float * _lib.T_COUNT)()
+        check(self._L.cbx_last_timing(self._ctx, local, ms))
+        return np.array(ms[:], dtype=np.float64)
+
+    def timing_history(self, which: int = _lib.T_KERNEL, local: int = 0, max_steps: int = 1024) -> np.ndarray:
+        ms = (ctypes.c_float * max_steps)()
+        k = check(self._L.cbx_timing_history(self._ctx, local, which, ms, max_steps))
+        return np.array(ms[:k], dtype=np.float64)
+
+    def set_kernel_config(self, block: int = 256, blocks_per_cu: int = 0, policy: int = 1, unroll: int = 1) -> None:
+        check(self._L.cbx_set_kernel_config(self._ctx, block, blocks_per_cu, policy, unroll))
+
+    def set_bucket_elements(self, elements: int) -> None:
+        check(self._L.cbx_set_bucket_elements(self._ctx, elements))
+
+    def set_force_split(self, force: bool) -> None:
+        check(self._L.cbx_set_force_split(self._ctx, 1 if force else 0))
+
+    def fill_synthetic(self, seed: int) -> None:
+        check(self._L.cbx_fill_synthetic(self._ctx, seed))
+
+    def bench_copy(self, nbytes: int, iters: int) -> float:
+        g = ctypes.c_float(0.0)
+        check(self._L.cbx_bench_copy(self._ctx, nbytes, iters, ctypes.byref(g)))
+        return g.value

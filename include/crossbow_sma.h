@@ -1,0 +1,216 @@
+/*
+ * crossbow_sma.h -- C-ABI of the MI355X-native synchronous model averaging
+ * (SMA) path of Crossbow.  Library: crossbow_amd/libcrossbow_sma.so
+ * (hipcc, gfx950).  Plain C types only; no HIP or torch types cross it.
+ *
+ * The entry points are the ones Crossbow's JNI glue binds for the model path
+ * (clib-multigpu/GPU.c, header clib-multigpu/uk_ac_imperial_lsds_crossbow_device_TheGPU.h).
+ * Each declaration cites the JNI native it replaces.  The reference keeps a
+ * process-global context (static theGPU, GPU.c:12); this ABI passes it as an
+ * explicit handle and the JNI shim (crossbow_amd/csrc/jni/) keeps the global.
+ *
+ * Error behaviour: the reference prints and exit(1)s on every failure
+ * (clib-multigpu/debug.h:37-57).  Here every function returns a status
+ * (CBX_OK or a negative CBX_ERR_*), cbx_last_error() holds the message, and
+ * the JNI shim restores "fatal = process exit".  Functions documented as
+ * returning a count return it when >= 0.
+ */
+#ifndef CROSSBOW_SMA_H_
+#define CROSSBOW_SMA_H_
+
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CBX_ABI_VERSION 1
+
+#define CBX_OK               0
+#define CBX_ERR_INVALID     -1  /* bad argument                                   */
+#define CBX_ERR_STATE       -2  /* call out of order (e.g. sync before manager)   */
+#define CBX_ERR_HIP         -3  /* HIP runtime failure                            */
+#define CBX_ERR_RCCL        -4  /* RCCL failure                                   */
+#define CBX_ERR_IO          -5  /* checkpoint file I/O                            */
+#define CBX_ERR_NO_DEVICE   -6  /* no usable MI355X (gfx950) device               */
+#define CBX_ERR_BARRIER     -7  /* BSP barrier could not lock every replica       */
+#define CBX_ERR_UNSUPPORTED -8  /* outside this library's scope   */
+
+/* Update model ids, uk/ac/imperial/lsds/crossbow/types/UpdateModel.java:5 */
+#define CBX_UPDATE_SYNCHRONOUSEAMSGD 3   /* routed to SMA: clib-multigpu/utils.h:56-57 */
+#define CBX_UPDATE_SMA               7
+
+/* Synchronisation models, types/SynchronisationModel.java:5 */
+#define CBX_SYNC_BSP 0
+#define CBX_SYNC_SSP 1
+#define CBX_SYNC_ASP 2
+
+/* Per-model buffers, clib-multigpu/model.h:22-87 */
+#define CBX_BUF_DATA     0   /* base: z ; replica: w                    */
+#define CBX_BUF_GRADIENT 1   /* base: acc (Phase A output)              */
+#define CBX_BUF_DIFF     2   /* base: D (all-reduced) ; replica: s      */
+#define CBX_BUF_LAST     3   /* momentum buffer; exists iff momentum>0  */
+
+typedef struct cbx_context cbx_context;
+
+int         cbx_abi_version (void);
+const char *cbx_last_error (void);
+/* Number of visible gfx950 devices (0 on a host without one). */
+int         cbx_device_count (int *count);
+
+/* ---- execution context ------------------------------------------------ */
+/* TheGPU.init([I...)  GPU.c:21-63 -> executioncontext.c:152-345.
+ * One process drives `ndevices` local GPUs; RCCL comms via ncclCommInitAll
+ * (executioncontext.c:185-201), indexed by rank, not device id.          */
+int cbx_init (cbx_context **ctx, const int *devices, int ndevices);
+/* One process per GPU (torch.distributed launch): rank r of n drives one
+ * device; `unique_id` (128 bytes) comes from cbx_get_unique_id on rank 0. */
+int cbx_get_unique_id (unsigned char unique_id[128]);
+int cbx_init_rank (cbx_context **ctx, int device, int nranks, int rank,
+		const unsigned char unique_id[128]);
+/* TheGPU.free()  GPU.c:65-75 -> executioncontext.c:728-898 */
+int cbx_free (cbx_context *ctx);
+
+/* ---- model registration (Model.GPURegister, Model.java:338-371) ------- */
+/* TheGPU.setModel(II)                      GPU.c:672-681  */
+int cbx_set_model (cbx_context *ctx, int variables, int bytes);
+/* TheGPU.setModelVariable(II[II)           GPU.c:683-696  */
+int cbx_set_model_variable (cbx_context *ctx, int id, int order, int ndims,
+		const int *shape, int capacity);
+/* TheGPU.setModelVariableBuffer(IILjava/nio/ByteBuffer;)  GPU.c:698-708 */
+int cbx_set_model_variable_buffer (cbx_context *ctx, int id, int order, const void *src);
+/* TheGPU.setModelWorkPerClock(I)           GPU.c:721-730  */
+int cbx_set_model_work_per_clock (cbx_context *ctx, int wpc);
+/* TheGPU.setUpdateModelType(I)             GPU.c:732-741; 3 and 7 accepted */
+int cbx_set_update_model_type (cbx_context *ctx, int type);
+
+/* ---- solver (SolverConf.GPURegister, SolverConf.java:355-409) --------- */
+/* TheGPU.setLearningRateDecayPolicy*  GPU.c:743-821 */
+int cbx_set_learning_rate_decay_policy_fixed (cbx_context *ctx, float rate);
+int cbx_set_learning_rate_decay_policy_inv (cbx_context *ctx, float rate, double gamma, double power);
+int cbx_set_learning_rate_decay_policy_step (cbx_context *ctx, float rate, double gamma, int size);
+int cbx_set_learning_rate_decay_policy_multistep (cbx_context *ctx, float rate, double gamma,
+		int warmuptasks, int nsteps, const int *steps);
+int cbx_set_learning_rate_decay_policy_exp (cbx_context *ctx, float rate, double gamma);
+/* TheGPU.setBaseModelMomentum(F)  GPU.c:823-832 (stored, unused: sma.c:152) */
+int cbx_set_base_model_momentum (cbx_context *ctx, float momentum);
+/* TheGPU.setMomentum(FI)          GPU.c:834-843 */
+int cbx_set_momentum (cbx_context *ctx, float momentum, int method);
+/* TheGPU.setWeightDecay(F)        GPU.c:845-854 */
+int cbx_set_weight_decay (cbx_context *ctx, float decay);
+/* TheGPU.setEamsgdAlpha(F)        GPU.c:856-865 */
+int cbx_set_eamsgd_alpha (cbx_context *ctx, float alpha);
+/* TheGPU.setEamsgdTau(I)          GPU.c:867-876 */
+int cbx_set_eamsgd_tau (cbx_context *ctx, int tau);
+
+/* ---- model manager ---------------------------------------------------- */
+/* TheGPU.setModelManager(II)  GPU.c:878-886 -> executioncontext.c:1720-1764:
+ * finalise, push theModel, one base model per GPU, `replicas` per GPU placed
+ * round-robin (replica j*G+d on device d, modelmanager.c:51-64).           */
+int cbx_set_model_manager (cbx_context *ctx, int replicas, int type);
+
+/* ---- the barrier path (ModelManager.trySynchronise, ModelManager.java:293-353) */
+/* TheGPU.lockAny()   GPU.c:1113-1120 -> executioncontext.c:2197-2211.
+ * Returns the locked count (BSP: the replica count, or CBX_ERR_BARRIER).  */
+int cbx_lock_any (cbx_context *ctx);
+/* TheGPU.merge(Z)    GPU.c:1122-1131 -> executioncontext.c:2219-2245.
+ * *first = first locked replica id, or -1 when no locked replica has an
+ * update (the JNI return value).                                          */
+int cbx_merge (cbx_context *ctx, int pull, int *first);
+/* TheGPU.synchronise(IIIZ)  GPU.c:1133-1140 -> executioncontext.c:2262-2334
+ * -> synch/sma.c:233-248.  Enqueues the SMA step on each device's model
+ * synchronisation stream and returns without blocking the host.          */
+int cbx_synchronise (cbx_context *ctx, int first, int clock, int autotune, int push);
+/* TheGPU.unlockAny() GPU.c:1142-1149 -> modelmanager.c:233-245           */
+int cbx_unlock_any (cbx_context *ctx);
+
+/* ---- checkpoint / resume ---------------------------------------------- */
+/* TheGPU.checkpointModel(String)   GPU.c:1151-1163 -> executioncontext.c:2340-2367 */
+int cbx_checkpoint_model (cbx_context *ctx, const char *dir);
+/* TheGPU.overrideModelData(String) GPU.c:1165-1176 -> executioncontext.c:2369-2388 */
+int cbx_override_model_data (cbx_context *ctx, const char *dir);
+/* TheGPU.addModel() / delModel()   GPU.c:1178-1199 (autotune)            */
+int cbx_add_model (cbx_context *ctx);
+int cbx_del_model (cbx_context *ctx);
+
+/* ---- task-side replica access (modelmanager.c:147-204) ---------------- */
+int cbx_replica_lock (cbx_context *ctx, int id);       /* crossbowModelManagerGet   */
+int cbx_replica_unlock (cbx_context *ctx, int id);     /* crossbowModelManagerRelease */
+int cbx_replica_task_done (cbx_context *ctx, int id);  /* callbackhandler.c:149-165: updates++ */
+int cbx_replica_clock (cbx_context *ctx, int id);
+/* crossbowSolverConfGetLearningRate (solverconfiguration.c:116-162) on the
+ * replica's own configuration: may raise its _copy flag (LR drop).        */
+int cbx_replica_learning_rate (cbx_context *ctx, int id, int task, float *rate);
+int cbx_replica_get_copy (cbx_context *ctx, int id);
+int cbx_replica_set_copy (cbx_context *ctx, int id, int flag);
+/* Global device index a replica lives on (id % G). */
+int cbx_replica_device (cbx_context *ctx, int id);
+/* 1 if the replica lives in this process. */
+int cbx_replica_is_local (cbx_context *ctx, int id);
+
+int cbx_num_replicas (cbx_context *ctx);       /* R * G (modelmanager->size) */
+int cbx_num_devices (cbx_context *ctx);        /* G, all ranks               */
+int cbx_num_local_devices (cbx_context *ctx);
+int cbx_local_device_index (cbx_context *ctx, int local); /* global index    */
+long long cbx_model_elements (cbx_context *ctx);
+
+/* ---- buffers ---------------------------------------------------------- */
+/* Device pointers (for the task-side kernels that produce w and s).       */
+int cbx_replica_buffer (cbx_context *ctx, int id, int kind, void **dev_ptr);
+int cbx_base_buffer (cbx_context *ctx, int device, int kind, void **dev_ptr);
+/* Blocking copies of a whole buffer (model->bytes) to/from host memory.   */
+int cbx_replica_write (cbx_context *ctx, int id, int kind, const void *src, size_t bytes);
+int cbx_replica_read (cbx_context *ctx, int id, int kind, void *dst, size_t bytes);
+int cbx_base_write (cbx_context *ctx, int device, int kind, const void *src, size_t bytes);
+int cbx_base_read (cbx_context *ctx, int device, int kind, void *dst, size_t bytes);
+
+/* Pinned-host staging of the synchronisation buffers (databuffer.c:95-122).
+ * stage_in pushes z, last, s_i, w_i; stage_out pulls z, last, w_i.  Async on
+ * the sync stream(s); host views are the pinned mirrors below.            */
+int cbx_stage_in (cbx_context *ctx);
+int cbx_stage_out (cbx_context *ctx);
+int cbx_replica_host_buffer (cbx_context *ctx, int id, int kind, void **host_ptr);
+int cbx_base_host_buffer (cbx_context *ctx, int device, int kind, void **host_ptr);
+/* Block until every local sync stream has drained. */
+int cbx_wait (cbx_context *ctx);
+
+/* ---- measurement ------------------------------------------------------ */
+#define CBX_T_KERNEL    0   /* fused kernel, or kernel A (G > 1)       */
+#define CBX_T_ALLREDUCE 1   /* RCCL all-reduce (G > 1)                 */
+#define CBX_T_APPLY     2   /* kernel B (G > 1)                        */
+#define CBX_T_STEP      3   /* whole synchronise() on the device       */
+#define CBX_T_H2D       4   /* last cbx_stage_in                       */
+#define CBX_T_D2H       5   /* last cbx_stage_out                      */
+#define CBX_T_COUNT     6
+/* When enabled, HIP events bracket each launch on the sync stream.       */
+int cbx_set_timing (cbx_context *ctx, int enable);
+/* Milliseconds of the last step on local device `local`, CBX_T_COUNT floats
+ * (blocks on the recorded events).                                        */
+int cbx_last_timing (cbx_context *ctx, int local, float *ms);
+/* Per-launch history of the last steps (up to 1024) on local device `local`:
+ * `which` is CBX_T_KERNEL, CBX_T_ALLREDUCE, CBX_T_APPLY or CBX_T_STEP; fills
+ * ms[0..count) oldest first and returns count.                             */
+int cbx_timing_history (cbx_context *ctx, int local, int which, float *ms, int max);
+/* Launch geometry for the SMA kernels: threads per block (multiple of 64),
+ * workgroups per CU for the grid-stride loop (0 = one float4 per thread),
+ * load/store policy (0 plain, 1 nontemporal), float4s per thread per trip. */
+int cbx_set_kernel_config (cbx_context *ctx, int block, int blocks_per_cu, int policy, int unroll);
+/* Bucketed pipeline for G > 1: kernel A / all-reduce / kernel B per bucket
+ * of `bucket_elements` floats (0 = one bucket).                           */
+int cbx_set_bucket_elements (cbx_context *ctx, long long bucket_elements);
+/* Force the multi-GPU pipeline (kernel A + RCCL all-reduce + kernel B) even
+ * at G = 1 (a one-rank communicator), so a single-GPU host exercises it.  */
+int cbx_set_force_split (cbx_context *ctx, int force);
+/* Synthetic inputs of BASELINE.md 2.3, generated on the device:
+ * z ~ N(0,.05^2), s_i = z + N(0,.01^2), w_i = s_i + N(0,.001^2),
+ * last ~ N(0,.001^2); seeds derive from `seed` ^ buffer id.               */
+int cbx_fill_synthetic (cbx_context *ctx, unsigned long long seed);
+/* Float4 device-to-device copy ceiling on local device 0: `bytes` per
+ * buffer, `iters` timed launches; writes achieved GB/s (read + write).    */
+int cbx_bench_copy (cbx_context *ctx, size_t bytes, int iters, float *gbps);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* CROSSBOW_SMA_H_ */

@@ -1,0 +1,283 @@
+/*
+ * sma_oracle.c -- CPU restatement of Crossbow's SMA step.
+ *
+ * TEST INFRASTRUCTURE ONLY (see sma_oracle.h).  Imported by tests/, by
+ * __graft_entry__.smoke() as the checker, and by bench.py's cpu_baseline leg.
+ * The product library (crossbow_amd/csrc) never links or calls this file.
+ *
+ * Every function cites the reference lines it restates.  Arithmetic follows
+ * cuBLAS saxpy semantics y := fma(a, x, y) in float32 (one rounding per
+ * element), in the reference's operation order.
+ */
+#define _GNU_SOURCE
+#include "sma_oracle.h"
+
+#include <dlfcn.h>
+#include <math.h>
+#include <sched.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+#include <unistd.h>
+
+/* ---------------------------------------------------------------------- */
+/* PRNG: splitmix64 (one step from state x) and Box-Muller in double.      */
+/* ---------------------------------------------------------------------- */
+#define CBO_GOLDEN 0x9E3779B97F4A7C15ULL
+
+uint64_t cbo_splitmix64 (uint64_t x) {
+	uint64_t z = x + CBO_GOLDEN;
+	z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+	z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+	return z ^ (z >> 31);
+}
+
+static inline double cbo_normal (uint64_t seed, uint64_t k) {
+	uint64_t a = cbo_splitmix64 (seed + (2 * k) * CBO_GOLDEN);
+	uint64_t b = cbo_splitmix64 (seed + (2 * k + 1) * CBO_GOLDEN);
+	double u1 = ((double) ((a >> 11) + 1)) * (1.0 / 9007199254740992.0); /* (0, 1] */
+	double u2 = ((double) (b >> 11)) * (1.0 / 9007199254740992.0);       /* [0, 1) */
+	return sqrt (-2.0 * log (u1)) * cos (6.283185307179586 * u2);
+}
+
+void cbo_fill_normal (float *out, size_t n, uint64_t seed, float sigma, const float *mean) {
+	size_t k;
+	for (k = 0; k < n; ++k) {
+		float v = (float) ((double) sigma * cbo_normal (seed, k));
+		out[k] = mean ? (mean[k] + v) : v;
+	}
+}
+
+/* ---------------------------------------------------------------------- */
+/* The SMA step with explicit fmaf (the fast, portable restatement).       */
+/* ---------------------------------------------------------------------- */
+int cbo_sma_fma (int G, int size, size_t n, float alpha, float momentum,
+		float **z, float **last, float **s, float **w,
+		const int *locked, int *copy, int first, float *scratch) {
+
+	int g, i, copies = 0;
+	size_t k;
+	float *acc = scratch;                /* base->gradient per device */
+	float *D = scratch + (size_t) G * n; /* reduced base->diff        */
+
+	/* Phase A, clib-multigpu/synch/sma.c:42-128: per device, replicas in
+	 * increasing id order, restricted to locked replicas on that device. */
+	for (g = 0; g < G; ++g) {
+		float *a = acc + (size_t) g * n;
+		memset (a, 0, n * sizeof(float));                                   /* sma.c:66 */
+		for (i = first; i < size; ++i) {
+			if (! locked[i] || (i % G) != g)                                /* sma.c:71 */
+				continue;
+			for (k = 0; k < n; ++k) {
+				float d = fmaf (-1.0f, z[g][k], s[i][k]);                   /* sma.c:79-90 */
+				w[i][k] = fmaf (-alpha, d, w[i][k]);                        /* sma.c:93-99 */
+				a[k] = fmaf (alpha, d, a[k]);                               /* sma.c:102-107 */
+			}
+			if (copy[i])                                                    /* sma.c:113-120 */
+				copies++;
+		}
+	}
+
+	/* Phase B, clib-multigpu/synch/common.c:3-57: D = sum_g acc_g.  A
+	 * single-rank all-reduce is a copy; otherwise sum in rank order. */
+	memcpy (D, acc, n * sizeof(float));
+	for (g = 1; g < G; ++g)
+		for (k = 0; k < n; ++k)
+			D[k] = D[k] + acc[(size_t) g * n + k];
+
+	/* Phase C, sma.c:135-183: base momentum hard-coded to 0.9 when the base
+	 * model's momentum is positive; then z += D on every device. */
+	for (g = 0; g < G; ++g) {
+		for (k = 0; k < n; ++k) {
+			float Dg = D[k];
+			if (momentum > 0) {
+				Dg = fmaf (CBO_BASE_MOMENTUM, last[g][k], Dg);              /* sma.c:155-160 */
+				last[g][k] = Dg;                                            /* sma.c:163-164 */
+			}
+			z[g][k] = fmaf (1.0f, Dg, z[g][k]);                             /* sma.c:169-174 */
+		}
+	}
+
+	/* Phase D, sma.c:185-227: any locked replica with _copy set makes every
+	 * locked replica (on every device) copy its device's base model. */
+	if (copies > 0) {
+		for (i = first; i < size; ++i) {
+			if (! locked[i])
+				continue;
+			memcpy (w[i], z[i % G], n * sizeof(float));                     /* sma.c:213-217 */
+			copy[i] = 0;                                                    /* sma.c:220 */
+		}
+	}
+	return copies;
+}
+
+/* Phase A for one device: sma.c:66-121 restricted to the given replicas.  */
+int cbo_sma_accumulate (int R, size_t n, float alpha, const float *z,
+		float **s, float **w, const int *copy, float *acc) {
+	int i, copies = 0;
+	size_t k;
+	memset (acc, 0, n * sizeof(float));                                     /* sma.c:66 */
+	for (i = 0; i < R; ++i) {
+		for (k = 0; k < n; ++k) {
+			float d = fmaf (-1.0f, z[k], s[i][k]);                          /* sma.c:79-90 */
+			w[i][k] = fmaf (-alpha, d, w[i][k]);                            /* sma.c:93-99 */
+			acc[k] = fmaf (alpha, d, acc[k]);                               /* sma.c:102-107 */
+		}
+		if (copy && copy[i])
+			copies++;
+	}
+	return copies;
+}
+
+/* Phases C and D for one device: sma.c:148-174, 185-227. */
+void cbo_sma_apply (int R, size_t n, float momentum, const float *D,
+		float *z, float *last, float **w, int copy) {
+	int i;
+	size_t k;
+	for (k = 0; k < n; ++k) {
+		float Dg = D[k];
+		if (momentum > 0) {
+			Dg = fmaf (CBO_BASE_MOMENTUM, last[k], Dg);
+			last[k] = Dg;
+		}
+		z[k] = fmaf (1.0f, Dg, z[k]);
+	}
+	if (copy)
+		for (i = 0; i < R; ++i)
+			memcpy (w[i], z, n * sizeof(float));
+}
+
+/* ---------------------------------------------------------------------- */
+/* OpenBLAS replay of the reference call sequence.                         */
+/* ---------------------------------------------------------------------- */
+typedef void (*saxpy_fn) (int, float, const float *, int, float *, int);
+typedef void (*threads_fn) (int);
+
+static void *blas_handle = NULL;
+static saxpy_fn blas_saxpy = NULL;
+static threads_fn blas_threads = NULL;
+static char blas_name[512] = "";
+
+int cbo_blas_open (const char *path) {
+	static const char *probe[] = { "libopenblas.so.0", "libopenblas.so", NULL };
+	static const char *saxpy_names[] = { "cblas_saxpy", "scipy_cblas_saxpy", NULL };
+	static const char *thread_names[] = { "openblas_set_num_threads", "scipy_openblas_set_num_threads", NULL };
+	int j;
+	if (blas_handle)
+		return 0;
+	if (path)
+		blas_handle = dlopen (path, RTLD_NOW | RTLD_LOCAL);
+	for (j = 0; ! blas_handle && probe[j]; ++j) {
+		blas_handle = dlopen (probe[j], RTLD_NOW | RTLD_LOCAL);
+		if (blas_handle)
+			path = probe[j];
+	}
+	if (! blas_handle)
+		return -1;
+	for (j = 0; ! blas_saxpy && saxpy_names[j]; ++j)
+		blas_saxpy = (saxpy_fn) dlsym (blas_handle, saxpy_names[j]);
+	for (j = 0; ! blas_threads && thread_names[j]; ++j)
+		blas_threads = (threads_fn) dlsym (blas_handle, thread_names[j]);
+	if (! blas_saxpy) {
+		dlclose (blas_handle);
+		blas_handle = NULL;
+		return -2;
+	}
+	snprintf (blas_name, sizeof(blas_name), "%s", path);
+	/* clib-multigpu/BLAS.c:32: openblas_set_num_threads(1) */
+	if (blas_threads)
+		blas_threads (1);
+	return 0;
+}
+
+const char *cbo_blas_name (void) { return blas_name; }
+
+int cbo_blas_is_open (void) { return blas_handle != NULL; }
+
+void cbo_blas_set_threads (int threads) {
+	if (blas_threads)
+		blas_threads (threads);
+}
+
+int cbo_sma_blas (int G, int size, size_t n, float alpha, float momentum,
+		float **z, float **last, float **s, float **w,
+		const int *locked, int *copy, int first, float *scratch) {
+
+	int g, h, i, copies = 0;
+	int N = (int) n; /* the reference passes model->elements, an int */
+	size_t bytes = n * sizeof(float);
+	float *gradient = scratch;                      /* base->gradient, per device */
+	float *diff = scratch + (size_t) G * n;         /* base->diff, per device     */
+
+	if (! blas_saxpy)
+		return -1;
+
+	for (g = 0; g < G; ++g) {
+		float *acc = gradient + (size_t) g * n;
+		float *d = diff + (size_t) g * n;
+		memset (acc, 0, bytes);                                         /* sma.c:66 */
+		for (i = first; i < size; ++i) {
+			if (! locked[i] || (i % G) != g)
+				continue;
+			memcpy (d, s[i], bytes);                                    /* sma.c:79-83 */
+			blas_saxpy (N, -1.0f, z[g], 1, d, 1);                       /* sma.c:85-90 */
+			blas_saxpy (N, -alpha, d, 1, w[i], 1);                      /* sma.c:93-99 */
+			blas_saxpy (N, alpha, d, 1, acc, 1);                        /* sma.c:102-107 */
+			if (copy[i])
+				copies++;
+		}
+	}
+
+	/* common.c:43-52: receive buffer base->diff := all-reduce(base->gradient) */
+	for (g = 0; g < G; ++g) {
+		float *d = diff + (size_t) g * n;
+		memcpy (d, gradient, bytes);
+		for (h = 1; h < G; ++h)
+			blas_saxpy (N, 1.0f, gradient + (size_t) h * n, 1, d, 1);
+	}
+
+	for (g = 0; g < G; ++g) {
+		float *d = diff + (size_t) g * n;
+		if (momentum > 0) {
+			blas_saxpy (N, CBO_BASE_MOMENTUM, last[g], 1, d, 1);        /* sma.c:155-160 */
+			memcpy (last[g], d, bytes);                                 /* sma.c:163-164 */
+		}
+		blas_saxpy (N, 1.0f, d, 1, z[g], 1);                            /* sma.c:169-174 */
+	}
+
+	if (copies > 0) {
+		for (i = first; i < size; ++i) {
+			if (! locked[i])
+				continue;
+			memcpy (w[i], z[i % G], bytes);                             /* sma.c:213-217 */
+			copy[i] = 0;
+		}
+	}
+	return copies;
+}
+
+/* ---------------------------------------------------------------------- */
+/* CPU affinity, clib-multigpu/CPU.c:39-60                                 */
+/* ---------------------------------------------------------------------- */
+int cbo_bind_core (int core) {
+	cpu_set_t set;
+	CPU_ZERO (&set);
+	CPU_SET (core, &set);
+	return sched_setaffinity (0, sizeof(set), &set);
+}
+
+int cbo_unbind (void) {
+	cpu_set_t set;
+	long j, ncores = sysconf (_SC_NPROCESSORS_ONLN);
+	CPU_ZERO (&set);
+	for (j = 0; j < ncores && j < CPU_SETSIZE; ++j)
+		CPU_SET (j, &set);
+	return sched_setaffinity (0, sizeof(set), &set);
+}
+
+double cbo_now (void) {
+	struct timespec ts;
+	clock_gettime (CLOCK_MONOTONIC, &ts);
+	return (double) ts.tv_sec + 1e-9 * (double) ts.tv_nsec;
+}

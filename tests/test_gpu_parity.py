@@ -1,0 +1,297 @@
+"""HIP SMA path vs the CPU oracle, through the C-ABI (run with -m gpu).
+
+Bar: at G = 1 the HIP kernels use the reference's fp32
+operation order (cuBLAS saxpy = fma), so results must be BIT-EXACT with the
+oracle (oracle/sma_oracle.c, restating clib-multigpu/synch/sma.c:13-231).
+"""
+from __future__ import annotations
+
+import os
+import tempfile
+
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+from tests.helpers import assert_bitexact, compare_states, download, make_gpu, upload
+
+pytestmark = pytest.mark.gpu
+
+
+def _run(n, R, alpha, momentum, copy_ids=(), first=0, held=(), sync=0, config=None, split=False,
+         bucket=0, steps=1):
+    st = O.make_state(n, 1, R, alpha, momentum)
+    g = make_gpu(n, R, alpha, momentum, sync=sync)
+    try:
+        if config:
+            g.set_kernel_config(**config)
+        if split:
+            g.set_force_split(True)
+        if bucket:
+            g.set_bucket_elements(bucket)
+        upload(g, st)
+        want = st.clone()
+        for _ in range(steps):
+            for i in copy_ids:
+                g.set_replica_copy(i, True)
+                want.copy[i] = 1
+            for i in held:
+                g.replica_lock(i)
+            locked = g.lockAny()
+            want.locked[:] = 1
+            for i in held:
+                want.locked[i] = 0
+            if sync == 0:
+                assert locked == R
+            else:
+                assert locked == R - len(held)
+            want.first = first
+            g.synchronise(first, 1, 0, False)
+            assert g.unlockAny() == R - len(held)
+            for i in held:
+                g.replica_unlock(i)
+            O.sma_step(want)
+        g.wait()
+        got = download(g, st)
+        compare_states(got, want)
+        for i in copy_ids:
+            assert g.replica_copy(i) == 0, "Phase D must reset _copy (sma.c:220)"
+    finally:
+        g.free()
+
+
+@pytest.mark.parametrize("R", [1, 2, 3, 4, 8])
+@pytest.mark.parametrize("momentum", [0.0, 0.9])
+def test_fused_bitexact(R, momentum):
+    _run(4099, R, 0.1, momentum)
+
+
+@pytest.mark.parametrize("R", [9, 16])
+def test_fused_generic_replica_count(R):
+    # > 8 replicas per GPU takes the chunked (register-resident groups of 8) kernel.
+    _run(1031, R, 0.1, 0.9)
+
+
+def test_lenet_size_alpha_half():
+    # C2: LeNet, 4 replicas on 1 GPU, alpha = 0.5 (SolverConf default).
+    _run(1_111_946, 4, 0.5, 0.0)
+
+
+def test_copy_flag_phase_d():
+    # A learning-rate drop on one replica copies the new base model into all.
+    _run(4099, 4, 0.1, 0.9, copy_ids=(2,))
+
+
+def test_first_offset():
+    _run(4099, 6, 0.1, 0.9, first=2)
+
+
+def test_ssp_partial_lock():
+    # A replica busy on the task side is skipped by lockAny under SSP.
+    _run(4099, 4, 0.1, 0.9, held=(1,), sync=1)
+
+
+def test_bsp_barrier_failure():
+    from crossbow_amd import CbxError
+    n, R = 1031, 2
+    g = make_gpu(n, R, 0.1, 0.0, sync=0)
+    try:
+        g.replica_lock(1)
+        with pytest.raises(CbxError) as e:
+            g.lockAny()
+        assert "failed to lock all" in str(e.value)
+        g.replica_unlock(1)
+        assert g.lockAny() == R
+        g.unlockAny()
+    finally:
+        g.free()
+
+
+@pytest.mark.parametrize("config", [
+    dict(block=256, blocks_per_cu=0, policy=0, unroll=1),
+    dict(block=256, blocks_per_cu=8, policy=1, unroll=1),
+    dict(block=512, blocks_per_cu=4, policy=1, unroll=2),
+    dict(block=128, blocks_per_cu=0, policy=1, unroll=2),
+])
+def test_launch_configs_identical(config):
+    _run(70_001, 8, 0.1, 0.9, config=config)
+
+
+@pytest.mark.parametrize("momentum", [0.0, 0.9])
+def test_split_pipeline_one_rank(momentum):
+    # Kernel A + RCCL all-reduce (one-rank communicator) + kernel B.
+    _run(4099, 4, 0.1, momentum, split=True)
+
+
+def test_split_pipeline_buckets_and_copy():
+    _run(300_001, 3, 0.1, 0.9, split=True, bucket=65_536, copy_ids=(0,), steps=2)
+
+
+def test_multiple_steps_drift():
+    _run(50_000, 4, 0.1, 0.9, steps=3)
+
+
+def test_update_type_routing():
+    from crossbow_amd import CbxError
+    # SYNCHRONOUSEAMSGD (3) routes to SMA (executioncontext.c:2287-2295).
+    n, R = 1031, 2
+    st = O.make_state(n, 1, R, 0.1, 0.0)
+    g = make_gpu(n, R, 0.1, 0.0, update_type=3)
+    try:
+        upload(g, st)
+        g.lockAny()
+        g.synchronise(0, 1, 0, False)
+        g.unlockAny()
+        want = st.clone()
+        O.sma_step(want)
+        compare_states(download(g, st), want)
+    finally:
+        g.free()
+    g = make_gpu(n, R, 0.1, 0.0, update_type=1)  # WORKER: not this path
+    try:
+        g.lockAny()
+        with pytest.raises(CbxError):
+            g.synchronise(0, 1, 0, False)
+    finally:
+        g.free()
+
+
+def test_register_variables_and_replication():
+    from crossbow_amd import BUF_DATA, TheGPU
+    from crossbow_amd.variables import lenet_variables, register
+    n = 1_111_946
+    init = O.fill_normal(n, 99, 0.05)
+    g = TheGPU()
+    g.init([0])
+    try:
+        assert register(g, lenet_variables(), init) == n
+        g.setUpdateModelType(7)
+        g.setMomentum(0.9, 0)
+        g.setModelManager(3, 0)
+        assert g.num_replicas() == 3 and g.elements() == n
+        assert_bitexact(g.base_read(0, BUF_DATA), init, "theModel pushed")
+        for i in range(3):
+            assert_bitexact(g.replica_read(i, BUF_DATA), init, f"replica {i}")
+    finally:
+        g.free()
+
+
+def test_checkpoint_roundtrip_file_format():
+    from crossbow_amd import BUF_DATA, BUF_LAST
+    n, R = 4099, 2
+    st = O.make_state(n, 1, R, 0.1, 0.9)
+    g = make_gpu(n, R, 0.1, 0.9)
+    try:
+        upload(g, st)
+        with tempfile.TemporaryDirectory() as d:
+            g.checkpointModel(d)
+            ck = os.path.join(d, "000001")
+            names = sorted(os.listdir(ck))
+            assert names == ["gpu-00-replica-000-data.dat", "gpu-00-replica-000-last.dat",
+                             "gpu-00-replica-001-data.dat", "gpu-00-replica-001-last.dat",
+                             "gpu-00-theModel-data.dat", "gpu-00-theModel-last.dat"]
+            raw = np.fromfile(os.path.join(ck, "gpu-00-theModel-data.dat"), dtype="<f4")
+            assert_bitexact(raw, st.z[0], "raw little-endian fp32 file")
+            g.base_write(0, BUF_DATA, np.zeros(n, np.float32))
+            g.replica_write(1, BUF_DATA, np.zeros(n, np.float32))
+            g.overrideModelData(ck)
+            assert_bitexact(g.base_read(0, BUF_DATA), st.z[0], "z restored")
+            assert_bitexact(g.base_read(0, BUF_LAST), st.last[0], "last restored")
+            assert_bitexact(g.replica_read(1, BUF_DATA), st.w[1], "w restored")
+            g.checkpointModel(d)
+            assert os.path.isdir(os.path.join(d, "000002"))
+    finally:
+        g.free()
+
+
+def test_staged_roundtrip():
+    # Pinned-host staging: stage_in -> step -> stage_out equals the oracle.
+    from crossbow_amd import BUF_DATA, BUF_DIFF, BUF_LAST
+    n, R = 65_536, 4
+    st = O.make_state(n, 1, R, 0.1, 0.9)
+    g = make_gpu(n, R, 0.1, 0.9)
+    try:
+        g.base_host_view(0, BUF_DATA)[:] = st.z[0]
+        g.base_host_view(0, BUF_LAST)[:] = st.last[0]
+        for i in range(R):
+            g.replica_host_view(i, BUF_DIFF)[:] = st.s[i]
+            g.replica_host_view(i, BUF_DATA)[:] = st.w[i]
+        g.set_timing(True)
+        g.stage_in()
+        g.lockAny()
+        g.synchronise(0, 1, 0, False)
+        g.unlockAny()
+        g.stage_out()
+        g.wait()
+        t = g.last_timing(0)
+        assert t[4] > 0 and t[5] > 0 and t[0] > 0
+        want = st.clone()
+        O.sma_step(want)
+        assert_bitexact(g.base_host_view(0, BUF_DATA), want.z[0], "z staged out")
+        assert_bitexact(g.base_host_view(0, BUF_LAST), want.last[0], "last staged out")
+        for i in range(R):
+            assert_bitexact(g.replica_host_view(i, BUF_DATA), want.w[i], f"w[{i}] staged out")
+    finally:
+        g.free()
+
+
+def test_resnet50_full_size_sampled_parity_and_conservation():
+    """C3 at full size (n = 25,557,032, R = 8, mu = 0.9): the step is elementwise,
+    so the oracle run on a random sample of element positions must match the
+    GPU bit for bit there; plus a size-independent conservation checksum:
+    z' + sum_i w_i' = z + sum_i w_i + 0.9 last  (exact in real arithmetic)."""
+    from crossbow_amd import BUF_DATA, BUF_DIFF, BUF_LAST
+    n, R = 25_557_032, 8
+    g = make_gpu(n, R, 0.1, 0.9)
+    try:
+        g.fill_synthetic(O.SEED)
+        rng = np.random.default_rng(7)
+        idx = np.unique(np.concatenate([rng.integers(0, n, 200_000), [0, 1, 2, 3, n - 4, n - 3, n - 2, n - 1]]))
+        z0 = g.base_read(0, BUF_DATA)
+        l0 = g.base_read(0, BUF_LAST)
+        s0 = [g.replica_read(i, BUF_DIFF) for i in range(R)]
+        w0 = [g.replica_read(i, BUF_DATA) for i in range(R)]
+        before = float(np.sum(z0, dtype=np.float64) + sum(np.sum(w, dtype=np.float64) for w in w0)
+                       + 0.9 * np.sum(l0, dtype=np.float64))
+        g.lockAny()
+        g.synchronise(0, 1, 0, False)
+        g.unlockAny()
+        g.wait()
+        z1 = g.base_read(0, BUF_DATA)
+        l1 = g.base_read(0, BUF_LAST)
+        w1 = [g.replica_read(i, BUF_DATA) for i in range(R)]
+        after = float(np.sum(z1, dtype=np.float64) + sum(np.sum(w, dtype=np.float64) for w in w1))
+        assert abs(after - before) <= 1e-6 * max(1.0, abs(before)) + 1e-3, (after, before)
+        st = O.SmaState(1, R, idx.size, 0.1, 0.9, [z0[idx].copy()], [l0[idx].copy()],
+                        [s[idx].copy() for s in s0], [w[idx].copy() for w in w0])
+        O.sma_step(st)
+        assert_bitexact(z1[idx], st.z[0], "z sample")
+        assert_bitexact(l1[idx], st.last[0], "last sample")
+        for i in range(R):
+            assert_bitexact(w1[i][idx], st.w[i], f"w[{i}] sample")
+    finally:
+        g.free()
+
+
+def test_golden_fixtures_on_gpu():
+    from tests.test_oracle import GOLDEN_DIR, load_golden_cases
+    cases = load_golden_cases()
+    assert cases, f"no fixtures in {GOLDEN_DIR}"
+    for case in cases:
+        if case["G"] != 1:
+            continue
+        st = case["state"]
+        g = make_gpu(st.n, st.size, st.alpha, st.momentum)
+        try:
+            upload(g, st)
+            for i in np.nonzero(st.copy)[0]:
+                g.set_replica_copy(int(i), True)
+            g.lockAny()
+            g.synchronise(st.first, 1, 0, False)
+            g.unlockAny()
+            got = download(g, st)
+            for k in range(st.size):
+                assert_bitexact(got.w[k], case["w_out"][k], f"{case['name']} w[{k}]")
+            assert_bitexact(got.z[0], case["z_out"][0], f"{case['name']} z")
+        finally:
+            g.free()
