@@ -103,28 +103,20 @@ def cpu_baseline(args, n_full):
 
 def main():
     args = parse()
-    rank = int(os.environ.get("RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    from crossbow_amd import dist as D
+    rank, world, local_rank = D.env_rank()
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: launch N>1 with torch.distributed.run")
 
     import torch
-    import torch.distributed as dist
 
     from crossbow_amd import SYNC_BSP, UPDATE_SMA, TheGPU, _lib
     from crossbow_amd.variables import MODELS, register
 
     torch.cuda.set_device(local_rank)
-    if world > 1:
-        dist.init_process_group("gloo", rank=rank, world_size=world)
-
+    D.init(world, rank)
     gpu = TheGPU()
-    uid = None
-    if world > 1:
-        obj = [gpu.unique_id() if rank == 0 else None]
-        dist.broadcast_object_list(obj, src=0)
-        uid = obj[0]
+    uid = D.share_unique_id(rank, world, TheGPU.unique_id)
     gpu.init_rank(local_rank, world, rank, uid)
 
     shapes = MODELS[args.model]()
@@ -154,19 +146,15 @@ def main():
         step()
     gpu.wait()
     torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
+    D.barrier(world)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
     gpu.wait()
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
-    if world > 1:
-        dist.barrier()
-        t = torch.tensor([el], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = float(t.item())
+    D.barrier(world)
+    el = D.max_over_ranks(el, world)
 
     G = world
     split = G > 1 or args.force_split
@@ -259,8 +247,7 @@ def main():
     gpu.free()
     if rank == 0:
         print(json.dumps(result), flush=True)
-    if world > 1:
-        dist.destroy_process_group()
+    D.finalize(world)
 
 
 if __name__ == "__main__":

@@ -116,6 +116,7 @@ SIGNATURES = {
     "cbx_replica_host_buffer": (_I, [_P, _I, _I, _PP]),
     "cbx_base_host_buffer": (_I, [_P, _I, _I, _PP]),
     "cbx_wait": (_I, [_P]),
+    "cbx_step_event": (_I, [_P, _I, _PP]),
     "cbx_set_timing": (_I, [_P, _I]),
     "cbx_last_timing": (_I, [_P, _I, _FP]),
     "cbx_timing_history": (_I, [_P, _I, _I, _FP, _I]),

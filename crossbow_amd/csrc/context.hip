@@ -162,7 +162,6 @@ struct Replica {
   int updates = 0;
   SolverConf conf;
   pthread_mutex_t lock;
-  hipEvent_t updated = nullptr;
 };
 
 enum TimingEv { EV_START = 0, EV_A, EV_AR, EV_B, EV_H2D0, EV_H2D1, EV_D2H0, EV_D2H1, EV_COUNT };
@@ -180,7 +179,7 @@ struct Device {
   size_t arena_bytes = 0;
   size_t stride = 0;  // bytes per buffer slot
   std::vector<int> replicas;  // global ids, increasing
-  hipEvent_t base_updated = nullptr, accumulated = nullptr, synched = nullptr;
+  hipEvent_t synched = nullptr;  // end of the last step (cbx_step_event)
   hipEvent_t ev[EV_COUNT] = {};
   bool ev_valid[EV_COUNT] = {};
   // Per-step timing ring: events {START, A, AR, B} of the last kRing steps,
@@ -340,8 +339,6 @@ int open_device(Device &d, int hip_id, int g) {
   HIP_TRY(hipSetDevice(hip_id));
   // executioncontext.c:324: one non-blocking model-synchronisation stream.
   HIP_TRY(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
-  HIP_TRY(hipEventCreateWithFlags(&d.base_updated, hipEventDisableTiming));
-  HIP_TRY(hipEventCreateWithFlags(&d.accumulated, hipEventDisableTiming));
   HIP_TRY(hipEventCreateWithFlags(&d.synched, hipEventDisableTiming));
   for (int k = 0; k < EV_COUNT; ++k) HIP_TRY(hipEventCreate(&d.ev[k]));
   return CBX_OK;
@@ -354,8 +351,6 @@ void close_device(Device &d) {
   if (d.comm) (void)ncclCommDestroy(d.comm);
   if (d.arena) (void)hipFree(d.arena);
   if (d.host) (void)hipHostFree(d.host);
-  if (d.base_updated) (void)hipEventDestroy(d.base_updated);
-  if (d.accumulated) (void)hipEventDestroy(d.accumulated);
   if (d.synched) (void)hipEventDestroy(d.synched);
   for (int k = 0; k < EV_COUNT; ++k)
     if (d.ev[k]) (void)hipEventDestroy(d.ev[k]);
@@ -455,9 +450,10 @@ int sma_step(cbx_context *c, int first) {
   }
   if (c->G == 1 && !c->force_split) {
     // Single GPU: Phase B is the identity, so A + C (+ D) fuse into one pass.
+    // (sma.c:63 waits on base->updated; every producer of z is this stream,
+    // so stream order already gives that dependency.)
     Device &d = c->devs[0];
     HIP_TRY(hipSetDevice(d.hip_id));
-    HIP_TRY(hipStreamWaitEvent(d.stream, d.base_updated, 0));  // sma.c:63
     cbx::LaunchConfig cfg = c->cfg;
     cfg.num_cus = d.num_cus;
     TRY(mark(c, d, EV_START));
@@ -476,7 +472,6 @@ int sma_step(cbx_context *c, int first) {
     for (size_t k = 0; k < c->devs.size(); ++k) {
       Device &d = c->devs[k];
       HIP_TRY(hipSetDevice(d.hip_id));
-      HIP_TRY(hipStreamWaitEvent(d.stream, d.base_updated, 0));
       TRY(mark(c, d, EV_START));
     }
     for (int64_t b = 0; b < nb; ++b) {
@@ -488,10 +483,7 @@ int sma_step(cbx_context *c, int first) {
         cbx::LaunchConfig cfg = c->cfg;
         cfg.num_cus = d.num_cus;
         HIP_TRY(cbx::launch_sma_accumulate(offset_args(args[k], start, len), b == 0, cfg, d.stream));
-        if (b == nb - 1) {
-          TRY(mark(c, d, EV_A));
-          HIP_TRY(hipEventRecord(d.accumulated, d.stream));  // sma.c:127
-        }
+        if (b == nb - 1) TRY(mark(c, d, EV_A));
       }
       // common.c:14-54: grouped all-reduce, fp32 sum.  Bucket 0 also carries
       // the control block that sits right in front of the data.
@@ -528,16 +520,17 @@ int sma_step(cbx_context *c, int first) {
     c->last_step_split = true;
   }
 
-  // Events the unchanged scheduler waits on: synched / base->updated
-  // (sma.c:177,204) and replica->updated (sma.c:115,222).
+  // The reference records synched / base->updated (sma.c:177,204) and one
+  // replica->updated per replica (sma.c:115,222) at points that, in this
+  // pipeline, are all the same: the end of the step on the sync stream.  One
+  // event per device stands for all of them (cbx_step_event); each extra
+  // record is a marker packet costing GPU time between steps.
   for (size_t k = 0; k < c->devs.size(); ++k) {
     Device &d = c->devs[k];
     HIP_TRY(hipSetDevice(d.hip_id));
     HIP_TRY(hipEventRecord(d.synched, d.stream));
-    HIP_TRY(hipEventRecord(d.base_updated, d.stream));
     for (int id : d.replicas) {
       if (id < first || !c->locked[id]) continue;
-      HIP_TRY(hipEventRecord(c->replicas[id]->updated, d.stream));
       c->replicas[id]->conf.copy = 0;  // sma.c:220 (a no-op unless a copy happened)
     }
   }
@@ -700,7 +693,6 @@ int cbx_free(cbx_context *c) {
   for (Device &d : c->devs) close_device(d);
   for (Replica *r : c->replicas) {
     if (!r) continue;
-    if (r->updated) (void)hipEventDestroy(r->updated);
     pthread_mutex_destroy(&r->lock);
     delete r;
   }
@@ -910,9 +902,8 @@ int cbx_set_model_manager(cbx_context *c, int replicas, int type) {
     for (int id : d.replicas) {
       Replica &r = *c->replicas[id];
       HIP_TRY(hipMemcpyAsync(replica_dev(d, r, CBX_BUF_DATA), z, (size_t)c->n * 4, hipMemcpyDeviceToDevice, d.stream));
-      HIP_TRY(hipEventCreateWithFlags(&r.updated, hipEventDisableTiming));
     }
-    HIP_TRY(hipEventRecord(d.base_updated, d.stream));
+    HIP_TRY(hipEventRecord(d.synched, d.stream));
     HIP_TRY(hipStreamSynchronize(d.stream));
   }
   c->manager = true;
@@ -1278,6 +1269,13 @@ int cbx_wait(cbx_context *c) {
     HIP_TRY(hipSetDevice(d.hip_id));
     HIP_TRY(hipStreamSynchronize(d.stream));
   }
+  return CBX_OK;
+}
+
+int cbx_step_event(cbx_context *c, int local, void **event) {
+  TRY(check_ctx(c));
+  if (local < 0 || local >= (int)c->devs.size() || !event) return fail(CBX_ERR_INVALID, "bad step-event query");
+  *event = reinterpret_cast<void *>(c->devs[local].synched);
   return CBX_OK;
 }
 

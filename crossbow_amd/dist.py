@@ -1,0 +1,68 @@
+"""One-process-per-GPU plumbing around the C-ABI (torch.distributed, host side).
+
+The data path never goes through torch: each rank's ``libcrossbow_sma``
+context owns its RCCL communicator (ncclCommInitRank) and runs the all-reduce
+of the SMA step itself.  torch.distributed (gloo, CPU) only carries the
+control plane: the 128-byte RCCL unique id from rank 0 to every rank, the
+barriers around the timed region and the max-over-ranks of the wall time.
+
+Rank r drives global device r; replica i lives on device i % G, i.e. on rank
+i % G (the reference's round-robin placement, clib-multigpu/modelmanager.c:51-64).
+"""
+from __future__ import annotations
+
+import os
+from typing import Callable, Optional, Tuple
+
+
+def env_rank() -> Tuple[int, int, int]:
+    """(rank, world_size, local_rank) from the torch.distributed.run environment."""
+    return (int(os.environ.get("RANK", "0")), int(os.environ.get("WORLD_SIZE", "1")),
+            int(os.environ.get("LOCAL_RANK", "0")))
+
+
+def init(world: int, rank: int, backend: str = "gloo") -> None:
+    import torch.distributed as dist
+    if world > 1 and not dist.is_initialized():
+        dist.init_process_group(backend, rank=rank, world_size=world)
+
+
+def share_unique_id(rank: int, world: int, make: Callable[[], bytes]) -> Optional[bytes]:
+    """Rank 0 creates the RCCL unique id with ``make``; every rank returns it."""
+    if world <= 1:
+        return None
+    import torch.distributed as dist
+    obj = [make() if rank == 0 else None]
+    dist.broadcast_object_list(obj, src=0)
+    uid = obj[0]
+    if not isinstance(uid, (bytes, bytearray)) or len(uid) != 128:
+        raise RuntimeError("bad RCCL unique id from rank 0")
+    return bytes(uid)
+
+
+def barrier(world: int) -> None:
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+
+
+def max_over_ranks(value: float, world: int) -> float:
+    if world <= 1:
+        return float(value)
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([float(value)], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def local_replicas(size: int, world: int, rank: int):
+    """Global replica ids this rank owns (round-robin placement)."""
+    return [i for i in range(size) if i % world == rank]
+
+
+def finalize(world: int) -> None:
+    if world > 1:
+        import torch.distributed as dist
+        if dist.is_initialized():
+            dist.destroy_process_group()

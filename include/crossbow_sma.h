@@ -173,6 +173,12 @@ int cbx_replica_host_buffer (cbx_context *ctx, int id, int kind, void **host_ptr
 int cbx_base_host_buffer (cbx_context *ctx, int device, int kind, void **host_ptr);
 /* Block until every local sync stream has drained. */
 int cbx_wait (cbx_context *ctx);
+/* The event (a hipEvent_t, as void*) recorded on local device `local`'s sync
+ * stream at the end of every synchronise(): it stands for the reference's
+ * base->updated, synched[dev] and each locked replica's replica->updated
+ * (sma.c:115,177,204,222), which this pipeline completes at the same point.
+ * Task-side streams wait on it before using a replica again.             */
+int cbx_step_event (cbx_context *ctx, int local, void **event);
 
 /* ---- measurement ------------------------------------------------------ */
 #define CBX_T_KERNEL    0   /* fused kernel, or kernel A (G > 1)       */

@@ -281,14 +281,19 @@ def test_golden_fixtures_on_gpu():
         if case["G"] != 1:
             continue
         st = case["state"]
-        g = make_gpu(st.n, st.size, st.alpha, st.momentum)
+        held = [int(i) for i in np.nonzero(st.locked == 0)[0]]
+        g = make_gpu(st.n, st.size, st.alpha, st.momentum, sync=1 if held else 0)
         try:
             upload(g, st)
             for i in np.nonzero(st.copy)[0]:
                 g.set_replica_copy(int(i), True)
-            g.lockAny()
+            for i in held:  # busy on the task side: lockAny (SSP) skips it
+                g.replica_lock(i)
+            assert g.lockAny() == st.size - len(held)
             g.synchronise(st.first, 1, 0, False)
             g.unlockAny()
+            for i in held:
+                g.replica_unlock(i)
             got = download(g, st)
             for k in range(st.size):
                 assert_bitexact(got.w[k], case["w_out"][k], f"{case['name']} w[{k}]")
