@@ -169,7 +169,10 @@ enum TimingEv { EV_START = 0, EV_A, EV_AR, EV_B, EV_H2D0, EV_H2D1, EV_D2H0, EV_D
 struct Device {
   int hip_id = 0;
   int g = 0;  // global device index
-  hipStream_t stream = nullptr;
+  hipStream_t stream = nullptr;       // model synchronisation stream (kernels)
+  hipStream_t comm_stream = nullptr;  // RCCL all-reduce of the bucketed pipeline (G > 1)
+  std::vector<hipEvent_t> bucket_acc;  // per bucket: kernel A done (stream -> comm_stream)
+  std::vector<hipEvent_t> bucket_red;  // per bucket: all-reduce done (comm_stream -> stream)
   ncclComm_t comm = nullptr;
   int num_cus = 256;
   // Arena: [base data][base gradient(ctrl+acc)][base diff(ctrl+D)][base last]
@@ -224,6 +227,12 @@ namespace {
 constexpr int kBaseSlots = 4;     // data, gradient, diff, last
 constexpr int kReplicaSlots = 4;  // data, diff, last, gradient
 constexpr size_t kAlign = 2u << 20;
+// Extra bytes between consecutive buffer slots, so the 2R+2 streams of one
+// element index do not all start on the same 2 MiB boundary (measured +1-2 %
+// on the fused kernel, scripts/membench.hip, profiles/r01).
+constexpr size_t kSlotStagger = 4096;
+// Buckets of the G > 1 pipeline when cbx_set_bucket_elements was not called.
+constexpr int64_t kDefaultBuckets = 8;
 
 size_t slot_index_base(int kind) {
   switch (kind) {
@@ -339,6 +348,7 @@ int open_device(Device &d, int hip_id, int g) {
   HIP_TRY(hipSetDevice(hip_id));
   // executioncontext.c:324: one non-blocking model-synchronisation stream.
   HIP_TRY(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
+  HIP_TRY(hipStreamCreateWithFlags(&d.comm_stream, hipStreamNonBlocking));
   HIP_TRY(hipEventCreateWithFlags(&d.synched, hipEventDisableTiming));
   for (int k = 0; k < EV_COUNT; ++k) HIP_TRY(hipEventCreate(&d.ev[k]));
   return CBX_OK;
@@ -348,6 +358,7 @@ void close_device(Device &d) {
   if (d.stream == nullptr && d.arena == nullptr) return;
   (void)hipSetDevice(d.hip_id);
   if (d.stream) (void)hipStreamSynchronize(d.stream);
+  if (d.comm_stream) (void)hipStreamSynchronize(d.comm_stream);
   if (d.comm) (void)ncclCommDestroy(d.comm);
   if (d.arena) (void)hipFree(d.arena);
   if (d.host) (void)hipHostFree(d.host);
@@ -355,7 +366,10 @@ void close_device(Device &d) {
   for (int k = 0; k < EV_COUNT; ++k)
     if (d.ev[k]) (void)hipEventDestroy(d.ev[k]);
   for (hipEvent_t e : d.ring) (void)hipEventDestroy(e);
+  for (hipEvent_t e : d.bucket_acc) (void)hipEventDestroy(e);
+  for (hipEvent_t e : d.bucket_red) (void)hipEventDestroy(e);
   if (d.stream) (void)hipStreamDestroy(d.stream);
+  if (d.comm_stream) (void)hipStreamDestroy(d.comm_stream);
   d = Device();
 }
 
@@ -372,9 +386,11 @@ int mark(cbx_context *c, Device &d, int ev) {
   return CBX_OK;
 }
 
-void ring_advance(cbx_context *c, Device &d, bool split) {
+// kind: 0 fused (START, A=B), 1 split in order (START, A, AR, B),
+// 2 split pipelined (START, B only: per-kernel spans are not separable).
+void ring_advance(cbx_context *c, Device &d, int kind) {
   if (!c->timing || d.ring.empty()) return;
-  d.ring_split[d.ring_pos] = split ? 1 : 0;
+  d.ring_split[d.ring_pos] = (char)kind;
   d.ring_pos = (d.ring_pos + 1) % Device::kRing;
   if (d.ring_count < Device::kRing) d.ring_count++;
 }
@@ -460,33 +476,51 @@ int sma_step(cbx_context *c, int first) {
     HIP_TRY(cbx::launch_sma_fused(args[0], mom, copies_total > 0, cfg, d.stream));
     TRY(mark(c, d, EV_A));
     TRY(mark(c, d, EV_B));
-    ring_advance(c, d, false);
+    ring_advance(c, d, 0);
     c->last_step_split = false;
   } else {
     // G > 1: kernel A, grouped RCCL all-reduce of acc (+ control block),
-    // kernel B; optionally per bucket so A(k+1) overlaps all-reduce(k).
+    // kernel B.  With one bucket everything runs in order on the sync
+    // stream.  With nb > 1 buckets the all-reduce runs on a second stream:
+    //   stream      : A(0) A(1) [wait red(0)] B(0) A(2) [wait red(1)] B(1) ...
+    //   comm_stream :      [wait acc(0)] AR(0) [wait acc(1)] AR(1) ...
+    // so kernel A of bucket k+1 overlaps the xGMI all-reduce of bucket k.
     const int64_t pad = cbx::kPadFloat4;
-    int64_t b4 = c->bucket_elems > 0 ? ((c->bucket_elems / 4 + pad - 1) / pad) * pad : c->n4;
+    int64_t b4 = c->n4;
+    if (c->bucket_elems > 0) {
+      b4 = ((c->bucket_elems / 4 + pad - 1) / pad) * pad;
+    } else if (c->G > 1) {
+      b4 = ((c->n4 / kDefaultBuckets + pad - 1) / pad) * pad;  // auto: kDefaultBuckets buckets
+    }
     if (b4 <= 0 || b4 > c->n4) b4 = c->n4;
     const int64_t nb = (c->n4 + b4 - 1) / b4;
+    const bool pipelined = nb > 1;
     for (size_t k = 0; k < c->devs.size(); ++k) {
       Device &d = c->devs[k];
       HIP_TRY(hipSetDevice(d.hip_id));
       TRY(mark(c, d, EV_START));
+      if (pipelined) {
+        while ((int64_t)d.bucket_acc.size() < nb) {
+          hipEvent_t ea, er;
+          HIP_TRY(hipEventCreateWithFlags(&ea, hipEventDisableTiming));
+          HIP_TRY(hipEventCreateWithFlags(&er, hipEventDisableTiming));
+          d.bucket_acc.push_back(ea);
+          d.bucket_red.push_back(er);
+        }
+      }
     }
-    for (int64_t b = 0; b < nb; ++b) {
+    auto allreduce = [&](int64_t b, bool on_comm) -> int {
       const int64_t start = b * b4;
       const int64_t len = std::min(b4, c->n4 - start);
-      for (size_t k = 0; k < c->devs.size(); ++k) {
-        Device &d = c->devs[k];
-        HIP_TRY(hipSetDevice(d.hip_id));
-        cbx::LaunchConfig cfg = c->cfg;
-        cfg.num_cus = d.num_cus;
-        HIP_TRY(cbx::launch_sma_accumulate(offset_args(args[k], start, len), b == 0, cfg, d.stream));
-        if (b == nb - 1) TRY(mark(c, d, EV_A));
-      }
       // common.c:14-54: grouped all-reduce, fp32 sum.  Bucket 0 also carries
       // the control block that sits right in front of the data.
+      if (on_comm) {
+        for (size_t k = 0; k < c->devs.size(); ++k) {
+          Device &d = c->devs[k];
+          HIP_TRY(hipSetDevice(d.hip_id));
+          HIP_TRY(hipStreamWaitEvent(d.comm_stream, d.bucket_acc[b], 0));
+        }
+      }
       NCCL_TRY(ncclGroupStart());
       for (size_t k = 0; k < c->devs.size(); ++k) {
         Device &d = c->devs[k];
@@ -499,23 +533,71 @@ int sma_step(cbx_context *c, int first) {
           dst -= cbx::kCtrlFloats;
           count += cbx::kCtrlFloats;
         }
-        NCCL_TRY(ncclAllReduce(src, dst, count, ncclFloat, ncclSum, d.comm, d.stream));
+        NCCL_TRY(ncclAllReduce(src, dst, count, ncclFloat, ncclSum, d.comm, on_comm ? d.comm_stream : d.stream));
       }
       NCCL_TRY(ncclGroupEnd());
+      if (on_comm) {
+        for (size_t k = 0; k < c->devs.size(); ++k) {
+          Device &d = c->devs[k];
+          HIP_TRY(hipSetDevice(d.hip_id));
+          HIP_TRY(hipEventRecord(d.bucket_red[b], d.comm_stream));
+        }
+      }
+      return CBX_OK;
+    };
+    auto accumulate = [&](int64_t b) -> int {
+      const int64_t start = b * b4;
+      const int64_t len = std::min(b4, c->n4 - start);
       for (size_t k = 0; k < c->devs.size(); ++k) {
         Device &d = c->devs[k];
         HIP_TRY(hipSetDevice(d.hip_id));
-        if (b == nb - 1) TRY(mark(c, d, EV_AR));
+        cbx::LaunchConfig cfg = c->cfg;
+        cfg.num_cus = d.num_cus;
+        HIP_TRY(cbx::launch_sma_accumulate(offset_args(args[k], start, len), b == 0, cfg, d.stream));
+        if (pipelined) HIP_TRY(hipEventRecord(d.bucket_acc[b], d.stream));
+      }
+      return CBX_OK;
+    };
+    auto apply = [&](int64_t b) -> int {
+      const int64_t start = b * b4;
+      const int64_t len = std::min(b4, c->n4 - start);
+      for (size_t k = 0; k < c->devs.size(); ++k) {
+        Device &d = c->devs[k];
+        HIP_TRY(hipSetDevice(d.hip_id));
+        if (pipelined) HIP_TRY(hipStreamWaitEvent(d.stream, d.bucket_red[b], 0));
         cbx::LaunchConfig cfg = c->cfg;
         cfg.num_cus = d.num_cus;
         HIP_TRY(cbx::launch_sma_apply(offset_args(args[k], start, len), mom, cfg, d.stream));
       }
+      return CBX_OK;
+    };
+    if (!pipelined) {
+      TRY(accumulate(0));
+      for (Device &d : c->devs) {
+        HIP_TRY(hipSetDevice(d.hip_id));
+        TRY(mark(c, d, EV_A));
+      }
+      TRY(allreduce(0, false));
+      for (Device &d : c->devs) {
+        HIP_TRY(hipSetDevice(d.hip_id));
+        TRY(mark(c, d, EV_AR));
+      }
+      TRY(apply(0));
+    } else {
+      for (int64_t b = 0; b < nb; ++b) {
+        TRY(accumulate(b));
+        TRY(allreduce(b, true));
+        if (b > 0) TRY(apply(b - 1));
+      }
+      // The wait inside apply(nb-1) also joins every earlier all-reduce
+      // (comm_stream is in order) back into the sync stream.
+      TRY(apply(nb - 1));
     }
     for (size_t k = 0; k < c->devs.size(); ++k) {
       Device &d = c->devs[k];
       HIP_TRY(hipSetDevice(d.hip_id));
       TRY(mark(c, d, EV_B));
-      ring_advance(c, d, true);
+      ring_advance(c, d, pipelined ? 2 : 1);
     }
     c->last_step_split = true;
   }
@@ -883,7 +965,7 @@ int cbx_set_model_manager(cbx_context *c, int replicas, int type) {
   }
 
   const size_t data_bytes = (size_t)c->n4 * 16 + (size_t)cbx::kCtrlFloats * sizeof(float);
-  const size_t stride = (data_bytes + kAlign - 1) / kAlign * kAlign;
+  const size_t stride = (data_bytes + kAlign - 1) / kAlign * kAlign + kSlotStagger;
   for (Device &d : c->devs) {
     HIP_TRY(hipSetDevice(d.hip_id));
     d.stride = stride;
@@ -1305,8 +1387,9 @@ int cbx_last_timing(cbx_context *c, int local, float *ms) {
   for (int k = 0; k < CBX_T_COUNT; ++k) ms[k] = -1.0f;
   if (d.ring_count > 0) {
     const int slot = (d.ring_pos + Device::kRing - 1) % Device::kRing;
-    TRY(ring_span(d, slot, EV_START, EV_A, &ms[CBX_T_KERNEL]));
-    if (d.ring_split[slot]) {
+    const int kind = d.ring_split[slot];
+    if (kind != 2) TRY(ring_span(d, slot, EV_START, EV_A, &ms[CBX_T_KERNEL]));
+    if (kind == 1) {
       TRY(ring_span(d, slot, EV_A, EV_AR, &ms[CBX_T_ALLREDUCE]));
       TRY(ring_span(d, slot, EV_AR, EV_B, &ms[CBX_T_APPLY]));
     }
@@ -1337,7 +1420,9 @@ int cbx_timing_history(cbx_context *c, int local, int which, float *ms, int max)
     if (which == CBX_T_ALLREDUCE) { a = EV_A; b = EV_AR; }
     if (which == CBX_T_APPLY) { a = EV_AR; b = EV_B; }
     if (which == CBX_T_STEP) { a = EV_START; b = EV_B; }
-    if ((which == CBX_T_ALLREDUCE || which == CBX_T_APPLY) && !d.ring_split[slot]) {
+    const int kind = d.ring_split[slot];
+    if ((which == CBX_T_KERNEL && kind == 2) ||
+        ((which == CBX_T_ALLREDUCE || which == CBX_T_APPLY) && kind != 1)) {
       ms[k] = -1.0f;
       continue;
     }

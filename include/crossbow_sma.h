@@ -191,7 +191,7 @@ int cbx_step_event (cbx_context *ctx, int local, void **event);
 /* When enabled, HIP events bracket each launch on the sync stream.       */
 int cbx_set_timing (cbx_context *ctx, int enable);
 /* Milliseconds of the last step on local device `local`, CBX_T_COUNT floats
- * (blocks on the recorded events).                                        */
+ * (blocks on the recorded events); -1 for a span the step did not have.   */
 int cbx_last_timing (cbx_context *ctx, int local, float *ms);
 /* Per-launch history of the last steps (up to 1024) on local device `local`:
  * `which` is CBX_T_KERNEL, CBX_T_ALLREDUCE, CBX_T_APPLY or CBX_T_STEP; fills
@@ -202,7 +202,10 @@ int cbx_timing_history (cbx_context *ctx, int local, int which, float *ms, int m
  * load/store policy (0 plain, 1 nontemporal), float4s per thread per trip. */
 int cbx_set_kernel_config (cbx_context *ctx, int block, int blocks_per_cu, int policy, int unroll);
 /* Bucketed pipeline for G > 1: kernel A / all-reduce / kernel B per bucket
- * of `bucket_elements` floats (0 = one bucket).                           */
+ * of `bucket_elements` floats; 0 (default) = 8 buckets when G > 1, one at
+ * G = 1; a value >= n = one bucket, all in order on the sync stream.  With
+ * more than one bucket the all-reduce of bucket k runs on a second stream
+ * beside kernel A of bucket k+1, and only CBX_T_STEP is timed per step.  */
 int cbx_set_bucket_elements (cbx_context *ctx, long long bucket_elements);
 /* Force the multi-GPU pipeline (kernel A + RCCL all-reduce + kernel B) even
  * at G = 1 (a one-rank communicator), so a single-GPU host exercises it.  */

@@ -1,0 +1,324 @@
+// membench.hip -- exploration microbenchmark for the fused SMA kernel's
+// memory shape on one MI355X (not part of the product library).
+//
+// Workload C3: n = 25,557,032 fp32, R = 8 replicas, momentum on:
+// 18 read streams (z, last, 8 s, 8 w) and 10 write streams (8 w, z, last).
+// Measures ceilings (copy, read-only, write-only) and fused-kernel variants
+// over buffer layouts (arena stagger) and launch shapes.  Prints one JSON
+// line per variant.  Build: hipcc --offload-arch=gfx950 -O3 -o membench membench.hip
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+#define CK(x)                                                                                   \
+  do {                                                                                          \
+    hipError_t e_ = (x);                                                                        \
+    if (e_ != hipSuccess) {                                                                     \
+      std::fprintf(stderr, "%s:%d %s: %s\n", __FILE__, __LINE__, #x, hipGetErrorString(e_)); \
+      std::exit(2);                                                                             \
+    }                                                                                           \
+  } while (0)
+
+typedef float v4f __attribute__((ext_vector_type(4)));
+
+constexpr int R = 8;
+
+struct Args {
+  const v4f *s[R];
+  v4f *w[R];
+  v4f *z;
+  v4f *last;
+  uint32_t n4;
+  float alpha;
+};
+
+template <int P>
+__device__ __forceinline__ v4f ld(const v4f *p) {
+  if constexpr (P == 1) return __builtin_nontemporal_load(p);
+  else return *p;
+}
+template <int P>
+__device__ __forceinline__ void st(v4f *p, v4f v) {
+  if constexpr (P == 1) __builtin_nontemporal_store(v, p);
+  else *p = v;
+}
+__device__ __forceinline__ v4f vfma(v4f a, v4f b, v4f c) { return __builtin_elementwise_fma(a, b, c); }
+
+// PL / PS: load / store policy (0 plain, 1 nontemporal).
+// ORDER 0: all s, all w loads first.  ORDER 1: s_i, w_i interleaved.
+// ORDER 2: per replica load-compute-store.
+// WC: wave-contiguous (lane l of a wave handles float4s wbase + l + 64u, so a
+// wave touches 64*U*16 contiguous bytes per stream) instead of block-strided.
+template <int PL, int PS, int ORDER, int U, bool WC>
+__global__ __launch_bounds__(1024) void fused(const Args a) {
+  const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+  const uint32_t stride_u = WC ? 64u : blockDim.x;
+  const uint32_t first = WC ? (blockIdx.x * blockDim.x * U + wave * 64u * U + lane)
+                            : (blockIdx.x * blockDim.x * U + threadIdx.x);
+  const v4f al = a.alpha, nal = -a.alpha, mb = 0.9f, one = 1.0f, mone = -1.0f;
+  const uint32_t base = first;
+  if (base >= a.n4) return;
+  v4f zv[U], lv[U], acc[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const uint32_t i = base + u * stride_u;
+    zv[u] = ld<PL>(a.z + i);
+    lv[u] = ld<PL>(a.last + i);
+    acc[u] = 0.0f;
+  }
+  if constexpr (ORDER == 2) {
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const uint32_t i = base + u * stride_u;
+        v4f s = ld<PL>(a.s[r] + i), w = ld<PL>(a.w[r] + i);
+        v4f d = vfma(mone, zv[u], s);
+        st<PS>(a.w[r] + i, vfma(nal, d, w));
+        acc[u] = vfma(al, d, acc[u]);
+      }
+    }
+  } else {
+    v4f sv[U][R], wv[U][R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const uint32_t i = base + u * stride_u;
+        sv[u][r] = ld<PL>(a.s[r] + i);
+        if constexpr (ORDER == 1) wv[u][r] = ld<PL>(a.w[r] + i);
+      }
+    }
+    if constexpr (ORDER == 0) {
+#pragma unroll
+      for (int r = 0; r < R; ++r)
+#pragma unroll
+        for (int u = 0; u < U; ++u) wv[u][r] = ld<PL>(a.w[r] + base + u * stride_u);
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        v4f d = vfma(mone, zv[u], sv[u][r]);
+        wv[u][r] = vfma(nal, d, wv[u][r]);
+        acc[u] = vfma(al, d, acc[u]);
+      }
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+#pragma unroll
+      for (int u = 0; u < U; ++u) st<PS>(a.w[r] + base + u * stride_u, wv[u][r]);
+  }
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const uint32_t i = base + u * stride_u;
+    v4f D = vfma(mb, lv[u], acc[u]);
+    st<PS>(a.last + i, D);
+    st<PS>(a.z + i, vfma(one, D, zv[u]));
+  }
+}
+
+template <int P>
+__global__ __launch_bounds__(1024) void copyk(v4f *dst, const v4f *src, uint32_t n4) {
+  const uint32_t stride = gridDim.x * blockDim.x;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) st<P>(dst + i, ld<P>(src + i));
+}
+
+// Read-only: 18 streams, one float4 each per thread (one trip).
+template <int P>
+__global__ __launch_bounds__(1024) void readk(const Args a, float *sink) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= a.n4) return;
+  v4f t = ld<P>(a.z + i) + ld<P>(a.last + i);
+#pragma unroll
+  for (int r = 0; r < R; ++r) t += ld<P>(a.s[r] + i) + ld<P>(a.w[r] + i);
+  if (t.x == 12345.678f) sink[0] = t.y;
+}
+
+// Write-only: 10 streams, one trip.
+template <int P>
+__global__ __launch_bounds__(1024) void writek(const Args a) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= a.n4) return;
+  const v4f v = (float)i;
+  st<P>(a.z + i, v);
+  st<P>(a.last + i, v);
+#pragma unroll
+  for (int r = 0; r < R; ++r) st<P>(a.w[r] + i, v);
+}
+
+
+// ---- v3: library-style kernel (SGPR base + 32-bit lane offset), min-waves
+// hint MW (caps VGPRs), optional XCD-aware block remap, no-dependency mix.
+template <int P>
+__device__ __forceinline__ v4f ldo(const v4f *b, uint32_t off) {
+  return ld<P>(reinterpret_cast<const v4f *>(reinterpret_cast<const char *>(b) + off));
+}
+template <int P>
+__device__ __forceinline__ void sto(v4f *b, uint32_t off, v4f v) {
+  st<P>(reinterpret_cast<v4f *>(reinterpret_cast<char *>(b) + off), v);
+}
+template <int MW, bool XCD>
+__global__ __launch_bounds__(256, MW) void fused3(const Args a) {
+  uint32_t blk = blockIdx.x;
+  if constexpr (XCD) {
+    // blocks b, b+8, ... share an XCD: give each XCD one contiguous range.
+    const uint32_t per = gridDim.x / 8, full = per * 8;
+    if (blockIdx.x < full) blk = (blockIdx.x & 7u) * per + (blockIdx.x >> 3);
+  }
+  const uint32_t e = blk * blockDim.x + threadIdx.x;
+  if (e >= a.n4) return;
+  const uint32_t i = e * 16u;
+  const v4f al = a.alpha, nal = -a.alpha, mb = 0.9f, one = 1.0f, mone = -1.0f;
+  v4f zv = ldo<1>(a.z, i), lv = ldo<1>(a.last, i), acc = 0.0f;
+  v4f sv[R], wv[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) sv[r] = ldo<1>(a.s[r], i);
+#pragma unroll
+  for (int r = 0; r < R; ++r) wv[r] = ldo<1>(a.w[r], i);
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    v4f d = vfma(mone, zv, sv[r]);
+    wv[r] = vfma(nal, d, wv[r]);
+    acc = vfma(al, d, acc);
+  }
+#pragma unroll
+  for (int r = 0; r < R; ++r) sto<1>(a.w[r], i, wv[r]);
+  v4f D = vfma(mb, lv, acc);
+  sto<1>(a.last, i, D);
+  sto<1>(a.z, i, vfma(one, D, zv));
+}
+
+// Same memory shape, stores independent of loads (loads kept alive by a
+// never-taken sink store): the DRAM read/write mix without the dependency.
+__global__ __launch_bounds__(256) void mixnodep(const Args a, float *sink) {
+  const uint32_t e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= a.n4) return;
+  const uint32_t i = e * 16u;
+  const v4f v = (float)e;
+  sto<1>(a.z, i, v);
+  sto<1>(a.last, i, v);
+#pragma unroll
+  for (int r = 0; r < R; ++r) sto<1>(a.w[r], i, v);
+  v4f t = ldo<1>(a.z, i + 0) ;
+  t += ldo<1>(a.last, i);
+#pragma unroll
+  for (int r = 0; r < R; ++r) t += ldo<1>(a.s[r], i) + ldo<1>(a.w[r], i);
+  if (t.x == 12345.678f) sink[0] = t.y;
+}
+
+static hipEvent_t e0, e1;
+
+template <typename F>
+static float time_ms(F launch, int iters) {
+  for (int k = 0; k < 3; ++k) launch();
+  CK(hipDeviceSynchronize());
+  std::vector<float> t;
+  for (int k = 0; k < iters; ++k) {
+    CK(hipEventRecord(e0, 0));
+    launch();
+    CK(hipEventRecord(e1, 0));
+    CK(hipEventSynchronize(e1));
+    float ms;
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    t.push_back(ms);
+  }
+  std::sort(t.begin(), t.end());
+  return t[t.size() / 2];
+}
+
+int main(int argc, char **argv) {
+  const int64_t n = 25557032;
+  const uint32_t n4 = (uint32_t)(((n + 3) / 4 + 1023) / 1024 * 1024);
+  const int iters = argc > 1 ? std::atoi(argv[1]) : 20;
+  CK(hipSetDevice(0));
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  int cus = 256;
+  {
+    hipDeviceProp_t p;
+    CK(hipGetDeviceProperties(&p, 0));
+    cus = p.multiProcessorCount;
+  }
+  const size_t buf = (size_t)n4 * 16;
+  const int nbuf = 2 + 2 * R;
+  // One big arena; layouts carve it with different strides/staggers.
+  const size_t max_stagger = 4u << 20;
+  const size_t arena_bytes = std::max((size_t)nbuf * (buf + (2u << 20) + max_stagger) + (64u << 20),
+                                      ((size_t)2 << 30) + (8u << 20));
+  char *arena;
+  CK(hipMalloc(&arena, arena_bytes));
+  CK(hipMemset(arena, 0, arena_bytes));
+  float *sink;
+  CK(hipMalloc(&sink, 64));
+  const double alg = (12.0 * R + 16.0) * (double)n;
+
+  struct Layout {
+    const char *name;
+    size_t stride_align;
+    size_t stagger;
+  };
+  std::vector<Layout> layouts = {
+      {"2MiB-aligned", 2u << 20, 0}, {"packed-256B", 256, 0}, {"stagger-4KiB", 2u << 20, 4096},
+  };
+
+  // Ceilings on the same arena (1 GiB copy).
+  {
+    const uint32_t cn4 = (uint32_t)((1u << 30) / 16);
+    v4f *a = (v4f *)arena, *b = (v4f *)(arena + (1u << 30) + (2u << 20));
+    for (int blk : {256, 512}) {
+      unsigned g = (cn4 + blk - 1) / blk;
+      float ms = time_ms([&] { hipLaunchKernelGGL(copyk<1>, dim3(g), dim3(blk), 0, 0, b, a, cn4); }, iters);
+      std::printf("{\"kind\":\"copy-nt\",\"block\":%d,\"ms\":%.4f,\"GBs\":%.1f}\n", blk, ms, 2.0 * cn4 * 16 / ms / 1e6);
+      ms = time_ms([&] { hipLaunchKernelGGL(copyk<0>, dim3(g), dim3(blk), 0, 0, b, a, cn4); }, iters);
+      std::printf("{\"kind\":\"copy-plain\",\"block\":%d,\"ms\":%.4f,\"GBs\":%.1f}\n", blk, ms, 2.0 * cn4 * 16 / ms / 1e6);
+    }
+    for (int wpc : {4, 8, 16}) {
+      unsigned g = cus * wpc;
+      float ms = time_ms([&] { hipLaunchKernelGGL(copyk<1>, dim3(g), dim3(256), 0, 0, b, a, cn4); }, iters);
+      std::printf("{\"kind\":\"copy-nt-gridstride\",\"wg_per_cu\":%d,\"ms\":%.4f,\"GBs\":%.1f}\n", wpc, ms,
+                  2.0 * cn4 * 16 / ms / 1e6);
+    }
+  }
+
+  for (int round = 0; round < 2; ++round)
+  for (const Layout &L : layouts) {
+    const size_t stride = (buf + L.stride_align - 1) / L.stride_align * L.stride_align + L.stagger;
+    Args a;
+    std::vector<char *> p(nbuf);
+    for (int k = 0; k < nbuf; ++k) p[k] = arena + (size_t)k * stride;
+    a.z = (v4f *)p[0];
+    a.last = (v4f *)p[1];
+    for (int r = 0; r < R; ++r) {
+      a.s[r] = (const v4f *)p[2 + 2 * r];
+      a.w[r] = (v4f *)p[3 + 2 * r];
+    }
+    a.n4 = n4;
+    a.alpha = 0.1f;
+    auto run = [&](const char *kind, auto kern, int blk, int U) {
+      const unsigned grid = n4 / (blk * U);
+      float ms = time_ms([&] { hipLaunchKernelGGL(kern, dim3(grid), dim3(blk), 0, 0, a); }, iters);
+      std::printf("{\"round\":%d,\"layout\":\"%s\",\"kind\":\"%s\",\"block\":%d,\"U\":%d,\"ms\":%.4f,\"GBs\":%.1f}\n",
+                  round, L.name, kind, blk, U, ms, alg / ms / 1e6);
+    };
+    for (int blk : {64, 128, 256}) {
+      run("lib", fused3<1, false>, blk, 1);
+    }
+    if (L.stagger != 0) continue;
+    for (int blk : {128, 256}) {
+      run("lib-xcd", fused3<1, true>, blk, 1);
+      run("lib-mw5", fused3<5, false>, blk, 1);
+      run("lib-mw6", fused3<6, false>, blk, 1);
+      run("lib-mw8", fused3<8, false>, blk, 1);
+      run("o2-128", fused<1, 1, 2, 1, false>, blk, 1);
+      float ms = time_ms([&] { hipLaunchKernelGGL(mixnodep, dim3(n4 / blk), dim3(blk), 0, 0, a, sink); }, iters);
+      std::printf("{\"round\":%d,\"layout\":\"%s\",\"kind\":\"mixnodep\",\"block\":%d,\"ms\":%.4f,\"GBs\":%.1f}\n", round, L.name, blk, ms, alg / ms / 1e6);
+    }
+  }
+  CK(hipFree(arena));
+  CK(hipFree(sink));
+  return 0;
+}

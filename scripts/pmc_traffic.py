@@ -1,0 +1,85 @@
+#!/usr/bin/env python3
+"""HBM traffic per launch of the SMA kernels from rocprofv3 PMC passes.
+
+Reads the ``*_counter_collection.csv`` files of separate ``rocprofv3 --pmc``
+passes (one counter group per pass: FETCH_SIZE in one, WRITE_SIZE in another,
+as MI355X_MICROARCH.md "rocprofv3 PMC slots" requires) and writes, per kernel,
+the mean bytes per dispatch.  gfx950 corrections (MI355X_MICROARCH.md "HBM"):
+
+* FETCH_SIZE (KiB) reports half the bytes of a wide (16 B/lane) coalesced
+  streaming read, so read bytes = 2 * FETCH_SIZE * 1024;
+* WRITE_SIZE (KiB) is exact for 16 B/lane streaming stores.
+
+hbm_bytes_per_launch = 2 * FETCH_SIZE * 1024 + WRITE_SIZE * 1024.
+
+Usage: pmc_traffic.py --out traffic.json --key-suffix resnet50/R8/m1 DIR [DIR...]
+"""
+from __future__ import annotations
+
+import argparse
+import csv
+import glob
+import json
+import os
+import re
+from collections import defaultdict
+
+
+def short_name(kernel: str) -> str:
+    m = re.search(r"(sma_\w+_kernel|copy_kernel|fill_normal_kernel)", kernel)
+    return m.group(1) if m else kernel.split("(")[0]
+
+
+def collect(dirs):
+    # (kernel, counter) -> list of per-dispatch values
+    vals = defaultdict(list)
+    for d in dirs:
+        for path in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+            per_dispatch = defaultdict(float)
+            with open(path, newline="") as f:
+                for row in csv.DictReader(f):
+                    k = (short_name(row["Kernel_Name"]), row["Counter_Name"], row.get("Dispatch_Id", ""))
+                    per_dispatch[k] += float(row["Counter_Value"])  # sum over dimensions, if any
+            for (kern, ctr, _), v in per_dispatch.items():
+                vals[(kern, ctr)].append(v)
+    return vals
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("--out", required=True)
+    p.add_argument("--key-suffix", required=True, help="e.g. resnet50/R8/m1 (matches bench.py)")
+    p.add_argument("--alg-bytes", type=float, default=None, help="algorithmic bytes per launch, for the ratio")
+    p.add_argument("dirs", nargs="+")
+    a = p.parse_args()
+    vals = collect(a.dirs)
+    kernels = sorted({k for k, _ in vals})
+    out = {}
+    if os.path.exists(a.out):
+        with open(a.out) as f:
+            out = json.load(f)
+    for kern in kernels:
+        rec = {}
+        for (k, ctr), v in vals.items():
+            if k == kern and v:
+                rec[ctr] = {"mean": sum(v) / len(v), "dispatches": len(v)}
+        fetch = rec.get("FETCH_SIZE", {}).get("mean")
+        write = rec.get("WRITE_SIZE", {}).get("mean")
+        entry = {"counters": rec}
+        if fetch is not None and write is not None:
+            entry["read_bytes_per_launch"] = 2 * fetch * 1024
+            entry["write_bytes_per_launch"] = write * 1024
+            entry["hbm_bytes_per_launch"] = 2 * fetch * 1024 + write * 1024
+            if a.alg_bytes:
+                entry["alg_bytes_per_launch"] = a.alg_bytes
+                entry["traffic_over_alg"] = entry["hbm_bytes_per_launch"] / a.alg_bytes
+        entry["correction"] = "read = 2*FETCH_SIZE KiB (gfx950 half-count of 16B/lane streams), write = WRITE_SIZE KiB"
+        out[f"{kern}/{a.key_suffix}"] = entry
+    os.makedirs(os.path.dirname(os.path.abspath(a.out)), exist_ok=True)
+    with open(a.out, "w") as f:
+        json.dump(out, f, indent=1, sort_keys=True)
+    print(json.dumps(out, indent=1, sort_keys=True))
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,90 @@
+"""C-ABI boundary checks that need no GPU.
+
+* every function ``include/crossbow_sma.h`` declares is exported by
+  ``libcrossbow_sma.so`` and bound by ``crossbow_amd._lib`` (and vice versa);
+* the JNI shim defines every Java native of the model path that
+  ``TheGPU.java:268-354`` declares (names as javah mangles them);
+* on a host without an MI355X the product path fails loudly
+  (``CBX_ERR_NO_DEVICE``) instead of falling back to the CPU.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import re
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "crossbow_sma.h")
+JNI_SRC = os.path.join(ROOT, "crossbow_amd", "csrc", "jni", "TheGPU_jni.c")
+
+
+def declared_functions():
+    text = open(HEADER).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(cbx_[a-z0-9_]+)\s*\(", text)))
+
+
+def test_header_declares_the_barrier_path():
+    names = declared_functions()
+    for must in ("cbx_init", "cbx_init_rank", "cbx_set_model", "cbx_set_model_variable",
+                 "cbx_set_model_manager", "cbx_lock_any", "cbx_merge", "cbx_synchronise",
+                 "cbx_unlock_any", "cbx_checkpoint_model", "cbx_override_model_data", "cbx_free"):
+        assert must in names
+
+
+def test_library_exports_every_declared_symbol():
+    from crossbow_amd import _lib
+    lib = _lib.load()
+    raw = ctypes.CDLL(_lib.LIB_PATH)
+    missing = [n for n in declared_functions() if not hasattr(raw, n)]
+    assert not missing, f"declared in crossbow_sma.h but not exported: {missing}"
+    unbound = [n for n in declared_functions() if n not in _lib.SIGNATURES]
+    assert not unbound, f"declared but not bound in _lib.SIGNATURES: {unbound}"
+    extra = [n for n in _lib.SIGNATURES if n not in declared_functions()]
+    assert not extra, f"bound in _lib but not declared in the header: {extra}"
+    assert lib.cbx_abi_version() == 1
+
+
+def test_no_device_fails_loudly():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is visible; this checks the no-device behaviour")
+    from crossbow_amd import CbxError, TheGPU, _lib
+    assert TheGPU.device_count() == 0
+    g = TheGPU()
+    with pytest.raises(CbxError) as e:
+        g.init([0])
+    assert e.value.code == _lib.CBX_ERR_NO_DEVICE
+
+
+def test_null_context_is_an_error_not_a_crash():
+    from crossbow_amd import _lib
+    lib = _lib.load()
+    assert lib.cbx_set_model(None, 1, 16) == _lib.CBX_ERR_INVALID
+    assert lib.cbx_lock_any(None) == _lib.CBX_ERR_INVALID
+    assert lib.cbx_synchronise(None, 0, 1, 0, 0) == _lib.CBX_ERR_INVALID
+    assert "null context" in _lib.last_error()
+    assert lib.cbx_free(None) == _lib.CBX_OK
+
+
+# The model-path natives of TheGPU.java (:268-354) the shim must export.
+JNI_NATIVES = [
+    "init", "free", "setModel", "setModelVariable", "setModelVariableBuffer", "setModelWorkPerClock",
+    "setUpdateModelType", "setLearningRateDecayPolicyFixed", "setLearningRateDecayPolicyInv",
+    "setLearningRateDecayPolicyStep", "setLearningRateDecayPolicyMultiStep", "setLearningRateDecayPolicyExp",
+    "setBaseModelMomentum", "setMomentum", "setWeightDecay", "setEamsgdAlpha", "setEamsgdTau",
+    "setModelManager", "lockAny", "merge", "synchronise", "unlockAny", "checkpointModel",
+    "overrideModelData", "addModel", "delModel",
+]
+
+
+def test_jni_shim_defines_model_path_natives():
+    src = open(JNI_SRC).read()
+    defined = set(re.findall(r"NATIVE\(\s*\w+\s*,\s*(\w+)\s*\)", src))
+    missing = [n for n in JNI_NATIVES if n not in defined]
+    assert not missing, f"JNI shim lacks {missing}"
+    # Every native forwards to a declared C-ABI function.
+    used = set(re.findall(r"\b(cbx_[a-z0-9_]+)\s*\(", src))
+    assert used <= set(declared_functions()), used - set(declared_functions())

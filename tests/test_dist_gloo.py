@@ -1,0 +1,142 @@
+"""The G > 1 path, rehearsed on CPU with two gloo ranks (no GPU needed).
+
+Each rank owns the replicas ``i % G == rank`` (clib-multigpu/modelmanager.c:
+51-64, ``crossbow_amd.dist.local_replicas``), runs Phase A over its locked
+replicas in id order (the oracle's kernel-A restatement), all-reduces
+``acc`` together with the Phase-D copy count in a control slot in front of
+it (what ``libcrossbow_sma`` sends through RCCL), and applies Phase C / D.
+The result on every rank must equal the single-address-space G = 2 oracle
+(clib-multigpu/synch/sma.c:13-231): with two ranks the fp32 sum a + b is
+order independent, so the comparison is bit for bit.  The control plane of
+``crossbow_amd.dist`` (unique-id broadcast, barrier, max over ranks) runs
+over the same gloo group.
+"""
+from __future__ import annotations
+
+import os
+import socket
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+CASES = [
+    # (n, R per rank, alpha, momentum, copy ids, unlocked ids, first)
+    (4099, 2, 0.1, 0.9, [], [], 0),
+    (1031, 3, 0.5, 0.0, [3], [], 0),
+    (2053, 2, 0.1, 0.9, [], [1], 0),
+    (777, 2, 0.1, 0.9, [0], [], 1),
+]
+
+
+def _rank_main(rank, world, port, q):
+    import sys
+    sys.path.insert(0, ROOT)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    try:
+        import torch
+        import torch.distributed as dist
+
+        from crossbow_amd import dist as D
+        from oracle import oracle as O
+
+        D.init(world, rank, backend="gloo")
+        uid = D.share_unique_id(rank, world, lambda: bytes(range(128)))
+        assert uid == bytes(range(128))
+        assert D.max_over_ranks(float(rank + 1), world) == float(world)
+        D.barrier(world)
+
+        results = []
+        for (n, R, alpha, mom, copy_ids, unlocked, first) in CASES:
+            ref = O.make_state(n, world, R, alpha, mom)
+            for i in copy_ids:
+                ref.copy[i] = 1
+            for i in unlocked:
+                ref.locked[i] = 0
+            ref.first = first
+            mine = ref.clone()
+            O.sma_step(ref)  # single address space, G = world
+
+            ids = [i for i in D.local_replicas(mine.size, world, rank)
+                   if i >= first and mine.locked[i]]
+            z = mine.z[rank]
+            last = mine.last[rank] if mine.last is not None else None
+            s = [mine.s[i] for i in ids]
+            w = [mine.w[i] for i in ids]
+            acc, copies = O.sma_accumulate(alpha, z, s, w, [int(mine.copy[i]) for i in ids])
+            # control slot in front of acc, summed with it (context.hip, sma_internal.h)
+            buf = torch.from_numpy(np.concatenate([np.array([copies], np.float32), acc]))
+            dist.all_reduce(buf, op=dist.ReduceOp.SUM)
+            ctrl, Dsum = float(buf[0]), buf[1:].numpy().copy()
+            O.sma_apply(mom, Dsum, z, last, w, ctrl > 0)
+
+            ok = bool(np.array_equal(z.view(np.uint32), ref.z[rank].view(np.uint32)))
+            if last is not None:
+                ok &= bool(np.array_equal(last.view(np.uint32), ref.last[rank].view(np.uint32)))
+            for k, i in enumerate(ids):
+                ok &= bool(np.array_equal(w[k].view(np.uint32), ref.w[i].view(np.uint32)))
+            # replicas that did not take part are untouched
+            for i in D.local_replicas(mine.size, world, rank):
+                if i not in ids:
+                    ok &= bool(np.array_equal(mine.w[i], ref.w[i]))
+            results.append(ok)
+        D.barrier(world)
+        D.finalize(world)
+        q.put((rank, results, None))
+    except Exception as e:  # pragma: no cover - reported to the parent
+        import traceback
+        q.put((rank, None, traceback.format_exc()))
+
+
+def test_two_rank_sharded_sma_equals_single_process_oracle():
+    import torch.multiprocessing as mp
+    from oracle import oracle as O
+    O.lib()  # build the oracle before forking ranks
+    world = 2
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_rank_main, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = {}
+    try:
+        for _ in range(world):
+            rank, res, err = q.get(timeout=240)
+            out[rank] = (res, err)
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
+    for rank in range(world):
+        res, err = out[rank]
+        assert err is None, f"rank {rank} failed:\n{err}"
+        assert all(res), f"rank {rank}: per-case parity {res} (cases {CASES})"
+
+
+def test_local_replicas_round_robin():
+    from crossbow_amd import dist as D
+    assert D.local_replicas(8, 4, 1) == [1, 5]
+    assert D.local_replicas(32, 8, 7) == [7, 15, 23, 31]
+    assert sorted(sum((D.local_replicas(12, 3, r) for r in range(3)), [])) == list(range(12))
+
+
+def test_env_rank_defaults(monkeypatch):
+    from crossbow_amd import dist as D
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK"):
+        monkeypatch.delenv(k, raising=False)
+    assert D.env_rank() == (0, 1, 0)
+    monkeypatch.setenv("RANK", "3")
+    monkeypatch.setenv("WORLD_SIZE", "8")
+    monkeypatch.setenv("LOCAL_RANK", "3")
+    assert D.env_rank() == (3, 8, 3)

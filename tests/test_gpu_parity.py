@@ -127,6 +127,41 @@ def test_split_pipeline_buckets_and_copy():
     _run(300_001, 3, 0.1, 0.9, split=True, bucket=65_536, copy_ids=(0,), steps=2)
 
 
+@pytest.mark.parametrize("bucket", [4096, 1_000_000])
+def test_split_pipeline_many_buckets_two_streams(bucket):
+    # 4096-element buckets -> ~245 buckets per step on two streams with
+    # per-bucket events reused across steps; 1e6 > n -> one in-order bucket.
+    _run(1_000_003, 2, 0.5, 0.9, split=True, bucket=bucket, steps=3)
+
+
+def test_pipelined_timing_spans():
+    from crossbow_amd import _lib
+    n, R = 200_000, 2
+    g = make_gpu(n, R, 0.1, 0.9)
+    try:
+        g.set_force_split(True)
+        g.set_bucket_elements(16_384)
+        g.fill_synthetic(7)
+        g.set_timing(True)
+        for c in range(3):
+            g.lockAny()
+            g.synchronise(0, c, 0, False)
+            g.unlockAny()
+        g.wait()
+        t = g.last_timing(0)
+        assert t[_lib.T_KERNEL] == -1 and t[_lib.T_ALLREDUCE] == -1 and t[_lib.T_STEP] > 0
+        assert all(x == -1 for x in g.timing_history(_lib.T_KERNEL))
+        assert all(x > 0 for x in g.timing_history(_lib.T_STEP))
+        g.set_bucket_elements(1 << 40)
+        g.lockAny()
+        g.synchronise(0, 4, 0, False)
+        g.unlockAny()
+        t = g.last_timing(0)
+        assert t[_lib.T_KERNEL] > 0 and t[_lib.T_ALLREDUCE] > 0 and t[_lib.T_APPLY] > 0
+    finally:
+        g.free()
+
+
 def test_multiple_steps_drift():
     _run(50_000, 4, 0.1, 0.9, steps=3)
 
