@@ -182,7 +182,8 @@ struct Device {
   size_t arena_bytes = 0;
   size_t stride = 0;  // bytes per buffer slot
   std::vector<int> replicas;  // global ids, increasing
-  hipEvent_t synched = nullptr;  // end of the last step (cbx_step_event)
+  hipEvent_t synched = nullptr;     // end-of-step marker when timing is off
+  hipEvent_t step_event = nullptr;  // end of the last step (cbx_step_event)
   hipEvent_t ev[EV_COUNT] = {};
   bool ev_valid[EV_COUNT] = {};
   // Per-step timing ring: events {START, A, AR, B} of the last kRing steps,
@@ -373,7 +374,14 @@ void close_device(Device &d) {
   d = Device();
 }
 
-// Record a timing event when timing is enabled.  Step events (START..B) go
+// The current ring slot's event `ev` (START..B) when timing is enabled, for
+// a dispatch to timestamp itself (hipExtLaunchKernelGGL); else nullptr.
+hipEvent_t ring_event(cbx_context *c, Device &d, int ev) {
+  if (!c->timing || d.ring.empty()) return nullptr;
+  return d.ring[(size_t)d.ring_pos * 4 + ev];
+}
+
+// Record a timing marker when timing is enabled.  Step events (START..B) go
 // to the current ring slot, staging events to the fixed ones.
 int mark(cbx_context *c, Device &d, int ev) {
   if (!c->timing) return CBX_OK;
@@ -472,10 +480,10 @@ int sma_step(cbx_context *c, int first) {
     HIP_TRY(hipSetDevice(d.hip_id));
     cbx::LaunchConfig cfg = c->cfg;
     cfg.num_cus = d.num_cus;
-    TRY(mark(c, d, EV_START));
-    HIP_TRY(cbx::launch_sma_fused(args[0], mom, copies_total > 0, cfg, d.stream));
-    TRY(mark(c, d, EV_A));
-    TRY(mark(c, d, EV_B));
+    // The dispatch timestamps its own (start, stop) ring events: no marker
+    // packets between steps (each costs ~3 us of stream time, membench v4).
+    HIP_TRY(cbx::launch_sma_fused(args[0], mom, copies_total > 0, cfg, d.stream,
+                                  {ring_event(c, d, EV_START), ring_event(c, d, EV_A)}));
     ring_advance(c, d, 0);
     c->last_step_split = false;
   } else {
@@ -498,7 +506,6 @@ int sma_step(cbx_context *c, int first) {
     for (size_t k = 0; k < c->devs.size(); ++k) {
       Device &d = c->devs[k];
       HIP_TRY(hipSetDevice(d.hip_id));
-      TRY(mark(c, d, EV_START));
       if (pipelined) {
         while ((int64_t)d.bucket_acc.size() < nb) {
           hipEvent_t ea, er;
@@ -553,7 +560,10 @@ int sma_step(cbx_context *c, int first) {
         HIP_TRY(hipSetDevice(d.hip_id));
         cbx::LaunchConfig cfg = c->cfg;
         cfg.num_cus = d.num_cus;
-        HIP_TRY(cbx::launch_sma_accumulate(offset_args(args[k], start, len), b == 0, cfg, d.stream));
+        cbx::Timing t;
+        if (b == 0) t.start = ring_event(c, d, EV_START);
+        if (!pipelined) t.stop = ring_event(c, d, EV_A);
+        HIP_TRY(cbx::launch_sma_accumulate(offset_args(args[k], start, len), b == 0, cfg, d.stream, t));
         if (pipelined) HIP_TRY(hipEventRecord(d.bucket_acc[b], d.stream));
       }
       return CBX_OK;
@@ -567,16 +577,14 @@ int sma_step(cbx_context *c, int first) {
         if (pipelined) HIP_TRY(hipStreamWaitEvent(d.stream, d.bucket_red[b], 0));
         cbx::LaunchConfig cfg = c->cfg;
         cfg.num_cus = d.num_cus;
-        HIP_TRY(cbx::launch_sma_apply(offset_args(args[k], start, len), mom, cfg, d.stream));
+        cbx::Timing t;
+        if (b == nb - 1) t.stop = ring_event(c, d, EV_B);
+        HIP_TRY(cbx::launch_sma_apply(offset_args(args[k], start, len), mom, cfg, d.stream, t));
       }
       return CBX_OK;
     };
     if (!pipelined) {
       TRY(accumulate(0));
-      for (Device &d : c->devs) {
-        HIP_TRY(hipSetDevice(d.hip_id));
-        TRY(mark(c, d, EV_A));
-      }
       TRY(allreduce(0, false));
       for (Device &d : c->devs) {
         HIP_TRY(hipSetDevice(d.hip_id));
@@ -593,12 +601,7 @@ int sma_step(cbx_context *c, int first) {
       // (comm_stream is in order) back into the sync stream.
       TRY(apply(nb - 1));
     }
-    for (size_t k = 0; k < c->devs.size(); ++k) {
-      Device &d = c->devs[k];
-      HIP_TRY(hipSetDevice(d.hip_id));
-      TRY(mark(c, d, EV_B));
-      ring_advance(c, d, pipelined ? 2 : 1);
-    }
+    for (Device &d : c->devs) ring_advance(c, d, pipelined ? 2 : 1);
     c->last_step_split = true;
   }
 
@@ -606,11 +609,19 @@ int sma_step(cbx_context *c, int first) {
   // replica->updated per replica (sma.c:115,222) at points that, in this
   // pipeline, are all the same: the end of the step on the sync stream.  One
   // event per device stands for all of them (cbx_step_event); each extra
-  // record is a marker packet costing GPU time between steps.
+  // record is a marker packet costing GPU time between steps.  With timing
+  // on, the step's last dispatch already timestamps a ring event at its end;
+  // that event is the step event and no marker is added.
   for (size_t k = 0; k < c->devs.size(); ++k) {
     Device &d = c->devs[k];
     HIP_TRY(hipSetDevice(d.hip_id));
-    HIP_TRY(hipEventRecord(d.synched, d.stream));
+    if (c->timing && !d.ring.empty()) {
+      const int prev = (d.ring_pos + Device::kRing - 1) % Device::kRing;
+      d.step_event = d.ring[(size_t)prev * 4 + (d.ring_split[prev] == 0 ? EV_A : EV_B)];
+    } else {
+      HIP_TRY(hipEventRecord(d.synched, d.stream));
+      d.step_event = d.synched;
+    }
     for (int id : d.replicas) {
       if (id < first || !c->locked[id]) continue;
       c->replicas[id]->conf.copy = 0;  // sma.c:220 (a no-op unless a copy happened)
@@ -986,6 +997,7 @@ int cbx_set_model_manager(cbx_context *c, int replicas, int type) {
       HIP_TRY(hipMemcpyAsync(replica_dev(d, r, CBX_BUF_DATA), z, (size_t)c->n * 4, hipMemcpyDeviceToDevice, d.stream));
     }
     HIP_TRY(hipEventRecord(d.synched, d.stream));
+    d.step_event = d.synched;
     HIP_TRY(hipStreamSynchronize(d.stream));
   }
   c->manager = true;
@@ -1357,7 +1369,7 @@ int cbx_wait(cbx_context *c) {
 int cbx_step_event(cbx_context *c, int local, void **event) {
   TRY(check_ctx(c));
   if (local < 0 || local >= (int)c->devs.size() || !event) return fail(CBX_ERR_INVALID, "bad step-event query");
-  *event = reinterpret_cast<void *>(c->devs[local].synched);
+  *event = reinterpret_cast<void *>(c->devs[local].step_event ? c->devs[local].step_event : c->devs[local].synched);
   return CBX_OK;
 }
 
@@ -1393,7 +1405,7 @@ int cbx_last_timing(cbx_context *c, int local, float *ms) {
       TRY(ring_span(d, slot, EV_A, EV_AR, &ms[CBX_T_ALLREDUCE]));
       TRY(ring_span(d, slot, EV_AR, EV_B, &ms[CBX_T_APPLY]));
     }
-    TRY(ring_span(d, slot, EV_START, EV_B, &ms[CBX_T_STEP]));
+    TRY(ring_span(d, slot, EV_START, kind == 0 ? EV_A : EV_B, &ms[CBX_T_STEP]));
   }
   auto span = [&](int a, int b, float *out) -> int {
     if (!d.ev_valid[a] || !d.ev_valid[b]) return CBX_OK;
@@ -1419,8 +1431,8 @@ int cbx_timing_history(cbx_context *c, int local, int which, float *ms, int max)
     int a = EV_START, b = EV_A;
     if (which == CBX_T_ALLREDUCE) { a = EV_A; b = EV_AR; }
     if (which == CBX_T_APPLY) { a = EV_AR; b = EV_B; }
-    if (which == CBX_T_STEP) { a = EV_START; b = EV_B; }
     const int kind = d.ring_split[slot];
+    if (which == CBX_T_STEP) { a = EV_START; b = (kind == 0) ? EV_A : EV_B; }
     if ((which == CBX_T_KERNEL && kind == 2) ||
         ((which == CBX_T_ALLREDUCE || which == CBX_T_APPLY) && kind != 1)) {
       ms[k] = -1.0f;

@@ -54,15 +54,22 @@ struct LaunchConfig {
   int num_cus = 256;
 };
 
+// Every SMA launcher takes an optional (start, stop) event pair that the
+// dispatch itself timestamps (hipExtLaunchKernelGGL): timing a launch adds no
+// marker packets to the stream.  Pass nullptr for untimed launches.
+struct Timing {
+  hipEvent_t start = nullptr;
+  hipEvent_t stop = nullptr;
+};
 // Fused 1-GPU step: Phase A + (identity) B + C (+ D when copy).
 hipError_t launch_sma_fused(const SmaArgs &a, bool momentum, bool copy,
-                            const LaunchConfig &cfg, hipStream_t stream);
+                            const LaunchConfig &cfg, hipStream_t stream, Timing t = {});
 // Multi-GPU kernel A: Phase A only, writes acc and the control slot.
 hipError_t launch_sma_accumulate(const SmaArgs &a, bool write_ctrl,
-                                 const LaunchConfig &cfg, hipStream_t stream);
+                                 const LaunchConfig &cfg, hipStream_t stream, Timing t = {});
 // Multi-GPU kernel B: Phase C (+ D, gated by the reduced control slot).
 hipError_t launch_sma_apply(const SmaArgs &a, bool momentum,
-                            const LaunchConfig &cfg, hipStream_t stream);
+                            const LaunchConfig &cfg, hipStream_t stream, Timing t = {});
 // Synthetic normal fill.
 hipError_t launch_fill_normal(float *out, int64_t n, uint64_t seed, float sigma,
                               const float *mean, hipStream_t stream);

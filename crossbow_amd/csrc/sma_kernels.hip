@@ -16,6 +16,8 @@
 //
 // Arithmetic is the reference's, bit for bit: cuBLAS saxpy y := fma(a, x, y)
 // in fp32 and the same operation order, so 1-GPU results equal the oracle's.
+#include <hip/hip_ext.h>
+
 #include "sma_internal.h"
 
 namespace cbx {
@@ -100,6 +102,11 @@ __global__ __launch_bounds__(512) void sma_fused_kernel(const SmaArgs a) {
           if constexpr (!COPY) wv[u][r] = ldo<P>(a.w[c + r], i);
         }
       }
+      // Keep every load of the chunk in flight before the first use: without
+      // this fence the scheduler sinks the last load below the first FMAs to
+      // save registers, serialising one HBM round trip per wave (measured
+      // +1-4 %, scripts/membench.hip v5), and it needs fewer VGPRs, not more.
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int r = 0; r < RR; ++r) {
         if (R < 0 && c + r >= nrep) break;
@@ -173,6 +180,7 @@ __global__ __launch_bounds__(512) void sma_accumulate_kernel(const SmaArgs a) {
           wv[u][r] = ldo<P>(a.w[c + r], i);
         }
       }
+      __builtin_amdgcn_sched_barrier(0);  // all loads in flight first (see fused)
 #pragma unroll
       for (int r = 0; r < RR; ++r) {
         if (R < 0 && c + r >= nrep) break;
@@ -277,89 +285,90 @@ inline dim3 grid_for(int64_t n4, const LaunchConfig &cfg) {
 }
 
 template <int R, bool MOM, bool COPY, int P>
-hipError_t fused_u(const SmaArgs &a, const LaunchConfig &cfg, hipStream_t s) {
+hipError_t fused_u(const SmaArgs &a, const LaunchConfig &cfg, hipStream_t s, Timing t) {
   const dim3 g = grid_for(a.n4, cfg);
   if (cfg.unroll == 2)
-    hipLaunchKernelGGL((sma_fused_kernel<R, MOM, COPY, P, 2>), g, dim3(cfg.block), 0, s, a);
+    hipExtLaunchKernelGGL((sma_fused_kernel<R, MOM, COPY, P, 2>), g, dim3(cfg.block), 0, s, t.start, t.stop, 0, a);
   else
-    hipLaunchKernelGGL((sma_fused_kernel<R, MOM, COPY, P, 1>), g, dim3(cfg.block), 0, s, a);
+    hipExtLaunchKernelGGL((sma_fused_kernel<R, MOM, COPY, P, 1>), g, dim3(cfg.block), 0, s, t.start, t.stop, 0, a);
   return hipGetLastError();
 }
 
 template <bool MOM, bool COPY, int P>
-hipError_t fused_r(const SmaArgs &a, const LaunchConfig &cfg, hipStream_t s) {
+hipError_t fused_r(const SmaArgs &a, const LaunchConfig &cfg, hipStream_t s, Timing t) {
   switch (a.nrep) {
-    case 0: return fused_u<0, MOM, COPY, P>(a, cfg, s);
-    case 1: return fused_u<1, MOM, COPY, P>(a, cfg, s);
-    case 2: return fused_u<2, MOM, COPY, P>(a, cfg, s);
-    case 3: return fused_u<3, MOM, COPY, P>(a, cfg, s);
-    case 4: return fused_u<4, MOM, COPY, P>(a, cfg, s);
-    case 5: return fused_u<5, MOM, COPY, P>(a, cfg, s);
-    case 6: return fused_u<6, MOM, COPY, P>(a, cfg, s);
-    case 7: return fused_u<7, MOM, COPY, P>(a, cfg, s);
-    case 8: return fused_u<8, MOM, COPY, P>(a, cfg, s);
-    default: return fused_u<-1, MOM, COPY, P>(a, cfg, s);
+    case 0: return fused_u<0, MOM, COPY, P>(a, cfg, s, t);
+    case 1: return fused_u<1, MOM, COPY, P>(a, cfg, s, t);
+    case 2: return fused_u<2, MOM, COPY, P>(a, cfg, s, t);
+    case 3: return fused_u<3, MOM, COPY, P>(a, cfg, s, t);
+    case 4: return fused_u<4, MOM, COPY, P>(a, cfg, s, t);
+    case 5: return fused_u<5, MOM, COPY, P>(a, cfg, s, t);
+    case 6: return fused_u<6, MOM, COPY, P>(a, cfg, s, t);
+    case 7: return fused_u<7, MOM, COPY, P>(a, cfg, s, t);
+    case 8: return fused_u<8, MOM, COPY, P>(a, cfg, s, t);
+    default: return fused_u<-1, MOM, COPY, P>(a, cfg, s, t);
   }
 }
 
 template <int R, int P>
-hipError_t acc_u(const SmaArgs &a, const LaunchConfig &cfg, hipStream_t s) {
+hipError_t acc_u(const SmaArgs &a, const LaunchConfig &cfg, hipStream_t s, Timing t) {
   const dim3 g = grid_for(a.n4, cfg);
   if (cfg.unroll == 2)
-    hipLaunchKernelGGL((sma_accumulate_kernel<R, P, 2>), g, dim3(cfg.block), 0, s, a);
+    hipExtLaunchKernelGGL((sma_accumulate_kernel<R, P, 2>), g, dim3(cfg.block), 0, s, t.start, t.stop, 0, a);
   else
-    hipLaunchKernelGGL((sma_accumulate_kernel<R, P, 1>), g, dim3(cfg.block), 0, s, a);
+    hipExtLaunchKernelGGL((sma_accumulate_kernel<R, P, 1>), g, dim3(cfg.block), 0, s, t.start, t.stop, 0, a);
   return hipGetLastError();
 }
 
 template <int P>
-hipError_t acc_r(const SmaArgs &a, const LaunchConfig &cfg, hipStream_t s) {
+hipError_t acc_r(const SmaArgs &a, const LaunchConfig &cfg, hipStream_t s, Timing t) {
   switch (a.nrep) {
-    case 0: return acc_u<0, P>(a, cfg, s);
-    case 1: return acc_u<1, P>(a, cfg, s);
-    case 2: return acc_u<2, P>(a, cfg, s);
-    case 3: return acc_u<3, P>(a, cfg, s);
-    case 4: return acc_u<4, P>(a, cfg, s);
-    case 5: return acc_u<5, P>(a, cfg, s);
-    case 6: return acc_u<6, P>(a, cfg, s);
-    case 7: return acc_u<7, P>(a, cfg, s);
-    case 8: return acc_u<8, P>(a, cfg, s);
-    default: return acc_u<-1, P>(a, cfg, s);
+    case 0: return acc_u<0, P>(a, cfg, s, t);
+    case 1: return acc_u<1, P>(a, cfg, s, t);
+    case 2: return acc_u<2, P>(a, cfg, s, t);
+    case 3: return acc_u<3, P>(a, cfg, s, t);
+    case 4: return acc_u<4, P>(a, cfg, s, t);
+    case 5: return acc_u<5, P>(a, cfg, s, t);
+    case 6: return acc_u<6, P>(a, cfg, s, t);
+    case 7: return acc_u<7, P>(a, cfg, s, t);
+    case 8: return acc_u<8, P>(a, cfg, s, t);
+    default: return acc_u<-1, P>(a, cfg, s, t);
   }
 }
 
 template <bool MOM, int P>
-hipError_t apply_u(const SmaArgs &a, const LaunchConfig &cfg, hipStream_t s) {
+hipError_t apply_u(const SmaArgs &a, const LaunchConfig &cfg, hipStream_t s, Timing t) {
   const dim3 g = grid_for(a.n4, cfg);
   if (cfg.unroll == 2)
-    hipLaunchKernelGGL((sma_apply_kernel<MOM, P, 2>), g, dim3(cfg.block), 0, s, a);
+    hipExtLaunchKernelGGL((sma_apply_kernel<MOM, P, 2>), g, dim3(cfg.block), 0, s, t.start, t.stop, 0, a);
   else
-    hipLaunchKernelGGL((sma_apply_kernel<MOM, P, 1>), g, dim3(cfg.block), 0, s, a);
+    hipExtLaunchKernelGGL((sma_apply_kernel<MOM, P, 1>), g, dim3(cfg.block), 0, s, t.start, t.stop, 0, a);
   return hipGetLastError();
 }
 
 }  // namespace
 
 hipError_t launch_sma_fused(const SmaArgs &a, bool momentum, bool copy, const LaunchConfig &cfg,
-                            hipStream_t stream) {
+                            hipStream_t stream, Timing t) {
   if (cfg.policy == 1) {
-    if (momentum) return copy ? fused_r<true, true, 1>(a, cfg, stream) : fused_r<true, false, 1>(a, cfg, stream);
-    return copy ? fused_r<false, true, 1>(a, cfg, stream) : fused_r<false, false, 1>(a, cfg, stream);
+    if (momentum) return copy ? fused_r<true, true, 1>(a, cfg, stream, t) : fused_r<true, false, 1>(a, cfg, stream, t);
+    return copy ? fused_r<false, true, 1>(a, cfg, stream, t) : fused_r<false, false, 1>(a, cfg, stream, t);
   }
-  if (momentum) return copy ? fused_r<true, true, 0>(a, cfg, stream) : fused_r<true, false, 0>(a, cfg, stream);
-  return copy ? fused_r<false, true, 0>(a, cfg, stream) : fused_r<false, false, 0>(a, cfg, stream);
+  if (momentum) return copy ? fused_r<true, true, 0>(a, cfg, stream, t) : fused_r<true, false, 0>(a, cfg, stream, t);
+  return copy ? fused_r<false, true, 0>(a, cfg, stream, t) : fused_r<false, false, 0>(a, cfg, stream, t);
 }
 
 hipError_t launch_sma_accumulate(const SmaArgs &a, bool write_ctrl, const LaunchConfig &cfg,
-                                 hipStream_t stream) {
+                                 hipStream_t stream, Timing t) {
   SmaArgs b = a;
   if (!write_ctrl) b.ctrl_out = nullptr;
-  return cfg.policy == 1 ? acc_r<1>(b, cfg, stream) : acc_r<0>(b, cfg, stream);
+  return cfg.policy == 1 ? acc_r<1>(b, cfg, stream, t) : acc_r<0>(b, cfg, stream, t);
 }
 
-hipError_t launch_sma_apply(const SmaArgs &a, bool momentum, const LaunchConfig &cfg, hipStream_t stream) {
-  if (cfg.policy == 1) return momentum ? apply_u<true, 1>(a, cfg, stream) : apply_u<false, 1>(a, cfg, stream);
-  return momentum ? apply_u<true, 0>(a, cfg, stream) : apply_u<false, 0>(a, cfg, stream);
+hipError_t launch_sma_apply(const SmaArgs &a, bool momentum, const LaunchConfig &cfg, hipStream_t stream,
+                            Timing t) {
+  if (cfg.policy == 1) return momentum ? apply_u<true, 1>(a, cfg, stream, t) : apply_u<false, 1>(a, cfg, stream, t);
+  return momentum ? apply_u<true, 0>(a, cfg, stream, t) : apply_u<false, 0>(a, cfg, stream, t);
 }
 
 hipError_t launch_fill_normal(float *out, int64_t n, uint64_t seed, float sigma, const float *mean,

@@ -177,7 +177,9 @@ int cbx_wait (cbx_context *ctx);
  * stream at the end of every synchronise(): it stands for the reference's
  * base->updated, synched[dev] and each locked replica's replica->updated
  * (sma.c:115,177,204,222), which this pipeline completes at the same point.
- * Task-side streams wait on it before using a replica again.             */
+ * Task-side streams wait on it before using a replica again.  Query it
+ * after each synchronise(): with timing on it is the stop event the step's
+ * last dispatch timestamps (no extra marker), so the handle changes.      */
 int cbx_step_event (cbx_context *ctx, int local, void **event);
 
 /* ---- measurement ------------------------------------------------------ */

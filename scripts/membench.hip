@@ -161,7 +161,7 @@ template <int P>
 __device__ __forceinline__ void sto(v4f *b, uint32_t off, v4f v) {
   st<P>(reinterpret_cast<v4f *>(reinterpret_cast<char *>(b) + off), v);
 }
-template <int MW, bool XCD>
+template <int MW, bool XCD, bool SB = false>
 __global__ __launch_bounds__(256, MW) void fused3(const Args a) {
   uint32_t blk = blockIdx.x;
   if constexpr (XCD) {
@@ -179,6 +179,7 @@ __global__ __launch_bounds__(256, MW) void fused3(const Args a) {
   for (int r = 0; r < R; ++r) sv[r] = ldo<1>(a.s[r], i);
 #pragma unroll
   for (int r = 0; r < R; ++r) wv[r] = ldo<1>(a.w[r], i);
+  if constexpr (SB) __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
   for (int r = 0; r < R; ++r) {
     v4f d = vfma(mone, zv, sv[r]);
@@ -208,6 +209,16 @@ __global__ __launch_bounds__(256) void mixnodep(const Args a, float *sink) {
 #pragma unroll
   for (int r = 0; r < R; ++r) t += ldo<1>(a.s[r], i) + ldo<1>(a.w[r], i);
   if (t.x == 12345.678f) sink[0] = t.y;
+}
+
+
+__global__ void fillk(uint32_t *p, size_t nwords, uint32_t seed) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < nwords; i += (size_t)gridDim.x * blockDim.x) {
+    uint32_t x = (uint32_t)i * 2654435761u ^ seed;
+    x ^= x >> 16; x *= 0x7feb352dU; x ^= x >> 15; x *= 0x846ca68bU; x ^= x >> 16;
+    float f = ((float)(x >> 8) * (1.0f / 16777216.0f) - 0.5f) * 0.1f;
+    p[i] = __float_as_uint(f);
+  }
 }
 
 static hipEvent_t e0, e1;
@@ -265,6 +276,76 @@ int main(int argc, char **argv) {
       {"2MiB-aligned", 2u << 20, 0}, {"packed-256B", 256, 0}, {"stagger-4KiB", 2u << 20, 4096},
   };
 
+
+  if (argc > 2 && std::strcmp(argv[2], "v4") == 0) {
+    const size_t stride = (buf + (2u << 20) - 1) / (2u << 20) * (2u << 20) + 4096;
+    Args a;
+    a.z = (v4f *)arena;
+    a.last = (v4f *)(arena + stride);
+    for (int r = 0; r < R; ++r) {
+      a.s[r] = (const v4f *)(arena + (2 + 2 * r) * stride);
+      a.w[r] = (v4f *)(arena + (3 + 2 * r) * stride);
+    }
+    a.n4 = n4;
+    a.alpha = 0.1f;
+    hipEvent_t et, en;
+    CK(hipEventCreate(&et));
+    CK(hipEventCreateWithFlags(&en, hipEventDisableTiming));
+    for (int data = 0; data < 2; ++data) {
+      if (data == 1) {
+        hipLaunchKernelGGL(fillk, dim3(8192), dim3(256), 0, 0, (uint32_t *)arena, nbuf * stride / 4, 12345u);
+        CK(hipDeviceSynchronize());
+      }
+      for (int blk : {128, 256}) {
+        const unsigned grid = n4 / blk;
+        auto launch = [&] { hipLaunchKernelGGL((fused3<1, false>), dim3(grid), dim3(blk), 0, 0, a); };
+        float iso = time_ms(launch, iters);
+        for (int mode = 0; mode < 3; ++mode) {
+          const int K = 50;
+          for (int k = 0; k < 3; ++k) launch();
+          CK(hipDeviceSynchronize());
+          CK(hipEventRecord(e0, 0));
+          for (int k = 0; k < K; ++k) {
+            launch();
+            if (mode == 1) CK(hipEventRecord(et, 0));
+            if (mode == 2) CK(hipEventRecord(en, 0));
+          }
+          CK(hipEventRecord(e1, 0));
+          CK(hipEventSynchronize(e1));
+          float ms;
+          CK(hipEventElapsedTime(&ms, e0, e1));
+          ms /= K;
+          std::printf("{\"v4\":1,\"data\":\"%s\",\"block\":%d,\"isolated_ms\":%.4f,\"b2b_mode\":\"%s\",\"b2b_ms\":%.4f,\"iso_GBs\":%.1f,\"b2b_GBs\":%.1f}\n",
+                      data ? "random" : "zero", blk, iso, mode == 0 ? "none" : (mode == 1 ? "timing-event" : "notiming-event"),
+                      ms, alg / iso / 1e6, alg / ms / 1e6);
+        }
+      }
+    }
+    return 0;
+  }
+
+  if (argc > 2 && std::strcmp(argv[2], "v5") == 0) {
+    const size_t stride = (buf + (2u << 20) - 1) / (2u << 20) * (2u << 20) + 4096;
+    Args a;
+    a.z = (v4f *)arena;
+    a.last = (v4f *)(arena + stride);
+    for (int r = 0; r < R; ++r) {
+      a.s[r] = (const v4f *)(arena + (2 + 2 * r) * stride);
+      a.w[r] = (v4f *)(arena + (3 + 2 * r) * stride);
+    }
+    a.n4 = n4;
+    a.alpha = 0.1f;
+    hipLaunchKernelGGL(fillk, dim3(8192), dim3(256), 0, 0, (uint32_t *)arena, nbuf * stride / 4, 12345u);
+    CK(hipDeviceSynchronize());
+    for (int round = 0; round < 3; ++round)
+      for (int blk : {64, 128, 256}) {
+        const unsigned grid = n4 / blk;
+        float t0 = time_ms([&] { hipLaunchKernelGGL((fused3<1, false, false>), dim3(grid), dim3(blk), 0, 0, a); }, iters);
+        float t1 = time_ms([&] { hipLaunchKernelGGL((fused3<1, false, true>), dim3(grid), dim3(blk), 0, 0, a); }, iters);
+        std::printf("{\"v5\":%d,\"block\":%d,\"base_GBs\":%.1f,\"schedbar_GBs\":%.1f}\n", round, blk, alg / t0 / 1e6, alg / t1 / 1e6);
+      }
+    return 0;
+  }
   // Ceilings on the same arena (1 GiB copy).
   {
     const uint32_t cn4 = (uint32_t)((1u << 30) / 16);

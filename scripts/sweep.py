@@ -45,10 +45,10 @@ def main():
     m = 1 if args.momentum > 0 else 0
     nbytes = (12 * args.replicas + 8 + 8 * m) * n if not args.split else (12 * args.replicas + 8) * n
 
-    blocks = [256, 512] if not args.quick else [256]
-    bpcs = [0, 2, 4, 8, 16]
+    blocks = [64, 128, 256] if not args.quick else [128]
+    bpcs = [0, 4] if not args.quick else [0]
     policies = [0, 1]
-    unrolls = [1, 2]
+    unrolls = [1] if args.quick else [1, 2]
     rows = []
     clock = 0
     for block, bpc, pol, un in itertools.product(blocks, bpcs, policies, unrolls):
