@@ -63,6 +63,7 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-staged", action="store_true")
     p.add_argument("--no-copy-ceiling", action="store_true")
+    p.add_argument("--no-optimiser", action="store_true", help="skip the replica optimiser-step measurement")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
                    help="PMC-derived HBM bytes per launch (written by scripts/pmc_traffic.py)")
     return p.parse_args()
@@ -104,6 +105,36 @@ def cpu_baseline(args, n_full):
                       f"({os.path.basename(lib)}), 1 thread pinned to core 0, same algorithmic-bytes formula"}
 
 
+def bench_optimiser(gpu, torch, n, args, rounds=10):
+    """the fused replica optimiser step (kernels/optimisers/
+    sma.cu:3-100) of every replica, back to back on one torch stream.  Reads
+    w, g, last and writes s, w, g, last: (12 + 16) n bytes per launch with
+    momentum and weight decay (the reference issues 6 ops moving ~60n B)."""
+    stream = torch.cuda.Stream()
+    task = 0
+    with torch.cuda.stream(stream):
+        for i in range(args.replicas):  # warm
+            gpu.replica_optimise(i, task, stream.cuda_stream)
+            task += 1
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for _ in range(rounds):
+            for i in range(args.replicas):
+                gpu.replica_optimise(i, task, stream.cuda_stream)
+                task += 1
+        e1.record(stream)
+    e1.synchronize()
+    gpu.wait()
+    launches = rounds * args.replicas
+    ms = e0.elapsed_time(e1) / launches
+    m = 1 if args.momentum > 0 else 0
+    b = (12 + 16) * n if m else 16 * n + 4 * n
+    return {"kernel": "sma_optimise_kernel", "launch_ms_mean": round(ms, 4), "launches": launches,
+            "alg_bytes_per_launch": b, "achieved_GBs": round(b / (ms * 1e-3) / 1e9, 1),
+            "frac": round(b / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+            "timed": "torch events around back-to-back launches on one stream (includes launch gaps)"}
+
+
 def main():
     args = parse()
     from crossbow_amd import dist as D
@@ -127,6 +158,10 @@ def main():
     gpu.setUpdateModelType(UPDATE_SMA)
     gpu.setEamsgdAlpha(args.alpha)
     gpu.setMomentum(args.momentum, 0)
+    # scripts/benchmarks/resnet-50.sh:78-83: lr 0.1, multistep, gamma 0.1, decay 1e-4
+    # (used by the replica optimiser step; the SMA step itself needs alpha only).
+    gpu.setWeightDecay(1e-4)
+    gpu.setLearningRateDecayPolicyMultiStep(0.1, 0.1, 0, [1 << 30])
     gpu.setModelManager(args.replicas, SYNC_BSP)
     gpu.set_kernel_config(args.block, args.blocks_per_cu, args.policy, args.unroll)
     one_bucket = 1 << 62
@@ -232,6 +267,9 @@ def main():
                                "apply_ms_median": round(statistics.median(calib["apply"]), 4),
                                "unpipelined_step_ms_median": round(statistics.median(calib["step"]), 4),
                                "timed_in": "calibration steps (one bucket, in order)"}
+
+    if rank == 0 and world == 1 and not args.no_optimiser:
+        result["replica_optimiser"] = bench_optimiser(gpu, torch, n, args)
 
     if rank == 0 and world == 1:
         if not args.no_copy_ceiling:

@@ -96,6 +96,7 @@ SIGNATURES = {
     "cbx_replica_task_done": (_I, [_P, _I]),
     "cbx_replica_clock": (_I, [_P, _I]),
     "cbx_replica_learning_rate": (_I, [_P, _I, _I, _FP]),
+    "cbx_replica_optimise": (_I, [_P, _I, _I, _P]),
     "cbx_replica_get_copy": (_I, [_P, _I]),
     "cbx_replica_set_copy": (_I, [_P, _I, _I]),
     "cbx_replica_device": (_I, [_P, _I]),

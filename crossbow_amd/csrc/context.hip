@@ -162,6 +162,7 @@ struct Replica {
   int updates = 0;
   SolverConf conf;
   pthread_mutex_t lock;
+  hipEvent_t client = nullptr;  // end of the last optimiser step on a task stream (sma.cu:79)
 };
 
 enum TimingEv { EV_START = 0, EV_A, EV_AR, EV_B, EV_H2D0, EV_H2D1, EV_D2H0, EV_D2H1, EV_COUNT };
@@ -783,9 +784,17 @@ int cbx_init_rank(cbx_context **out, int device, int nranks, int rank, const uns
 
 int cbx_free(cbx_context *c) {
   if (!c) return CBX_OK;
+  for (Replica *r : c->replicas) {
+    if (r && r->client && r->local >= 0) {
+      (void)hipSetDevice(c->devs[r->local].hip_id);
+      (void)hipEventDestroy(r->client);
+      r->client = nullptr;
+    }
+  }
   for (Device &d : c->devs) close_device(d);
   for (Replica *r : c->replicas) {
     if (!r) continue;
+    if (r->client) (void)hipEventDestroy(r->client);
     pthread_mutex_destroy(&r->lock);
     delete r;
   }
@@ -1146,6 +1155,46 @@ int cbx_add_model(cbx_context *c) {
 int cbx_del_model(cbx_context *c) {
   TRY(check_manager(c));
   return fail(CBX_ERR_UNSUPPORTED, "autotune delModel is not implemented (DESIGN.md, out of scope for round 1)");
+}
+
+// ---- replica optimiser step (kernels/optimisers/sma.cu:3-100) -------------
+int cbx_replica_optimise(cbx_context *c, int id, int task, void *stream) {
+  TRY(check_replica(c, id, true));
+  Replica &r = *c->replicas[id];
+  Device &d = c->devs[r.local];
+  SolverConf &conf = r.conf;
+  if (conf.momentum > 0 && conf.momentumMethod == 1)
+    return fail(CBX_ERR_UNSUPPORTED, "Nesterov's momentum has been disabled");  // sma.cu:46-48
+  if (conf.momentum > 0 && !c->has_last)
+    return fail(CBX_ERR_STATE, "replica momentum without a `last` buffer (model.c:116-120)");
+  float lr = 0.0f;
+  TRY(conf.learning_rate(task, &lr));  // may raise _copy (solverconfiguration.c:133,147)
+  cbx::OptArgs a;
+  std::memset(&a, 0, sizeof(a));
+  a.w = reinterpret_cast<cbx::v4f *>(replica_dev(d, r, CBX_BUF_DATA));
+  a.g = reinterpret_cast<cbx::v4f *>(replica_dev(d, r, CBX_BUF_GRADIENT));
+  a.last = conf.momentum > 0 ? reinterpret_cast<cbx::v4f *>(replica_dev(d, r, CBX_BUF_LAST)) : nullptr;
+  a.s = reinterpret_cast<cbx::v4f *>(replica_dev(d, r, CBX_BUF_DIFF));
+  a.n4 = c->n4;
+  a.rate = -lr;  // sma.cu:43
+  a.momentum = conf.momentum;
+  a.wd = conf.weightDecay;
+  HIP_TRY(hipSetDevice(d.hip_id));
+  hipStream_t st = stream ? reinterpret_cast<hipStream_t>(stream) : d.stream;
+  cbx::LaunchConfig cfg = c->cfg;
+  cfg.num_cus = d.num_cus;
+  cfg.blocks_per_cu = 0;
+  // The replica must not be updated while the last synchronise() still uses
+  // it (the reference's forward kernels wait on replica->updated).
+  if (st != d.stream && d.step_event) HIP_TRY(hipStreamWaitEvent(st, d.step_event, 0));
+  HIP_TRY(cbx::launch_sma_optimise(a, cfg, st, {}));
+  if (st != d.stream) {
+    // sma.cu:79-81: the synchronisation stream waits for the updated replica.
+    if (!r.client) HIP_TRY(hipEventCreateWithFlags(&r.client, hipEventDisableTiming));
+    HIP_TRY(hipEventRecord(r.client, st));
+    HIP_TRY(hipStreamWaitEvent(d.stream, r.client, 0));
+  }
+  return CBX_OK;
 }
 
 // ---- task-side replica access ---------------------------------------------

@@ -70,6 +70,20 @@ hipError_t launch_sma_accumulate(const SmaArgs &a, bool write_ctrl,
 // Multi-GPU kernel B: Phase C (+ D, gated by the reduced control slot).
 hipError_t launch_sma_apply(const SmaArgs &a, bool momentum,
                             const LaunchConfig &cfg, hipStream_t stream, Timing t = {});
+// The replica's local optimiser step of one task (the producer of s and w,
+// clib-multigpu/kernels/optimisers/sma.cu:3-100), fused into one pass.
+struct OptArgs {
+  v4f *w;          // replica->data
+  v4f *g;          // replica->gradient (updated in place, as the reference leaves it)
+  v4f *last;       // replica->last (momentum > 0 only)
+  v4f *s;          // replica->diff: the snapshot of w before the update
+  int64_t n4;      // float4s (multiple of kPadFloat4)
+  float rate;      // -learning rate (sma.cu:43)
+  float momentum;  // replica conf->momentum
+  float wd;        // replica conf->weightDecay
+  int pad_;
+};
+hipError_t launch_sma_optimise(const OptArgs &a, const LaunchConfig &cfg, hipStream_t stream, Timing t = {});
 // Synthetic normal fill.
 hipError_t launch_fill_normal(float *out, int64_t n, uint64_t seed, float sigma,
                               const float *mean, hipStream_t stream);

@@ -244,6 +244,44 @@ __global__ __launch_bounds__(512) void sma_apply_kernel(const SmaArgs a) {
 }
 
 // ---------------------------------------------------------------------------
+// Replica optimiser step (clib-multigpu/kernels/optimisers/sma.cu:3-100).  The
+// reference issues up to 6 full-model ops per task (saxpy wd, sscal, saxpy mu,
+// copy last, copy diff, saxpy); here one pass reads w, g (, last) once and
+// writes g, s, w (, last) once:  (20 + 8m) n bytes, or 16n (+4n if wd > 0)
+// without momentum.  Per element, in the reference's order and rounding:
+//   g = fma(wd, w, g)                    :24-31 (wd > 0)
+//   g = rate * g ; g = fma(mu, last, g)  :52-64 ; last = g  :68
+//   s = w                                :71 / :87
+//   w = fma(1, g, w)  or  fma(rate, g, w) without momentum  :74 / :90
+// ---------------------------------------------------------------------------
+template <bool MOM, bool WD, int P>
+__global__ __launch_bounds__(512) void sma_optimise_kernel(const OptArgs a) {
+  const uint32_t trip = gridDim.x * blockDim.x;
+  const uint32_t n4 = (uint32_t)a.n4;
+  const v4f rate = a.rate, mu = a.momentum, wd = a.wd, one = 1.0f;
+  for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < n4; e += trip) {
+    const uint32_t i = e * 16u;
+    const v4f w = ldo<P>(a.w, i);
+    v4f g = ldo<P>(a.g, i);
+    v4f l;
+    if constexpr (MOM) l = ldo<P>(a.last, i);
+    __builtin_amdgcn_sched_barrier(0);
+    if constexpr (WD) g = vfma(wd, w, g);
+    sto<P>(a.s, i, w);
+    if constexpr (MOM) {
+      g = rate * g;
+      g = vfma(mu, l, g);
+      sto<P>(a.last, i, g);
+      sto<P>(a.w, i, vfma(one, g, w));
+      sto<P>(a.g, i, g);
+    } else {
+      sto<P>(a.w, i, vfma(rate, g, w));
+      if constexpr (WD) sto<P>(a.g, i, g);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Synthetic inputs: splitmix64 -> Box-Muller in double.
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
@@ -369,6 +407,32 @@ hipError_t launch_sma_apply(const SmaArgs &a, bool momentum, const LaunchConfig 
                             Timing t) {
   if (cfg.policy == 1) return momentum ? apply_u<true, 1>(a, cfg, stream, t) : apply_u<false, 1>(a, cfg, stream, t);
   return momentum ? apply_u<true, 0>(a, cfg, stream, t) : apply_u<false, 0>(a, cfg, stream, t);
+}
+
+hipError_t launch_sma_optimise(const OptArgs &a, const LaunchConfig &cfg, hipStream_t stream, Timing t) {
+  LaunchConfig c = cfg;
+  c.unroll = 1;
+  const dim3 g = grid_for(a.n4, c);
+  const dim3 b(c.block);
+  const bool mom = a.momentum > 0.0f, wd = a.wd > 0.0f;
+  if (cfg.policy == 1) {
+    if (mom) {
+      if (wd) hipExtLaunchKernelGGL((sma_optimise_kernel<true, true, 1>), g, b, 0, stream, t.start, t.stop, 0, a);
+      else hipExtLaunchKernelGGL((sma_optimise_kernel<true, false, 1>), g, b, 0, stream, t.start, t.stop, 0, a);
+    } else {
+      if (wd) hipExtLaunchKernelGGL((sma_optimise_kernel<false, true, 1>), g, b, 0, stream, t.start, t.stop, 0, a);
+      else hipExtLaunchKernelGGL((sma_optimise_kernel<false, false, 1>), g, b, 0, stream, t.start, t.stop, 0, a);
+    }
+  } else {
+    if (mom) {
+      if (wd) hipExtLaunchKernelGGL((sma_optimise_kernel<true, true, 0>), g, b, 0, stream, t.start, t.stop, 0, a);
+      else hipExtLaunchKernelGGL((sma_optimise_kernel<true, false, 0>), g, b, 0, stream, t.start, t.stop, 0, a);
+    } else {
+      if (wd) hipExtLaunchKernelGGL((sma_optimise_kernel<false, true, 0>), g, b, 0, stream, t.start, t.stop, 0, a);
+      else hipExtLaunchKernelGGL((sma_optimise_kernel<false, false, 0>), g, b, 0, stream, t.start, t.stop, 0, a);
+    }
+  }
+  return hipGetLastError();
 }
 
 hipError_t launch_fill_normal(float *out, int64_t n, uint64_t seed, float sigma, const float *mean,

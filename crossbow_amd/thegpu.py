@@ -172,6 +172,14 @@ class TheGPU:
         check(self._L.cbx_replica_learning_rate(self._ctx, id, task, ctypes.byref(r)))
         return r.value
 
+    def replica_optimise(self, id: int, task: int, stream: Optional[int] = None) -> None:
+        """crossbowKernelOptimiserSMA (kernels/optimisers/sma.cu:3-100) for one task.
+
+        ``stream`` is a raw hipStream_t handle (e.g. ``torch.cuda.current_stream().cuda_stream``);
+        None enqueues on the replica device's synchronisation stream.
+        """
+        check(self._L.cbx_replica_optimise(self._ctx, id, task, ctypes.c_void_p(stream) if stream else None))
+
     def replica_copy(self, id: int) -> int:
         return check(self._L.cbx_replica_get_copy(self._ctx, id))
 

@@ -143,6 +143,15 @@ int cbx_replica_clock (cbx_context *ctx, int id);
 int cbx_replica_learning_rate (cbx_context *ctx, int id, int task, float *rate);
 int cbx_replica_get_copy (cbx_context *ctx, int id);
 int cbx_replica_set_copy (cbx_context *ctx, int id, int flag);
+/* crossbowKernelOptimiserSMA (kernels/optimisers/sma.cu:3-100), fused into
+ * one pass: the replica's local step for task `task`, which produces the
+ * snapshot s (replica->diff) and the new w that the next synchronise()
+ * averages.  The learning rate comes from the replica's solver
+ * configuration (may raise its _copy flag, solverconfiguration.c:133,147).
+ * Enqueued on `stream` (a hipStream_t; NULL = the replica device's sync
+ * stream); the sync stream then waits for it (sma.cu:79-81).  Nesterov
+ * momentum is CBX_ERR_UNSUPPORTED, as in the reference (sma.cu:46-48).  */
+int cbx_replica_optimise (cbx_context *ctx, int id, int task, void *stream);
 /* Global device index a replica lives on (id % G). */
 int cbx_replica_device (cbx_context *ctx, int id);
 /* 1 if the replica lives in this process. */

@@ -59,6 +59,10 @@ def lib():
         L.cbo_sma_accumulate.argtypes = [ctypes.c_int, ctypes.c_size_t, ctypes.c_float, fp, fpp, fpp, ip, fp]
         L.cbo_sma_apply.restype = None
         L.cbo_sma_apply.argtypes = [ctypes.c_int, ctypes.c_size_t, ctypes.c_float, fp, fp, fp, fpp, ctypes.c_int]
+        for name in ("cbo_sma_optimise", "cbo_sma_optimise_blas"):
+            f = getattr(L, name)
+            f.restype = None if name == "cbo_sma_optimise" else ctypes.c_int
+            f.argtypes = [ctypes.c_size_t, ctypes.c_float, ctypes.c_float, ctypes.c_float, fp, fp, fp, fp]
         L.cbo_blas_open.restype = ctypes.c_int
         L.cbo_blas_open.argtypes = [ctypes.c_char_p]
         L.cbo_blas_name.restype = ctypes.c_char_p
@@ -175,6 +179,26 @@ def sma_apply(momentum: float, D: np.ndarray, z: np.ndarray, last: Optional[np.n
     """Phases C and D of one device, in place on z, last and (if copy) w."""
     lp = _fp(last) if last is not None else ctypes.POINTER(ctypes.c_float)()
     lib().cbo_sma_apply(len(w), z.size, momentum, _fp(D), _fp(z), lp, _fpp(w) if w else None, 1 if copy else 0)
+
+
+def sma_optimise(rate: float, momentum: float, wd: float, w: np.ndarray, g: np.ndarray,
+                 last: Optional[np.ndarray], s: np.ndarray, blas: bool = False) -> None:
+    """The replica optimiser step of one task (kernels/optimisers/sma.cu:3-100), in place.
+
+    ``rate`` is the negated learning rate (sma.cu:43).  ``blas=True`` replays
+    the reference's cuBLAS/memcpy call sequence on OpenBLAS instead.
+    """
+    if momentum > 0 and last is None:
+        raise ValueError("momentum > 0 needs the replica's `last` buffer (model.c:116-120)")
+    lp = _fp(last) if last is not None else ctypes.POINTER(ctypes.c_float)()
+    if blas:
+        if not lib().cbo_blas_is_open():
+            blas_open()
+        rc = lib().cbo_sma_optimise_blas(w.size, rate, momentum, wd, _fp(w), _fp(g), lp, _fp(s))
+        if rc != 0:
+            raise RuntimeError("OpenBLAS replay unavailable")
+    else:
+        lib().cbo_sma_optimise(w.size, rate, momentum, wd, _fp(w), _fp(g), lp, _fp(s))
 
 
 def openblas_path() -> Optional[str]:

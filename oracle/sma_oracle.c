@@ -148,20 +148,45 @@ void cbo_sma_apply (int R, size_t n, float momentum, const float *D,
 			memcpy (w[i], z, n * sizeof(float));
 }
 
+/* Replica optimiser step, clib-multigpu/kernels/optimisers/sma.cu:3-100.  */
+void cbo_sma_optimise (size_t n, float rate, float momentum, float wd,
+		float *w, float *g, float *last, float *s) {
+	size_t k;
+	for (k = 0; k < n; ++k) {
+		float gk = g[k];
+		if (wd > 0)
+			gk = fmaf (wd, w[k], gk);                                       /* sma.cu:24-31 */
+		if (momentum > 0) {
+			gk = rate * gk;                                                 /* sma.cu:52-57 sscal */
+			gk = fmaf (momentum, last[k], gk);                              /* sma.cu:58-64 */
+			last[k] = gk;                                                   /* sma.cu:68    */
+			s[k] = w[k];                                                    /* sma.cu:71    */
+			w[k] = fmaf (1.0f, gk, w[k]);                                   /* sma.cu:74    */
+		} else {
+			s[k] = w[k];                                                    /* sma.cu:87    */
+			w[k] = fmaf (rate, gk, w[k]);                                   /* sma.cu:90    */
+		}
+		g[k] = gk;
+	}
+}
+
 /* ---------------------------------------------------------------------- */
 /* OpenBLAS replay of the reference call sequence.                         */
 /* ---------------------------------------------------------------------- */
 typedef void (*saxpy_fn) (int, float, const float *, int, float *, int);
+typedef void (*sscal_fn) (int, float, float *, int);
 typedef void (*threads_fn) (int);
 
 static void *blas_handle = NULL;
 static saxpy_fn blas_saxpy = NULL;
+static sscal_fn blas_sscal = NULL;
 static threads_fn blas_threads = NULL;
 static char blas_name[512] = "";
 
 int cbo_blas_open (const char *path) {
 	static const char *probe[] = { "libopenblas.so.0", "libopenblas.so", NULL };
 	static const char *saxpy_names[] = { "cblas_saxpy", "scipy_cblas_saxpy", NULL };
+	static const char *sscal_names[] = { "cblas_sscal", "scipy_cblas_sscal", NULL };
 	static const char *thread_names[] = { "openblas_set_num_threads", "scipy_openblas_set_num_threads", NULL };
 	int j;
 	if (blas_handle)
@@ -177,9 +202,11 @@ int cbo_blas_open (const char *path) {
 		return -1;
 	for (j = 0; ! blas_saxpy && saxpy_names[j]; ++j)
 		blas_saxpy = (saxpy_fn) dlsym (blas_handle, saxpy_names[j]);
+	for (j = 0; ! blas_sscal && sscal_names[j]; ++j)
+		blas_sscal = (sscal_fn) dlsym (blas_handle, sscal_names[j]);
 	for (j = 0; ! blas_threads && thread_names[j]; ++j)
 		blas_threads = (threads_fn) dlsym (blas_handle, thread_names[j]);
-	if (! blas_saxpy) {
+	if (! blas_saxpy || ! blas_sscal) {
 		dlclose (blas_handle);
 		blas_handle = NULL;
 		return -2;
@@ -255,6 +282,28 @@ int cbo_sma_blas (int G, int size, size_t n, float alpha, float momentum,
 		}
 	}
 	return copies;
+}
+
+/* sma.cu:3-100 as the reference issues it (cuBLAS -> OpenBLAS, memcpy).  */
+int cbo_sma_optimise_blas (size_t n, float rate, float momentum, float wd,
+		float *w, float *g, float *last, float *s) {
+	int N = (int) n;
+	size_t bytes = n * sizeof(float);
+	if (! blas_saxpy || ! blas_sscal)
+		return -1;
+	if (wd > 0)
+		blas_saxpy (N, wd, w, 1, g, 1);                                     /* sma.cu:24-31 */
+	if (momentum > 0) {
+		blas_sscal (N, rate, g, 1);                                         /* sma.cu:52-57 */
+		blas_saxpy (N, momentum, last, 1, g, 1);                            /* sma.cu:58-64 */
+		memcpy (last, g, bytes);                                            /* sma.cu:68    */
+		memcpy (s, w, bytes);                                               /* sma.cu:71    */
+		blas_saxpy (N, 1.0f, g, 1, w, 1);                                   /* sma.cu:74    */
+	} else {
+		memcpy (s, w, bytes);                                               /* sma.cu:87    */
+		blas_saxpy (N, rate, g, 1, w, 1);                                   /* sma.cu:90    */
+	}
+	return 0;
 }
 
 /* ---------------------------------------------------------------------- */

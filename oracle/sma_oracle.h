@@ -82,6 +82,20 @@ int cbo_sma_accumulate (int R, size_t n, float alpha, const float *z,
 void cbo_sma_apply (int R, size_t n, float momentum, const float *D,
 		float *z, float *last, float **w, int copy);
 
+/* The replica's local optimiser step for one task, the producer of s and w */
+/* (crossbowKernelOptimiserSMA, clib-multigpu/kernels/optimisers/sma.cu:3-100). */
+/* `rate` is the already negated learning rate (sma.cu:43).  `last` may be  */
+/* NULL iff momentum <= 0.                                                  */
+/*   wd > 0      : g = fma(wd, w, g)                      sma.cu:24-31      */
+/*   momentum > 0: g = rate * g; g = fma(mu, last, g);    sma.cu:52-64      */
+/*                 last = g; s = w; w = fma(1, g, w)      sma.cu:68-74      */
+/*   else        : s = w; w = fma(rate, g, w)             sma.cu:87-90      */
+void cbo_sma_optimise (size_t n, float rate, float momentum, float wd,
+		float *w, float *g, float *last, float *s);
+/* Same step replaying the reference's cuBLAS/memcpy sequence on OpenBLAS. */
+int cbo_sma_optimise_blas (size_t n, float rate, float momentum, float wd,
+		float *w, float *g, float *last, float *s);
+
 /* dlopen an OpenBLAS build; returns 0 on success.  `path` may be NULL to  */
 /* probe the usual numpy/scipy wheels.  Records the library actually used. */
 int cbo_blas_open (const char *path);

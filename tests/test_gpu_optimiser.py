@@ -1,0 +1,155 @@
+"""GPU parity of the fused replica optimiser step.
+
+``cbx_replica_optimise`` restates crossbowKernelOptimiserSMA
+(clib-multigpu/kernels/optimisers/sma.cu:3-100): weight decay, learning-rate
+scale, momentum, the snapshot ``diff <- data`` and the update, in one pass.
+Checked bit for bit against the oracle (which is itself pinned to the
+reference's saxpy/sscal/memcpy sequence on OpenBLAS, tests/test_oracle.py),
+alone and inside a whole clock loop (local steps, then synchronise).
+"""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+from tests.helpers import assert_bitexact
+
+pytestmark = pytest.mark.gpu
+
+
+def _gpu(n, R, momentum, wd, alpha=0.1, policy=None):
+    from crossbow_amd import TheGPU
+    g = TheGPU()
+    g.init([0])
+    g.setModel(1, 4 * n)
+    g.setModelVariable(0, 1, [n], 4 * n)
+    g.setUpdateModelType(7)
+    g.setEamsgdAlpha(alpha)
+    g.setMomentum(momentum, 0)
+    g.setWeightDecay(wd)
+    if policy is None:
+        g.setLearningRateDecayPolicyFixed(0.05)
+    else:
+        policy(g)
+    g.setModelManager(R, 0)
+    return g
+
+
+@pytest.mark.parametrize("momentum", [0.0, 0.9])
+@pytest.mark.parametrize("wd", [0.0, 5e-4])
+@pytest.mark.parametrize("on_torch_stream", [False, True])
+def test_optimise_bitexact(momentum, wd, on_torch_stream):
+    import torch
+    from crossbow_amd import BUF_DATA, BUF_DIFF, BUF_GRADIENT, BUF_LAST
+    n, R = 70_001, 2
+    g = _gpu(n, R, momentum, wd)
+    try:
+        stream = torch.cuda.Stream() if on_torch_stream else None
+        for i in range(R):
+            w = O.fill_normal(n, 300 + i, 0.05)
+            gr = O.fill_normal(n, 310 + i, 0.01)
+            last = O.fill_normal(n, 320 + i, 0.001) if momentum > 0 else None
+            s = np.zeros(n, np.float32)
+            g.replica_write(i, BUF_DATA, w)
+            g.replica_write(i, BUF_GRADIENT, gr)
+            if last is not None:
+                g.replica_write(i, BUF_LAST, last)
+            g.replica_optimise(i, task=i, stream=stream.cuda_stream if stream else None)
+            g.wait()
+            O.sma_optimise(np.float32(-0.05), momentum, wd, w, gr, last, s)
+            assert_bitexact(g.replica_read(i, BUF_DATA), w, f"w[{i}]")
+            assert_bitexact(g.replica_read(i, BUF_DIFF), s, f"s[{i}]")
+            assert_bitexact(g.replica_read(i, BUF_GRADIENT), gr, f"g[{i}]")
+            if last is not None:
+                assert_bitexact(g.replica_read(i, BUF_LAST), last, f"last[{i}]")
+    finally:
+        g.free()
+
+
+def test_multistep_learning_rate_raises_copy():
+    # solverconfiguration.c:128-136: crossing a step divides the rate by 1/gamma
+    # and raises _copy, which the next synchronise turns into Phase D.
+    from crossbow_amd import BUF_DATA, BUF_GRADIENT
+    n, R = 8192, 2
+    g = _gpu(n, R, 0.0, 0.0, policy=lambda h: h.setLearningRateDecayPolicyMultiStep(0.1, 0.5, 0, [3]))
+    try:
+        assert g.replica_learning_rate(1, 0) == pytest.approx(0.1)
+        w = O.fill_normal(n, 400, 0.05)
+        gr = O.fill_normal(n, 401, 0.01)
+        g.replica_write(0, BUF_DATA, w)
+        g.replica_write(0, BUF_GRADIENT, gr)
+        g.replica_optimise(0, task=1)  # task+1 = 2 < 3
+        assert g.replica_copy(0) == 0
+        g.replica_optimise(0, task=2)  # task+1 = 3 >= 3: step, rate 0.05, copy
+        assert g.replica_copy(0) == 1
+        g.wait()
+        s = np.zeros(n, np.float32)
+        O.sma_optimise(np.float32(-0.1), 0.0, 0.0, w, gr, None, s)
+        O.sma_optimise(np.float32(-0.1) * np.float32(0.5), 0.0, 0.0, w, gr, None, s)
+        assert_bitexact(g.replica_read(0, BUF_DATA), w, "w after two steps")
+        # the next barrier copies the base model to every replica and resets _copy
+        g.lockAny()
+        g.synchronise(0, 1, 0, False)
+        g.unlockAny()
+        g.wait()
+        z = g.base_read(0, BUF_DATA)
+        for i in range(R):
+            assert_bitexact(g.replica_read(i, BUF_DATA), z, f"w[{i}] == z after Phase D")
+        assert g.replica_copy(0) == 0
+    finally:
+        g.free()
+
+
+@pytest.mark.parametrize("momentum", [0.0, 0.9])
+def test_clock_loop_bitexact(momentum):
+    # The whole per-clock loop of the SMA model on one GPU: every replica runs
+    # `wpc` local steps (a fresh gradient per task), then the barrier averages.
+    from crossbow_amd import BUF_DATA, BUF_GRADIENT, BUF_LAST
+    from tests.helpers import compare_states, download, upload
+    n, R, clocks, wpc, alpha = 33_333, 3, 3, 2, 0.1
+    g = _gpu(n, R, momentum, 1e-4, alpha=alpha)
+    try:
+        st = O.make_state(n, 1, R, alpha, momentum)
+        upload(g, st)
+        lasts = [np.zeros(n, np.float32) if momentum > 0 else None for _ in range(R)]
+        task = 0
+        for clock in range(1, clocks + 1):
+            for i in range(R):
+                for _ in range(wpc):
+                    gr = O.fill_normal(n, 1000 + task, 0.01)
+                    g.replica_write(i, BUF_GRADIENT, gr)
+                    g.replica_optimise(i, task)
+                    O.sma_optimise(np.float32(-0.05), momentum, 1e-4, st.w[i], gr, lasts[i], st.s[i])
+                    task += 1
+            g.lockAny()
+            g.synchronise(0, clock, 0, False)
+            g.unlockAny()
+            O.sma_step(st)
+        g.wait()
+        compare_states(download(g, st), st)
+        if momentum > 0:
+            for i in range(R):
+                assert_bitexact(g.replica_read(i, BUF_LAST), lasts[i], f"replica last[{i}]")
+        assert_bitexact(g.replica_read(0, BUF_DATA), st.w[0], "w[0]")
+    finally:
+        g.free()
+
+
+def test_nesterov_is_unsupported():
+    from crossbow_amd import CbxError, TheGPU, _lib
+    n = 4096
+    g = TheGPU()
+    g.init([0])
+    try:
+        g.setModel(1, 4 * n)
+        g.setModelVariable(0, 1, [n], 4 * n)
+        g.setUpdateModelType(7)
+        g.setMomentum(0.9, 1)  # NESTEROV (utils.h:101)
+        g.setLearningRateDecayPolicyFixed(0.1)
+        g.setModelManager(1, 0)
+        with pytest.raises(CbxError) as e:
+            g.replica_optimise(0, 0)
+        assert e.value.code == _lib.CBX_ERR_UNSUPPORTED
+    finally:
+        g.free()

@@ -142,3 +142,37 @@ def test_bytes_per_step_formula():
     assert O.bytes_per_step(n, 8, 0.9) == 112 * n  # C3: 2.862 GB
     assert O.bytes_per_step(1_111_946, 4, 0.0) == 56 * 1_111_946  # C2
     assert O.bytes_per_step(n, 4, 0.9, G=8) == 76 * n  # C5 per GPU
+
+
+@pytest.mark.parametrize("momentum", [0.0, 0.9])
+@pytest.mark.parametrize("wd", [0.0, 5e-4])
+def test_optimiser_restatement_equals_openblas_sequence(momentum, wd):
+    # kernels/optimisers/sma.cu:3-100: the fmaf restatement and the literal
+    # saxpy / sscal / memcpy sequence agree bit for bit.
+    n = 4099
+    w = O.fill_normal(n, 100, 0.05)
+    g = O.fill_normal(n, 101, 0.01)
+    last = O.fill_normal(n, 102, 0.001) if momentum > 0 else None
+    s = np.zeros(n, np.float32)
+    a = [x.copy() if x is not None else None for x in (w, g, last, s)]
+    b = [x.copy() if x is not None else None for x in (w, g, last, s)]
+    O.sma_optimise(-0.1, momentum, wd, *a)
+    O.sma_optimise(-0.1, momentum, wd, *b, blas=True)
+    for x, y in zip(a, b):
+        if x is not None:
+            assert _eq(x, y)
+    assert _eq(a[3], w), "s is the snapshot of w before the update (sma.cu:71,87)"
+    assert not _eq(a[0], w)
+
+
+def test_optimiser_then_sma_moves_replicas_toward_base():
+    # One clock of the whole loop on the oracle: local steps, then averaging.
+    st = O.make_state(2053, 1, 4, 0.5, 0.9)
+    grads = [O.fill_normal(st.n, 200 + i, 0.01) for i in range(st.size)]
+    lasts = [np.zeros(st.n, np.float32) for _ in range(st.size)]
+    spread0 = max(float(np.abs(st.w[i] - st.z[0]).max()) for i in range(st.size))
+    for i in range(st.size):
+        O.sma_optimise(-0.01, 0.9, 0.0, st.w[i], grads[i], lasts[i], st.s[i])
+    O.sma_step(st)
+    spread1 = max(float(np.abs(st.w[i] - st.z[0]).max()) for i in range(st.size))
+    assert spread1 < spread0
