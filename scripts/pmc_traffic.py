@@ -49,7 +49,8 @@ def main():
     p = argparse.ArgumentParser()
     p.add_argument("--out", required=True)
     p.add_argument("--key-suffix", required=True, help="e.g. resnet50/R8/m1 (matches bench.py)")
-    p.add_argument("--alg-bytes", type=float, default=None, help="algorithmic bytes per launch, for the ratio")
+    p.add_argument("--alg-bytes", action="append", default=[],
+                   help="KERNEL=BYTES algorithmic bytes per launch of KERNEL (repeatable), for the ratio")
     p.add_argument("dirs", nargs="+")
     a = p.parse_args()
     vals = collect(a.dirs)
@@ -70,9 +71,10 @@ def main():
             entry["read_bytes_per_launch"] = 2 * fetch * 1024
             entry["write_bytes_per_launch"] = write * 1024
             entry["hbm_bytes_per_launch"] = 2 * fetch * 1024 + write * 1024
-            if a.alg_bytes:
-                entry["alg_bytes_per_launch"] = a.alg_bytes
-                entry["traffic_over_alg"] = entry["hbm_bytes_per_launch"] / a.alg_bytes
+            alg = dict(x.split("=", 1) for x in a.alg_bytes)
+            if kern in alg:
+                entry["alg_bytes_per_launch"] = float(alg[kern])
+                entry["traffic_over_alg"] = entry["hbm_bytes_per_launch"] / float(alg[kern])
         entry["correction"] = "read = 2*FETCH_SIZE KiB (gfx950 half-count of 16B/lane streams), write = WRITE_SIZE KiB"
         out[f"{kern}/{a.key_suffix}"] = entry
     os.makedirs(os.path.dirname(os.path.abspath(a.out)), exist_ok=True)
