@@ -457,6 +457,27 @@ cbx::SmaArgs offset_args(const cbx::SmaArgs &a, int64_t start4, int64_t len4) {
   return b;
 }
 
+// The reference records synched / base->updated (sma.c:177,204) and one
+// replica->updated per replica (sma.c:115,222) at points that, in this
+// pipeline, are all the same: the end of the step on the sync stream.  One
+// event per device stands for all of them (cbx_step_event); each extra
+// record is a marker packet costing GPU time between steps.  With timing
+// on, the step's last dispatch already timestamps a ring event at its end;
+// that event is the step event and no marker is added.
+int finish_step(cbx_context *c) {
+  for (Device &d : c->devs) {
+    HIP_TRY(hipSetDevice(d.hip_id));
+    if (c->timing && !d.ring.empty()) {
+      const int prev = (d.ring_pos + Device::kRing - 1) % Device::kRing;
+      d.step_event = d.ring[(size_t)prev * 4 + (d.ring_split[prev] == 0 ? EV_A : EV_B)];
+    } else {
+      HIP_TRY(hipEventRecord(d.synched, d.stream));
+      d.step_event = d.synched;
+    }
+  }
+  return CBX_OK;
+}
+
 int sma_step(cbx_context *c, int first) {
   const bool mom = c->has_last && c->model.conf.momentum > 0;  // sma.c:150 (base conf)
   std::vector<cbx::SmaArgs> args(c->devs.size());
@@ -606,29 +627,78 @@ int sma_step(cbx_context *c, int first) {
     c->last_step_split = true;
   }
 
-  // The reference records synched / base->updated (sma.c:177,204) and one
-  // replica->updated per replica (sma.c:115,222) at points that, in this
-  // pipeline, are all the same: the end of the step on the sync stream.  One
-  // event per device stands for all of them (cbx_step_event); each extra
-  // record is a marker packet costing GPU time between steps.  With timing
-  // on, the step's last dispatch already timestamps a ring event at its end;
-  // that event is the step event and no marker is added.
-  for (size_t k = 0; k < c->devs.size(); ++k) {
-    Device &d = c->devs[k];
-    HIP_TRY(hipSetDevice(d.hip_id));
-    if (c->timing && !d.ring.empty()) {
-      const int prev = (d.ring_pos + Device::kRing - 1) % Device::kRing;
-      d.step_event = d.ring[(size_t)prev * 4 + (d.ring_split[prev] == 0 ? EV_A : EV_B)];
-    } else {
-      HIP_TRY(hipEventRecord(d.synched, d.stream));
-      d.step_event = d.synched;
-    }
+  TRY(finish_step(c));
+  for (Device &d : c->devs)
     for (int id : d.replicas) {
       if (id < first || !c->locked[id]) continue;
       c->replicas[id]->conf.copy = 0;  // sma.c:220 (a no-op unless a copy happened)
     }
-  }
   return CBX_OK;
+}
+
+// ---------------------------------------------------------------------------
+// Synchronous SGD barrier (update model WORKER), synch/synchronoussgd.c:13-106
+// with common.c:3-57 (all-reduce) and :198-220 (base -> replicas).  The
+// reference's SINGLE_GPU variant is disabled like SMA's (:5-11); G = 1 runs
+// the multi-GPU algorithm with an identity all-reduce, in one kernel.
+// ---------------------------------------------------------------------------
+int ssgd_step(cbx_context *c, int first) {
+  if (c->model.wpc <= 0) return fail(CBX_ERR_STATE, "S-SGD needs the work per clock (setModelWorkPerClock)");
+  const float ratio = (float)(1.0 / (double)(float)c->model.wpc);  // synchronoussgd.c:55
+  const bool mom = c->has_last && c->model.conf.momentum > 0;        // :64
+  const bool split = c->G > 1 || c->force_split;
+  if (split && c->G == 1 && c->devs[0].comm == nullptr) {
+    Device &d = c->devs[0];
+    HIP_TRY(hipSetDevice(d.hip_id));
+    int dev = d.hip_id;
+    NCCL_TRY(ncclCommInitAll(&d.comm, 1, &dev));
+  }
+  std::vector<cbx::SsgdArgs> args(c->devs.size());
+  for (size_t k = 0; k < c->devs.size(); ++k) {
+    Device &d = c->devs[k];
+    cbx::SsgdArgs &a = args[k];
+    std::memset(&a, 0, sizeof(a));
+    int r = 0;
+    for (int id : d.replicas) {
+      if (id < first || !c->locked[id]) continue;  // common.c:208
+      if (r >= cbx::kMaxReplicas) return fail(CBX_ERR_UNSUPPORTED, "too many replicas on one device");
+      a.w[r++] = reinterpret_cast<cbx::v4f *>(replica_dev(d, *c->replicas[id], CBX_BUF_DATA));
+    }
+    a.nrep = r;
+    a.z = reinterpret_cast<cbx::v4f *>(base_dev(c, d, CBX_BUF_DATA));
+    a.last = mom ? reinterpret_cast<cbx::v4f *>(base_dev(c, d, CBX_BUF_LAST)) : nullptr;
+    a.acc = reinterpret_cast<cbx::v4f *>(base_dev(c, d, CBX_BUF_GRADIENT));
+    a.D = split ? reinterpret_cast<const cbx::v4f *>(base_dev(c, d, CBX_BUF_DIFF)) : a.acc;
+    a.n4 = c->n4;
+    a.ratio = ratio;
+    a.momentum = mom ? c->model.conf.momentum : 0.0f;
+  }
+  if (split) {
+    for (Device &d : c->devs) {
+      HIP_TRY(hipSetDevice(d.hip_id));
+      TRY(mark(c, d, EV_START));
+    }
+    NCCL_TRY(ncclGroupStart());
+    for (Device &d : c->devs) {
+      HIP_TRY(hipSetDevice(d.hip_id));
+      NCCL_TRY(ncclAllReduce(base_dev(c, d, CBX_BUF_GRADIENT), base_dev(c, d, CBX_BUF_DIFF), (size_t)c->n4 * 4,
+                             ncclFloat, ncclSum, d.comm, d.stream));
+    }
+    NCCL_TRY(ncclGroupEnd());
+  }
+  for (size_t k = 0; k < c->devs.size(); ++k) {
+    Device &d = c->devs[k];
+    HIP_TRY(hipSetDevice(d.hip_id));
+    cbx::LaunchConfig cfg = c->cfg;
+    cfg.num_cus = d.num_cus;
+    cbx::Timing t;
+    if (!split) t.start = ring_event(c, d, EV_START);
+    t.stop = ring_event(c, d, split ? EV_B : EV_A);
+    HIP_TRY(cbx::launch_ssgd_apply(args[k], cfg, d.stream, t));
+    ring_advance(c, d, split ? 2 : 0);
+  }
+  c->last_step_split = split;
+  return finish_step(c);
 }
 
 // ---------------------------------------------------------------------------
@@ -1071,10 +1141,16 @@ int cbx_synchronise(cbx_context *c, int first, int clock, int autotune, int push
   // executioncontext.c:2287-2315: SYNCHRONOUSEAMSGD (3) routes to SMA because
   // ELASTIC_AVERAGE is #undef'd; SMA is 7.  The other update models are not
   // this library's path.
+  // WORKER (1) is synchronous SGD (executioncontext.c:2277-2279), which shares
+  // the base-model buffers and the all-reduce.
   const int type = c->model.type;
-  if (type != CBX_UPDATE_SMA && type != CBX_UPDATE_SYNCHRONOUSEAMSGD)
-    return fail(CBX_ERR_UNSUPPORTED, "update model %d is not the SMA path", type);
-  TRY(sma_step(c, first));
+  if (type == CBX_UPDATE_WORKER) {
+    TRY(ssgd_step(c, first));
+  } else if (type == CBX_UPDATE_SMA || type == CBX_UPDATE_SYNCHRONOUSEAMSGD) {
+    TRY(sma_step(c, first));
+  } else {
+    return fail(CBX_ERR_UNSUPPORTED, "update model %d is not on this library's path (SMA, SYNCHRONOUSEAMSGD, WORKER)", type);
+  }
   if (autotune < 0) TRY(cbx_del_model(c));
   if (autotune > 0) TRY(cbx_add_model(c));
   // modelmanager.c:259-265: clock of every locked replica.
@@ -1158,11 +1234,46 @@ int cbx_del_model(cbx_context *c) {
 }
 
 // ---- replica optimiser step (kernels/optimisers/sma.cu:3-100) -------------
+// crossbowKernelOptimiserSynchronousSGD, kernels/optimisers/synchronoussgd.cu:3-56:
+// weight decay on the replica gradient, then the lr-scaled gradient is added
+// into the device's base-model gradient on the sync stream (:38-52).
+static int ssgd_worker_step(cbx_context *c, Replica &r, Device &d, int task, hipStream_t st) {
+  SolverConf &conf = r.conf;
+  if (conf.momentumMethod == 1) return fail(CBX_ERR_UNSUPPORTED, "Nesterov's momentum has been disabled");  // :42-44
+  float lr = 0.0f;
+  TRY(conf.learning_rate(task, &lr));
+  cbx::SsgdArgs a;
+  std::memset(&a, 0, sizeof(a));
+  a.wsrc = reinterpret_cast<const cbx::v4f *>(replica_dev(d, r, CBX_BUF_DATA));
+  a.g = reinterpret_cast<cbx::v4f *>(replica_dev(d, r, CBX_BUF_GRADIENT));
+  a.acc = reinterpret_cast<cbx::v4f *>(base_dev(c, d, CBX_BUF_GRADIENT));
+  a.n4 = c->n4;
+  a.rate = -lr;  // :46
+  a.wd = conf.weightDecay;
+  HIP_TRY(hipSetDevice(d.hip_id));
+  if (st != d.stream) {
+    // :38-40: the sync stream waits for the task's gradient.
+    if (!r.client) HIP_TRY(hipEventCreateWithFlags(&r.client, hipEventDisableTiming));
+    HIP_TRY(hipEventRecord(r.client, st));
+    HIP_TRY(hipStreamWaitEvent(d.stream, r.client, 0));
+  }
+  cbx::LaunchConfig cfg = c->cfg;
+  cfg.num_cus = d.num_cus;
+  cfg.blocks_per_cu = 0;
+  HIP_TRY(cbx::launch_ssgd_accumulate(a, cfg, d.stream, {}));
+  return CBX_OK;
+}
+
 int cbx_replica_optimise(cbx_context *c, int id, int task, void *stream) {
   TRY(check_replica(c, id, true));
   Replica &r = *c->replicas[id];
   Device &d = c->devs[r.local];
   SolverConf &conf = r.conf;
+  const int type = c->model.type;
+  if (type == CBX_UPDATE_WORKER)
+    return ssgd_worker_step(c, r, d, task, stream ? reinterpret_cast<hipStream_t>(stream) : d.stream);
+  if (type != CBX_UPDATE_SMA && type != CBX_UPDATE_SYNCHRONOUSEAMSGD)
+    return fail(CBX_ERR_UNSUPPORTED, "update model %d has no optimiser step in this library", type);
   if (conf.momentum > 0 && conf.momentumMethod == 1)
     return fail(CBX_ERR_UNSUPPORTED, "Nesterov's momentum has been disabled");  // sma.cu:46-48
   if (conf.momentum > 0 && !c->has_last)

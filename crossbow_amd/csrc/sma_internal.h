@@ -84,6 +84,29 @@ struct OptArgs {
   int pad_;
 };
 hipError_t launch_sma_optimise(const OptArgs &a, const LaunchConfig &cfg, hipStream_t stream, Timing t = {});
+// Synchronous SGD (update model WORKER = 1), the other synchronous model that
+// shares the base-model buffers and the all-reduce.
+struct SsgdArgs {
+  v4f *w[kMaxReplicas];  // locked replicas on this device (barrier copy), id order
+  v4f *z;                // base->data
+  v4f *last;             // base->last (momentum > 0 only)
+  v4f *acc;              // base->gradient: accumulated lr-scaled replica gradients
+  const v4f *D;          // base->diff: all-reduced acc (== acc at G = 1)
+  const v4f *wsrc;       // task step: replica->data (weight decay input)
+  v4f *g;                // task step: replica->gradient
+  int64_t n4;
+  float rate;            // task step: -learning rate (synchronoussgd.cu:46)
+  float wd;              // task step: weight decay
+  float ratio;           // barrier: 1 / wpc (synchronoussgd.c:55)
+  float momentum;        // barrier: base conf->momentum (synchronoussgd.c:64)
+  int nrep;
+  int pad_;
+};
+// Per task (synchronoussgd.cu:3-56): g = fma(wd, w, g); acc = fma(rate, g, acc).
+hipError_t launch_ssgd_accumulate(const SsgdArgs &a, const LaunchConfig &cfg, hipStream_t stream, Timing t = {});
+// Barrier (synchronoussgd.c:13-106, common.c:198-220): D *= 1/wpc; momentum;
+// z += D; acc = 0; every locked replica := z.
+hipError_t launch_ssgd_apply(const SsgdArgs &a, const LaunchConfig &cfg, hipStream_t stream, Timing t = {});
 // Synthetic normal fill.
 hipError_t launch_fill_normal(float *out, int64_t n, uint64_t seed, float sigma,
                               const float *mean, hipStream_t stream);

@@ -282,6 +282,64 @@ __global__ __launch_bounds__(512) void sma_optimise_kernel(const OptArgs a) {
 }
 
 // ---------------------------------------------------------------------------
+// Synchronous SGD (WORKER).  Task step, on the sync stream so replicas add
+// into the device's one accumulator in enqueue order (synchronoussgd.cu:3-56):
+//   g = fma(wd, w, g)        :20-26 (wd > 0; g written back)
+//   acc = fma(rate, g, acc)  :46-52
+// Reads g, acc (, w) and writes acc (, g): 12n B (+8n with weight decay).
+// ---------------------------------------------------------------------------
+template <bool WD, int P>
+__global__ __launch_bounds__(512) void ssgd_accumulate_kernel(const SsgdArgs a) {
+  const uint32_t trip = gridDim.x * blockDim.x;
+  const uint32_t n4 = (uint32_t)a.n4;
+  const v4f rate = a.rate, wd = a.wd;
+  for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < n4; e += trip) {
+    const uint32_t i = e * 16u;
+    v4f g = ldo<P>(a.g, i);
+    const v4f acc = ldo<P>(a.acc, i);
+    v4f w;
+    if constexpr (WD) w = ldo<P>(a.wsrc, i);
+    __builtin_amdgcn_sched_barrier(0);
+    if constexpr (WD) {
+      g = vfma(wd, w, g);
+      sto<P>(a.g, i, g);
+    }
+    sto<P>(a.acc, i, vfma(rate, g, acc));
+  }
+}
+
+// S-SGD barrier, per device after the all-reduce (synchronoussgd.c:13-106):
+//   D = ratio * D                     :55-62 (sscal, ratio = 1/wpc)
+//   D = fma(mu, last, D); last = D    :64-76 (base momentum, NOT forced to 0.9)
+//   z = fma(1, D, z)                  :79-84
+//   acc = 0                           :103
+//   w_i = z for locked replicas       common.c:198-220
+// Reads D, z (, last) and writes z, acc, R x w (, last).
+template <bool MOM, int P>
+__global__ __launch_bounds__(512) void ssgd_apply_kernel(const SsgdArgs a) {
+  const uint32_t trip = gridDim.x * blockDim.x;
+  const uint32_t n4 = (uint32_t)a.n4;
+  const v4f ratio = a.ratio, mu = a.momentum, one = 1.0f, zero = 0.0f;
+  for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < n4; e += trip) {
+    const uint32_t i = e * 16u;
+    v4f D = ldo<P>(a.D, i);
+    v4f z = ldo<P>(a.z, i);
+    v4f l;
+    if constexpr (MOM) l = ldo<P>(a.last, i);
+    __builtin_amdgcn_sched_barrier(0);
+    D = ratio * D;
+    if constexpr (MOM) {
+      D = vfma(mu, l, D);
+      sto<P>(a.last, i, D);
+    }
+    z = vfma(one, D, z);
+    sto<P>(a.z, i, z);
+    sto<P>(a.acc, i, zero);
+    for (int r = 0; r < a.nrep; ++r) sto<P>(a.w[r], i, z);
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Synthetic inputs: splitmix64 -> Box-Muller in double.
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
@@ -431,6 +489,38 @@ hipError_t launch_sma_optimise(const OptArgs &a, const LaunchConfig &cfg, hipStr
       if (wd) hipExtLaunchKernelGGL((sma_optimise_kernel<false, true, 0>), g, b, 0, stream, t.start, t.stop, 0, a);
       else hipExtLaunchKernelGGL((sma_optimise_kernel<false, false, 0>), g, b, 0, stream, t.start, t.stop, 0, a);
     }
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_ssgd_accumulate(const SsgdArgs &a, const LaunchConfig &cfg, hipStream_t stream, Timing t) {
+  LaunchConfig c = cfg;
+  c.unroll = 1;
+  const dim3 g = grid_for(a.n4, c);
+  const dim3 b(c.block);
+  const bool wd = a.wd > 0.0f;
+  if (cfg.policy == 1) {
+    if (wd) hipExtLaunchKernelGGL((ssgd_accumulate_kernel<true, 1>), g, b, 0, stream, t.start, t.stop, 0, a);
+    else hipExtLaunchKernelGGL((ssgd_accumulate_kernel<false, 1>), g, b, 0, stream, t.start, t.stop, 0, a);
+  } else {
+    if (wd) hipExtLaunchKernelGGL((ssgd_accumulate_kernel<true, 0>), g, b, 0, stream, t.start, t.stop, 0, a);
+    else hipExtLaunchKernelGGL((ssgd_accumulate_kernel<false, 0>), g, b, 0, stream, t.start, t.stop, 0, a);
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_ssgd_apply(const SsgdArgs &a, const LaunchConfig &cfg, hipStream_t stream, Timing t) {
+  LaunchConfig c = cfg;
+  c.unroll = 1;
+  const dim3 g = grid_for(a.n4, c);
+  const dim3 b(c.block);
+  const bool mom = a.momentum > 0.0f;
+  if (cfg.policy == 1) {
+    if (mom) hipExtLaunchKernelGGL((ssgd_apply_kernel<true, 1>), g, b, 0, stream, t.start, t.stop, 0, a);
+    else hipExtLaunchKernelGGL((ssgd_apply_kernel<false, 1>), g, b, 0, stream, t.start, t.stop, 0, a);
+  } else {
+    if (mom) hipExtLaunchKernelGGL((ssgd_apply_kernel<true, 0>), g, b, 0, stream, t.start, t.stop, 0, a);
+    else hipExtLaunchKernelGGL((ssgd_apply_kernel<false, 0>), g, b, 0, stream, t.start, t.stop, 0, a);
   }
   return hipGetLastError();
 }

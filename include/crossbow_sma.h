@@ -37,6 +37,7 @@ extern "C" {
 #define CBX_ERR_UNSUPPORTED -8  /* outside this library's scope   */
 
 /* Update model ids, uk/ac/imperial/lsds/crossbow/types/UpdateModel.java:5 */
+#define CBX_UPDATE_WORKER            1   /* synchronous SGD: synch/synchronoussgd.c */
 #define CBX_UPDATE_SYNCHRONOUSEAMSGD 3   /* routed to SMA: clib-multigpu/utils.h:56-57 */
 #define CBX_UPDATE_SMA               7
 
@@ -119,7 +120,10 @@ int cbx_lock_any (cbx_context *ctx);
 int cbx_merge (cbx_context *ctx, int pull, int *first);
 /* TheGPU.synchronise(IIIZ)  GPU.c:1133-1140 -> executioncontext.c:2262-2334
  * -> synch/sma.c:233-248.  Enqueues the SMA step on each device's model
- * synchronisation stream and returns without blocking the host.          */
+ * synchronisation stream and returns without blocking the host.  Update
+ * models SMA (7) and SYNCHRONOUSEAMSGD (3) run SMA; WORKER (1) runs the
+ * synchronous-SGD barrier (synch/synchronoussgd.c:13-106, needs the work
+ * per clock); any other is CBX_ERR_UNSUPPORTED.                          */
 int cbx_synchronise (cbx_context *ctx, int first, int clock, int autotune, int push);
 /* TheGPU.unlockAny() GPU.c:1142-1149 -> modelmanager.c:233-245           */
 int cbx_unlock_any (cbx_context *ctx);
@@ -150,7 +154,11 @@ int cbx_replica_set_copy (cbx_context *ctx, int id, int flag);
  * configuration (may raise its _copy flag, solverconfiguration.c:133,147).
  * Enqueued on `stream` (a hipStream_t; NULL = the replica device's sync
  * stream); the sync stream then waits for it (sma.cu:79-81).  Nesterov
- * momentum is CBX_ERR_UNSUPPORTED, as in the reference (sma.cu:46-48).  */
+ * momentum is CBX_ERR_UNSUPPORTED, as in the reference (sma.cu:46-48).
+ * Under update model WORKER the step is crossbowKernelOptimiserSynchronousSGD
+ * (synchronoussgd.cu:3-56) instead: weight decay, then the lr-scaled
+ * gradient is added into the device's base-model gradient on the sync
+ * stream, to be all-reduced and applied at the next barrier.            */
 int cbx_replica_optimise (cbx_context *ctx, int id, int task, void *stream);
 /* Global device index a replica lives on (id % G). */
 int cbx_replica_device (cbx_context *ctx, int id);

@@ -63,6 +63,15 @@ def lib():
             f = getattr(L, name)
             f.restype = None if name == "cbo_sma_optimise" else ctypes.c_int
             f.argtypes = [ctypes.c_size_t, ctypes.c_float, ctypes.c_float, ctypes.c_float, fp, fp, fp, fp]
+        for name in ("cbo_ssgd_worker", "cbo_ssgd_worker_blas"):
+            f = getattr(L, name)
+            f.restype = None if name == "cbo_ssgd_worker" else ctypes.c_int
+            f.argtypes = [ctypes.c_size_t, ctypes.c_float, ctypes.c_float, fp, fp, fp]
+        for name in ("cbo_ssgd_sync", "cbo_ssgd_sync_blas"):
+            f = getattr(L, name)
+            f.restype = None if name == "cbo_ssgd_sync" else ctypes.c_int
+            f.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_size_t, ctypes.c_int, ctypes.c_float,
+                          fpp, fpp, fpp, fpp, ip, ctypes.c_int, fp]
         L.cbo_blas_open.restype = ctypes.c_int
         L.cbo_blas_open.argtypes = [ctypes.c_char_p]
         L.cbo_blas_name.restype = ctypes.c_char_p
@@ -199,6 +208,32 @@ def sma_optimise(rate: float, momentum: float, wd: float, w: np.ndarray, g: np.n
             raise RuntimeError("OpenBLAS replay unavailable")
     else:
         lib().cbo_sma_optimise(w.size, rate, momentum, wd, _fp(w), _fp(g), lp, _fp(s))
+
+
+def ssgd_worker(rate: float, wd: float, w: np.ndarray, g: np.ndarray, acc: np.ndarray, blas: bool = False) -> None:
+    """S-SGD task step (kernels/optimisers/synchronoussgd.cu:3-56), in place on g and acc."""
+    if blas:
+        if not lib().cbo_blas_is_open():
+            blas_open()
+        if lib().cbo_ssgd_worker_blas(w.size, rate, wd, _fp(w), _fp(g), _fp(acc)) != 0:
+            raise RuntimeError("OpenBLAS replay unavailable")
+    else:
+        lib().cbo_ssgd_worker(w.size, rate, wd, _fp(w), _fp(g), _fp(acc))
+
+
+def ssgd_sync(st: SmaState, acc: List[np.ndarray], wpc: int, blas: bool = False) -> None:
+    """S-SGD barrier (synch/synchronoussgd.c:13-106) on ``st`` (z, last, w) and the
+    per-device accumulators ``acc``, in place.  ``st.momentum`` is the base momentum."""
+    lp = _fpp(st.last) if st.last is not None else _fpp([None] * st.G)
+    args = (st.G, st.size, st.n, int(wpc), st.momentum, _fpp(st.z), lp, _fpp(st.w), _fpp(acc),
+            st.locked.ctypes.data_as(ctypes.POINTER(ctypes.c_int)), st.first)
+    if blas:
+        if not lib().cbo_blas_is_open():
+            blas_open()
+        if lib().cbo_ssgd_sync_blas(*args, _fp(np.empty(2 * st.n, np.float32))) != 0:
+            raise RuntimeError("OpenBLAS replay unavailable")
+    else:
+        lib().cbo_ssgd_sync(*args, _fp(np.empty(st.n, np.float32)))
 
 
 def openblas_path() -> Optional[str]:

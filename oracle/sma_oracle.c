@@ -307,6 +307,89 @@ int cbo_sma_optimise_blas (size_t n, float rate, float momentum, float wd,
 }
 
 /* ---------------------------------------------------------------------- */
+/* Synchronous SGD (WORKER).                                               */
+/* ---------------------------------------------------------------------- */
+void cbo_ssgd_worker (size_t n, float rate, float wd, const float *w, float *g, float *acc) {
+	size_t k;
+	for (k = 0; k < n; ++k) {
+		float gk = g[k];
+		if (wd > 0) {
+			gk = fmaf (wd, w[k], gk);                                       /* synchronoussgd.cu:20-26 */
+			g[k] = gk;
+		}
+		acc[k] = fmaf (rate, gk, acc[k]);                                   /* synchronoussgd.cu:46-52 */
+	}
+}
+
+int cbo_ssgd_worker_blas (size_t n, float rate, float wd, const float *w, float *g, float *acc) {
+	if (! blas_saxpy)
+		return -1;
+	if (wd > 0)
+		blas_saxpy ((int) n, wd, w, 1, g, 1);
+	blas_saxpy ((int) n, rate, g, 1, acc, 1);
+	return 0;
+}
+
+static float ssgd_ratio (int wpc) {
+	return (float) (1.0 / (double) (float) wpc);                            /* synchronoussgd.c:55 */
+}
+
+void cbo_ssgd_sync (int G, int size, size_t n, int wpc, float momentum,
+		float **z, float **last, float **w, float **acc,
+		const int *locked, int first, float *scratch) {
+	int g, h, i;
+	size_t k;
+	float ratio = ssgd_ratio (wpc);
+	float *D = scratch;
+	memcpy (D, acc[0], n * sizeof(float));                                  /* common.c:43-52 */
+	for (h = 1; h < G; ++h)
+		for (k = 0; k < n; ++k)
+			D[k] = D[k] + acc[h][k];
+	for (g = 0; g < G; ++g) {
+		for (k = 0; k < n; ++k) {
+			float Dg = ratio * D[k];                                        /* synchronoussgd.c:55-62 */
+			if (momentum > 0) {
+				Dg = fmaf (momentum, last[g][k], Dg);                       /* :64-71 */
+				last[g][k] = Dg;                                            /* :74-75 */
+			}
+			z[g][k] = fmaf (1.0f, Dg, z[g][k]);                             /* :79-84 */
+		}
+		memset (acc[g], 0, n * sizeof(float));                              /* :103 */
+		for (i = first; i < size; ++i)
+			if (locked[i] && (i % G) == g)
+				memcpy (w[i], z[g], n * sizeof(float));                     /* common.c:206-214 */
+	}
+}
+
+int cbo_ssgd_sync_blas (int G, int size, size_t n, int wpc, float momentum,
+		float **z, float **last, float **w, float **acc,
+		const int *locked, int first, float *scratch) {
+	int g, h, i, N = (int) n;
+	size_t bytes = n * sizeof(float);
+	float ratio = ssgd_ratio (wpc);
+	float *sum = scratch, *D = scratch + n;
+	if (! blas_saxpy || ! blas_sscal)
+		return -1;
+	memcpy (sum, acc[0], bytes);
+	for (h = 1; h < G; ++h)
+		blas_saxpy (N, 1.0f, acc[h], 1, sum, 1);
+	for (g = 0; g < G; ++g) {
+		memcpy (D, sum, bytes);                                             /* base->diff of device g */
+		blas_sscal (N, ratio, D, 1);
+		if (momentum > 0) {
+			blas_saxpy (N, momentum, last[g], 1, D, 1);
+			memcpy (last[g], D, bytes);
+		}
+		blas_saxpy (N, 1.0f, D, 1, z[g], 1);
+		memset (acc[g], 0, bytes);
+		for (i = first; i < size; ++i)
+			if (locked[i] && (i % G) == g)
+				memcpy (w[i], z[g], bytes);
+	}
+	return 0;
+}
+
+/* ---------------------------------------------------------------------- */
 /* CPU affinity, clib-multigpu/CPU.c:39-60                                 */
 /* ---------------------------------------------------------------------- */
 int cbo_bind_core (int core) {

@@ -96,6 +96,25 @@ void cbo_sma_optimise (size_t n, float rate, float momentum, float wd,
 int cbo_sma_optimise_blas (size_t n, float rate, float momentum, float wd,
 		float *w, float *g, float *last, float *s);
 
+/* Synchronous SGD (update model WORKER), the other synchronous model on the  */
+/* same buffers.  Task step, crossbowKernelOptimiserSynchronousSGD           */
+/* (kernels/optimisers/synchronoussgd.cu:3-56): rate is -learningRate(task). */
+/*   g = fma(wd, w, g) if wd > 0 (:20-26);  acc = fma(rate, g, acc) (:46-52)  */
+void cbo_ssgd_worker (size_t n, float rate, float wd, const float *w, float *g, float *acc);
+int cbo_ssgd_worker_blas (size_t n, float rate, float wd, const float *w, float *g, float *acc);
+/* Barrier, synch/synchronoussgd.c:13-106 (+ common.c:3-57, 198-220), G     */
+/* devices in one address space.  acc[g] is each device's base gradient.    */
+/*   D = sum_g acc_g (rank order); per device: D' = (1/wpc) * D; if         */
+/*   momentum > 0: D' = fma(mu, last, D'), last = D'; z = fma(1, D', z);    */
+/*   acc_g = 0; every locked replica i >= first on g: w_i = z_g.            */
+/* scratch: n floats (blas: 2n).                                            */
+void cbo_ssgd_sync (int G, int size, size_t n, int wpc, float momentum,
+		float **z, float **last, float **w, float **acc,
+		const int *locked, int first, float *scratch);
+int cbo_ssgd_sync_blas (int G, int size, size_t n, int wpc, float momentum,
+		float **z, float **last, float **w, float **acc,
+		const int *locked, int first, float *scratch);
+
 /* dlopen an OpenBLAS build; returns 0 on success.  `path` may be NULL to  */
 /* probe the usual numpy/scipy wheels.  Records the library actually used. */
 int cbo_blas_open (const char *path);

@@ -153,3 +153,55 @@ def test_nesterov_is_unsupported():
         assert e.value.code == _lib.CBX_ERR_UNSUPPORTED
     finally:
         g.free()
+
+
+@pytest.mark.parametrize("momentum", [0.0, 0.9])
+@pytest.mark.parametrize("split", [False, True])
+def test_ssgd_clock_loop_bitexact(momentum, split):
+    # Synchronous SGD (update model WORKER): task steps add
+    # lr-scaled gradients into the base gradient; the barrier all-reduces it,
+    # scales by 1/wpc, applies base momentum and copies z to every replica.
+    from crossbow_amd import BUF_DATA, BUF_GRADIENT, BUF_LAST, TheGPU
+    from tests.helpers import upload
+    n, R, wpc, clocks = 50_001, 3, 6, 2
+    g = TheGPU()
+    g.init([0])
+    try:
+        g.setModel(1, 4 * n)
+        g.setModelVariable(0, 1, [n], 4 * n)
+        g.setModelWorkPerClock(wpc)
+        g.setUpdateModelType(1)
+        g.setMomentum(momentum, 0)
+        g.setWeightDecay(1e-4)
+        g.setLearningRateDecayPolicyFixed(0.05)
+        g.setModelManager(R, 1)  # SSP: the barrier may skip a busy replica
+        if split:
+            g.set_force_split(True)
+        st = O.make_state(n, 1, R, 0.1, momentum)
+        st.locked[2] = 0  # hold replica 2 (SSP): not copied at the barrier
+        upload(g, st)
+        acc = [np.zeros(n, np.float32)]
+        task = 0
+        for clock in range(1, clocks + 1):
+            for k in range(wpc):
+                i = k % R
+                gr = O.fill_normal(n, 2000 + task, 0.01)
+                g.replica_write(i, BUF_GRADIENT, gr)
+                g.replica_optimise(i, task)
+                O.ssgd_worker(np.float32(-0.05), 1e-4, st.w[i], gr, acc[0])
+                task += 1
+            g.replica_lock(2)
+            g.lockAny()
+            g.synchronise(0, clock, 0, False)
+            g.unlockAny()
+            g.replica_unlock(2)
+            O.ssgd_sync(st, acc, wpc)
+        g.wait()
+        assert_bitexact(g.base_read(0, BUF_DATA), st.z[0], "z")
+        assert_bitexact(g.base_read(0, BUF_GRADIENT), acc[0], "base gradient reset")
+        if momentum > 0:
+            assert_bitexact(g.base_read(0, BUF_LAST), st.last[0], "last")
+        for i in range(R):
+            assert_bitexact(g.replica_read(i, BUF_DATA), st.w[i], f"w[{i}]")
+    finally:
+        g.free()

@@ -182,11 +182,21 @@ def test_update_type_routing():
         compare_states(download(g, st), want)
     finally:
         g.free()
-    g = make_gpu(n, R, 0.1, 0.0, update_type=1)  # WORKER: not this path
+    from crossbow_amd import _lib
+    g = make_gpu(n, R, 0.1, 0.0, update_type=5)  # HOGWILD: not this library's path
     try:
         g.lockAny()
-        with pytest.raises(CbxError):
+        with pytest.raises(CbxError) as e:
             g.synchronise(0, 1, 0, False)
+        assert e.value.code == _lib.CBX_ERR_UNSUPPORTED
+    finally:
+        g.free()
+    g = make_gpu(n, R, 0.1, 0.0, update_type=1)  # WORKER (S-SGD) needs the work per clock
+    try:
+        g.lockAny()
+        with pytest.raises(CbxError) as e:
+            g.synchronise(0, 1, 0, False)
+        assert e.value.code == _lib.CBX_ERR_STATE
     finally:
         g.free()
 

@@ -176,3 +176,30 @@ def test_optimiser_then_sma_moves_replicas_toward_base():
     O.sma_step(st)
     spread1 = max(float(np.abs(st.w[i] - st.z[0]).max()) for i in range(st.size))
     assert spread1 < spread0
+
+
+@pytest.mark.parametrize("G", [1, 2, 4])
+@pytest.mark.parametrize("momentum", [0.0, 0.9])
+def test_ssgd_restatement_equals_openblas_sequence(G, momentum):
+    # Synchronous SGD (WORKER): task steps (synchronoussgd.cu:3-56) then the
+    # barrier (synchronoussgd.c:13-106) -- fmaf restatement == BLAS replay.
+    n, R = 2053, 2
+    st = O.make_state(n, G, R, 0.1, momentum)
+    st.locked[0] = 0
+    grads = [O.fill_normal(n, 600 + i, 0.01) for i in range(st.size)]
+    outs = []
+    for blas in (False, True):
+        s2 = st.clone()
+        acc = [np.zeros(n, np.float32) for _ in range(G)]
+        gs = [x.copy() for x in grads]
+        for i in range(s2.size):
+            O.ssgd_worker(np.float32(-0.05), 1e-4, s2.w[i], gs[i], acc[i % G], blas=blas)
+        O.ssgd_sync(s2, acc, 8, blas=blas)
+        outs.append((s2, acc, gs))
+    (a, acc_a, g_a), (b, acc_b, g_b) = outs
+    for x, y in zip(a.z + a.w + (a.last or []) + acc_a + g_a, b.z + b.w + (b.last or []) + acc_b + g_b):
+        assert _eq(x, y)
+    assert all(not x.any() for x in acc_a), "barrier resets base->gradient (synchronoussgd.c:103)"
+    assert _eq(a.w[0], st.w[0]), "unlocked replica keeps its data"
+    for i in range(1, a.size):
+        assert _eq(a.w[i], a.z[i % G])
