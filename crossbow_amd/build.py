@@ -36,7 +36,8 @@ def _sources():
 
 
 def _deps():
-    return _sources() + [os.path.join(CSRC, "sma_internal.h"), os.path.join(ROOT, "include", "crossbow_sma.h")]
+    return _sources() + [os.path.join(CSRC, "sma_internal.h"), os.path.join(ROOT, "include", "crossbow_sma.h"),
+                         os.path.abspath(__file__)]
 
 
 def _stale(target: str, deps) -> bool:
@@ -51,6 +52,9 @@ def build_lib(force: bool = False, verbose: bool = False) -> str:
         return LIB
     tmp = LIB + ".tmp"
     cmd = [_hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wall",
+           # fp32 results must equal the reference's cuBLAS op order bit for bit: every
+           # fma is written explicitly, nothing may be contracted behind our back.
+           "-ffp-contract=off",
            "-I", os.path.join(ROOT, "include"), "-o", tmp] + _sources() + ["-lrccl", "-lpthread"]
     if verbose:
         print(" ".join(cmd), flush=True)
