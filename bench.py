@@ -77,6 +77,31 @@ def alg_bytes(n, R, momentum, G):
     return a + (12 + 8 * m) * n, a
 
 
+def cpu_baseline_threads(args, n_full, threads):
+    """Same replay with OpenBLAS on `threads` threads (no pinning): the
+    'all cores' row of BASELINE.md 3, capped at the GPU box's CPU share."""
+    from oracle import oracle as O
+    n = min(args.cpu_elements, n_full)
+    O.blas_open()
+    O.blas_set_threads(threads)
+    st = O.make_state(n, 1, args.replicas, args.alpha, args.momentum)
+    try:
+        O.sma_step_blas(st)
+        steps, t0 = 0, O.now()
+        while True:
+            O.sma_step_blas(st)
+            steps += 1
+            el = O.now() - t0
+            if el >= args.cpu_seconds / 2:
+                break
+    finally:
+        O.blas_set_threads(1)
+    b, _ = alg_bytes(n, args.replicas, args.momentum, 1)
+    return {"value": round(b * steps / el / 1e9, 3), "unit": "GB/s", "cores": threads, "kind": "port",
+            "sample": f"{n} fp32 elements x {args.replicas} replicas, {steps} steps in {el:.1f} s, "
+                      f"OpenBLAS on {threads} threads"}
+
+
 def cpu_baseline(args, n_full):
     """The reference's call sequence (memset, memcpy + 3 saxpy per replica,
     momentum, apply) on OpenBLAS, 1 thread bound to core 0 like TheCPU.bind(0)
@@ -297,7 +322,11 @@ def main():
                 "end_to_end_GBs": round(step_bytes / tot / 1e9, 2),
             }
         if not args.no_cpu_baseline:
+            # multithreaded first: OpenBLAS's pool must not start out bound to core 0
+            threads = max(1, min(16, len(os.sched_getaffinity(0))))
+            mt = cpu_baseline_threads(args, n, threads)
             result["cpu_baseline"] = cpu_baseline(args, n)
+            result["cpu_baseline_multithread"] = mt
         else:
             result["cpu_baseline"] = None
 
