@@ -88,3 +88,18 @@ def test_jni_shim_defines_model_path_natives():
     # Every native forwards to a declared C-ABI function.
     used = set(re.findall(r"\b(cbx_[a-z0-9_]+)\s*\(", src))
     assert used <= set(declared_functions()), used - set(declared_functions())
+
+
+def test_jni_shim_compiles_against_the_c_abi():
+    # No JDK in this image: compile-check the shim against a minimal jni.h
+    # stand-in (tests/jni_stub/jni.h, JNI-spec signatures of the few JNIEnv
+    # functions it calls) so a type mismatch with crossbow_sma.h is caught.
+    import shutil
+    import subprocess
+    gcc = shutil.which("gcc")
+    if gcc is None:
+        pytest.skip("no gcc")
+    r = subprocess.run([gcc, "-fsyntax-only", "-Wall", "-Wextra", "-Werror", "-std=c11",
+                        "-I", os.path.join(ROOT, "tests", "jni_stub"), "-I", os.path.join(ROOT, "include"),
+                        JNI_SRC], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
