@@ -91,6 +91,7 @@ SIGNATURES = {
     "cbx_override_model_data": (_I, [_P, _CP]),
     "cbx_add_model": (_I, [_P]),
     "cbx_del_model": (_I, [_P]),
+    "cbx_average_batchnorm_stats": (_I, [_P, _I, _IP, _PP, _PP, _IP]),
     "cbx_replica_lock": (_I, [_P, _I]),
     "cbx_replica_unlock": (_I, [_P, _I]),
     "cbx_replica_task_done": (_I, [_P, _I]),

@@ -175,6 +175,10 @@ struct Device {
   std::vector<hipEvent_t> bucket_acc;  // per bucket: kernel A done (stream -> comm_stream)
   std::vector<hipEvent_t> bucket_red;  // per bucket: all-reduce done (comm_stream -> stream)
   ncclComm_t comm = nullptr;
+  cbx::BnSegment *bn_table = nullptr;  // batch-norm averaging: segment table (device)
+  size_t bn_table_bytes = 0;
+  float *bn_scratch = nullptr;         // packed statistics, all-reduced
+  size_t bn_scratch_bytes = 0;
   int num_cus = 256;
   // Arena: [base data][base gradient(ctrl+acc)][base diff(ctrl+D)][base last]
   //        then per replica [data][diff][last][gradient].
@@ -363,6 +367,8 @@ void close_device(Device &d) {
   if (d.comm_stream) (void)hipStreamSynchronize(d.comm_stream);
   if (d.comm) (void)ncclCommDestroy(d.comm);
   if (d.arena) (void)hipFree(d.arena);
+  if (d.bn_table) (void)hipFree(d.bn_table);
+  if (d.bn_scratch) (void)hipFree(d.bn_scratch);
   if (d.host) (void)hipHostFree(d.host);
   if (d.synched) (void)hipEventDestroy(d.synched);
   for (int k = 0; k < EV_COUNT; ++k)
@@ -1304,6 +1310,76 @@ int cbx_replica_optimise(cbx_context *c, int id, int task, void *stream) {
     if (!r.client) HIP_TRY(hipEventCreateWithFlags(&r.client, hipEventDisableTiming));
     HIP_TRY(hipEventRecord(r.client, st));
     HIP_TRY(hipStreamWaitEvent(d.stream, r.client, 0));
+  }
+  return CBX_OK;
+}
+
+// ---- batch-norm running statistics (cudnn/cudnnbatchnormparams.c:157-222) --
+static int grow(void **p, size_t *have, size_t need) {
+  if (*have >= need) return CBX_OK;
+  if (*p) HIP_TRY(hipFree(*p));
+  *p = nullptr;
+  *have = 0;
+  HIP_TRY(hipMalloc(p, need));
+  *have = need;
+  return CBX_OK;
+}
+
+int cbx_average_batchnorm_stats(cbx_context *c, int layers, const int *elements, float *const *mean,
+                                float *const *variance, const int *updated) {
+  TRY(check_ctx(c));
+  if (layers < 0 || (layers > 0 && (!elements || !mean || !variance || !updated)))
+    return fail(CBX_ERR_INVALID, "bad batch-norm statistics arguments");
+  if (layers == 0) return CBX_OK;
+  // :165-166: nothing to average with one device.
+  const bool run = c->G > 1 || c->force_split;
+  if (!run) return CBX_OK;
+  if (c->G == 1 && c->devs[0].comm == nullptr) {
+    Device &d = c->devs[0];
+    HIP_TRY(hipSetDevice(d.hip_id));
+    int dev = d.hip_id;
+    NCCL_TRY(ncclCommInitAll(&d.comm, 1, &dev));
+  }
+  uint32_t maxlen = 0;
+  size_t total = 0;
+  for (int l = 0; l < layers; ++l) {
+    if (elements[l] < 0) return fail(CBX_ERR_INVALID, "layer %d has %d elements", l, elements[l]);
+    maxlen = std::max(maxlen, (uint32_t)elements[l]);
+    total += (size_t)elements[l];
+  }
+  const size_t head = ((size_t)layers + 63) / 64 * 64;  // count slots, one per layer
+  const size_t floats = head + 2 * total;
+  const int nseg = 2 * layers;
+  std::vector<cbx::BnSegment> segs(nseg);
+  for (size_t k = 0; k < c->devs.size(); ++k) {
+    Device &d = c->devs[k];
+    HIP_TRY(hipSetDevice(d.hip_id));
+    size_t off = head;
+    for (int l = 0; l < layers; ++l) {
+      const size_t j = k * (size_t)layers + l;
+      if (!mean[j] || !variance[j]) return fail(CBX_ERR_INVALID, "null statistics buffer (device %zu, layer %d)", k, l);
+      // :175: the default device (global 0) always counts, the others iff updated.
+      const float scale = (d.g == 0 || updated[j]) ? 1.0f : 0.0f;
+      segs[2 * l] = {mean[j], (uint32_t)elements[l], (uint32_t)off, (uint32_t)l, scale};
+      segs[2 * l + 1] = {variance[j], (uint32_t)elements[l], (uint32_t)(off + elements[l]), (uint32_t)l, scale};
+      off += 2 * (size_t)elements[l];
+    }
+    TRY(grow(reinterpret_cast<void **>(&d.bn_table), &d.bn_table_bytes, segs.size() * sizeof(cbx::BnSegment)));
+    TRY(grow(reinterpret_cast<void **>(&d.bn_scratch), &d.bn_scratch_bytes, floats * sizeof(float)));
+    HIP_TRY(hipDeviceSynchronize());  // :171 (producers on any stream are done)
+    HIP_TRY(hipMemcpy(d.bn_table, segs.data(), segs.size() * sizeof(cbx::BnSegment), hipMemcpyHostToDevice));
+    HIP_TRY(cbx::launch_bn_pack(d.bn_table, nseg, maxlen, d.bn_scratch, d.stream));
+  }
+  NCCL_TRY(ncclGroupStart());
+  for (Device &d : c->devs) {
+    HIP_TRY(hipSetDevice(d.hip_id));
+    NCCL_TRY(ncclAllReduce(d.bn_scratch, d.bn_scratch, floats, ncclFloat, ncclSum, d.comm, d.stream));
+  }
+  NCCL_TRY(ncclGroupEnd());
+  for (Device &d : c->devs) {
+    HIP_TRY(hipSetDevice(d.hip_id));
+    HIP_TRY(cbx::launch_bn_unpack(d.bn_table, nseg, maxlen, d.bn_scratch, d.stream));
+    HIP_TRY(hipStreamSynchronize(d.stream));  // :218
   }
   return CBX_OK;
 }

@@ -107,6 +107,21 @@ hipError_t launch_ssgd_accumulate(const SsgdArgs &a, const LaunchConfig &cfg, hi
 // Barrier (synchronoussgd.c:13-106, common.c:198-220): D *= 1/wpc; momentum;
 // z += D; acc = 0; every locked replica := z.
 hipError_t launch_ssgd_apply(const SsgdArgs &a, const LaunchConfig &cfg, hipStream_t stream, Timing t = {});
+// Batch-norm running-statistics averaging (cudnn/cudnnbatchnormparams.c:157-222):
+// every (layer, mean|variance) buffer of a device is one segment of a packed
+// scratch buffer that a single all-reduce sums across devices.
+struct BnSegment {
+  float *ptr;      // the layer's running mean or variance on this device
+  uint32_t len;    // floats
+  uint32_t off;    // offset of the segment in the scratch (floats)
+  uint32_t layer;  // count slot: scratch[layer] sums the counted devices
+  float scale;     // 1 if this device's statistics count, else 0
+};
+// scratch[seg.off + i] = seg.scale * seg.ptr[i]; scratch[seg.layer] = seg.scale.
+hipError_t launch_bn_pack(const BnSegment *segs, int nseg, uint32_t maxlen, float *scratch, hipStream_t stream);
+// seg.ptr[i] = r * scratch[seg.off + i], r = 1/count (count > 1) else 1.
+hipError_t launch_bn_unpack(const BnSegment *segs, int nseg, uint32_t maxlen, const float *scratch,
+                            hipStream_t stream);
 // Synthetic normal fill.
 hipError_t launch_fill_normal(float *out, int64_t n, uint64_t seed, float sigma,
                               const float *mean, hipStream_t stream);

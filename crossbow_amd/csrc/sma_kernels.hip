@@ -340,6 +340,28 @@ __global__ __launch_bounds__(512) void ssgd_apply_kernel(const SsgdArgs a) {
 }
 
 // ---------------------------------------------------------------------------
+// Batch-norm statistics averaging: pack -> (RCCL sum) -> unpack.  Small,
+// latency-bound buffers (one block row per segment); blockIdx.y = segment.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void bn_pack_kernel(const BnSegment *segs, float *scratch) {
+  const BnSegment sg = segs[blockIdx.y];
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < sg.len) scratch[sg.off + i] = sg.scale * sg.ptr[i];
+  // A device's count for the layer, written once (by its mean segment's first thread).
+  if (i == 0 && (blockIdx.y & 1u) == 0) scratch[sg.layer] = sg.scale;
+}
+
+__global__ __launch_bounds__(256) void bn_unpack_kernel(const BnSegment *segs, const float *scratch) {
+  const BnSegment sg = segs[blockIdx.y];
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= sg.len) return;
+  const float count = scratch[sg.layer];
+  // cudnnbatchnormparams.c:192-197: ratio = 1. / (float) count, only if count > 1.
+  const float ratio = count > 1.0f ? (float)(1.0 / (double)count) : 1.0f;
+  sg.ptr[i] = ratio * scratch[sg.off + i];
+}
+
+// ---------------------------------------------------------------------------
 // Synthetic inputs: splitmix64 -> Box-Muller in double.
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
@@ -522,6 +544,21 @@ hipError_t launch_ssgd_apply(const SsgdArgs &a, const LaunchConfig &cfg, hipStre
     if (mom) hipExtLaunchKernelGGL((ssgd_apply_kernel<true, 0>), g, b, 0, stream, t.start, t.stop, 0, a);
     else hipExtLaunchKernelGGL((ssgd_apply_kernel<false, 0>), g, b, 0, stream, t.start, t.stop, 0, a);
   }
+  return hipGetLastError();
+}
+
+hipError_t launch_bn_pack(const BnSegment *segs, int nseg, uint32_t maxlen, float *scratch, hipStream_t stream) {
+  if (nseg <= 0 || maxlen == 0) return hipSuccess;
+  const dim3 g((maxlen + 255) / 256, (unsigned)nseg);
+  hipLaunchKernelGGL(bn_pack_kernel, g, dim3(256), 0, stream, segs, scratch);
+  return hipGetLastError();
+}
+
+hipError_t launch_bn_unpack(const BnSegment *segs, int nseg, uint32_t maxlen, const float *scratch,
+                            hipStream_t stream) {
+  if (nseg <= 0 || maxlen == 0) return hipSuccess;
+  const dim3 g((maxlen + 255) / 256, (unsigned)nseg);
+  hipLaunchKernelGGL(bn_unpack_kernel, g, dim3(256), 0, stream, segs, scratch);
   return hipGetLastError();
 }
 

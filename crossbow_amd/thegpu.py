@@ -154,6 +154,21 @@ class TheGPU:
     def delModel(self) -> int:
         return check(self._L.cbx_del_model(self._ctx))
 
+    # ---- batch-norm running statistics (cudnnbatchnormparams.c:157-222) ------
+    def average_batchnorm_stats(self, elements: Sequence[int], mean_ptrs: Sequence[int],
+                                var_ptrs: Sequence[int], updated: Sequence[int]) -> None:
+        """Average every BN layer's running mean/variance across devices.
+
+        ``mean_ptrs[k * layers + l]`` / ``var_ptrs[...]``: device pointers of layer l on
+        local device k; ``updated[...]``: that layer ran on that device since the last call.
+        """
+        L = len(elements)
+        el = (ctypes.c_int * max(1, L))(*elements)
+        mp = (ctypes.c_void_p * max(1, len(mean_ptrs)))(*mean_ptrs)
+        vp = (ctypes.c_void_p * max(1, len(var_ptrs)))(*var_ptrs)
+        up = (ctypes.c_int * max(1, len(updated)))(*[1 if u else 0 for u in updated])
+        check(self._L.cbx_average_batchnorm_stats(self._ctx, L, el, mp, vp, up))
+
     # ---- task-side replica access -----------------------------------------
     def replica_lock(self, id: int) -> None:
         check(self._L.cbx_replica_lock(self._ctx, id))

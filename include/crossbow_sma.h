@@ -137,6 +137,21 @@ int cbx_override_model_data (cbx_context *ctx, const char *dir);
 int cbx_add_model (cbx_context *ctx);
 int cbx_del_model (cbx_context *ctx);
 
+/* ---- batch-norm running statistics ----------------------------------- */
+/* crossbowCudnnBatchNormParamsSynchroniseEstimatedMeanAndVariable
+ * (cudnn/cudnnbatchnormparams.c:157-222; its caller is commented out at
+ * executioncontext.c:2268, so this is opt-in), for `layers` BN layers in
+ * one all-reduce.  mean/variance[k * layers + l] are device pointers of
+ * layer l (elements[l] floats) on LOCAL device k; updated[k * layers + l]
+ * is that layer's "updates > 0" on that device.  Per layer, the default
+ * device (global device 0) always counts and every other device counts iff
+ * updated; every device ends with (sum of counted) / count (unscaled when
+ * count == 1).  No-op with one device (:165-166).  Device-synchronises
+ * before and after, as the reference does (:171, :218).  The sum order is
+ * RCCL's, not device order: equal to the reference within fp32 rounding. */
+int cbx_average_batchnorm_stats (cbx_context *ctx, int layers, const int *elements,
+		float *const *mean, float *const *variance, const int *updated);
+
 /* ---- task-side replica access (modelmanager.c:147-204) ---------------- */
 int cbx_replica_lock (cbx_context *ctx, int id);       /* crossbowModelManagerGet   */
 int cbx_replica_unlock (cbx_context *ctx, int id);     /* crossbowModelManagerRelease */

@@ -72,6 +72,8 @@ def lib():
             f.restype = None if name == "cbo_ssgd_sync" else ctypes.c_int
             f.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_size_t, ctypes.c_int, ctypes.c_float,
                           fpp, fpp, fpp, fpp, ip, ctypes.c_int, fp]
+        L.cbo_bn_average.restype = ctypes.c_int
+        L.cbo_bn_average.argtypes = [ctypes.c_int, ctypes.c_int, ip, fpp, fpp, ip]
         L.cbo_blas_open.restype = ctypes.c_int
         L.cbo_blas_open.argtypes = [ctypes.c_char_p]
         L.cbo_blas_name.restype = ctypes.c_char_p
@@ -234,6 +236,21 @@ def ssgd_sync(st: SmaState, acc: List[np.ndarray], wpc: int, blas: bool = False)
             raise RuntimeError("OpenBLAS replay unavailable")
     else:
         lib().cbo_ssgd_sync(*args, _fp(np.empty(st.n, np.float32)))
+
+
+def bn_average(mean: List[List[np.ndarray]], var: List[List[np.ndarray]], updated) -> None:
+    """BN running-stat averaging (cudnn/cudnnbatchnormparams.c:157-222), in place.
+
+    ``mean[g][l]`` / ``var[g][l]``: layer l's buffers on device g;
+    ``updated[g][l]``: that layer had updates on device g since the last call.
+    """
+    G, L = len(mean), len(mean[0])
+    elements = np.array([m.size for m in mean[0]], dtype=np.int32)
+    flat_m = [mean[g][l] for g in range(G) for l in range(L)]
+    flat_v = [var[g][l] for g in range(G) for l in range(L)]
+    upd = np.ascontiguousarray(np.asarray(updated, dtype=np.int32).reshape(G * L))
+    lib().cbo_bn_average(G, L, elements.ctypes.data_as(ctypes.POINTER(ctypes.c_int)), _fpp(flat_m), _fpp(flat_v),
+                         upd.ctypes.data_as(ctypes.POINTER(ctypes.c_int)))
 
 
 def openblas_path() -> Optional[str]:

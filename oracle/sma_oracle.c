@@ -390,6 +390,42 @@ int cbo_ssgd_sync_blas (int G, int size, size_t n, int wpc, float momentum,
 }
 
 /* ---------------------------------------------------------------------- */
+/* Batch-norm statistics averaging, cudnn/cudnnbatchnormparams.c:157-222   */
+/* ---------------------------------------------------------------------- */
+int cbo_bn_average (int G, int layers, const int *elements, float **mean, float **var, const int *updated) {
+	int l, g;
+	size_t k;
+	if (G == 1)                                                             /* :165-166 */
+		return 0;
+	for (l = 0; l < layers; ++l) {
+		float *M = mean[l], *V = var[l];                                    /* default device 0 */
+		size_t n = (size_t) elements[l];
+		int count = 1;
+		for (g = 1; g < G; ++g) {
+			if (! updated[g * layers + l])                                  /* :175 */
+				continue;
+			for (k = 0; k < n; ++k) {
+				M[k] = fmaf (1.0f, mean[g * layers + l][k], M[k]);           /* :185 */
+				V[k] = fmaf (1.0f, var[g * layers + l][k], V[k]);            /* :186 */
+			}
+			count++;
+		}
+		if (count > 1) {                                                    /* :192-197 */
+			float ratio = (float) (1. / (float) count);
+			for (k = 0; k < n; ++k) {
+				M[k] = ratio * M[k];
+				V[k] = ratio * V[k];
+			}
+		}
+		for (g = 1; g < G; ++g) {                                           /* :200-209 */
+			memcpy (mean[g * layers + l], M, n * sizeof(float));
+			memcpy (var[g * layers + l], V, n * sizeof(float));
+		}
+	}
+	return 0;
+}
+
+/* ---------------------------------------------------------------------- */
 /* CPU affinity, clib-multigpu/CPU.c:39-60                                 */
 /* ---------------------------------------------------------------------- */
 int cbo_bind_core (int core) {

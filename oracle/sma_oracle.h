@@ -115,6 +115,17 @@ int cbo_ssgd_sync_blas (int G, int size, size_t n, int wpc, float momentum,
 		float **z, float **last, float **w, float **acc,
 		const int *locked, int first, float *scratch);
 
+/* Batch-norm running-statistics averaging across devices                  */
+/* (crossbowCudnnBatchNormParamsSynchroniseEstimatedMeanAndVariable,        */
+/* cudnn/cudnnbatchnormparams.c:157-222), for `layers` BN layers at once.   */
+/* mean/var[g * layers + l] is layer l's buffer (elements[l] floats) on     */
+/* device g; updated[g * layers + l] is that layer's p->updates[g] > 0.     */
+/* Per layer: device 0 (the default device) accumulates, in device order,   */
+/* M = fma(1, m_g, M) for every other device g with updates (:175-190);     */
+/* count = 1 + their number; if count > 1, M *= 1/count (:193-197); every   */
+/* other device then receives M (:200-209).  Returns 0.                     */
+int cbo_bn_average (int G, int layers, const int *elements, float **mean, float **var, const int *updated);
+
 /* dlopen an OpenBLAS build; returns 0 on success.  `path` may be NULL to  */
 /* probe the usual numpy/scipy wheels.  Records the library actually used. */
 int cbo_blas_open (const char *path);

@@ -7,7 +7,9 @@ replicas in id order (the oracle's kernel-A restatement), all-reduces
 it (what ``libcrossbow_sma`` sends through RCCL), and applies Phase C / D.
 The result on every rank must equal the single-address-space G = 2 oracle
 (clib-multigpu/synch/sma.c:13-231): with two ranks the fp32 sum a + b is
-order independent, so the comparison is bit for bit.  The control plane of
+order independent, so the comparison is bit for bit.  The synchronous-SGD
+barrier and the batch-norm statistics averaging are rehearsed the same way.
+The control plane of
 ``crossbow_amd.dist`` (unique-id broadcast, barrier, max over ranks) runs
 over the same gloo group.
 """
@@ -89,6 +91,60 @@ def _rank_main(rank, world, port, q):
                 if i not in ids:
                     ok &= bool(np.array_equal(mine.w[i], ref.w[i]))
             results.append(ok)
+        # Synchronous SGD (WORKER, synchronoussgd.c:13-106): task steps add into
+        # each rank's base gradient; the barrier all-reduces it and every rank
+        # applies it to its own base model and replicas.
+        n, R, wpc = 3001, 2, 4
+        ref = O.make_state(n, world, R, 0.1, 0.9)
+        grads = [O.fill_normal(n, 4000 + i, 0.01) for i in range(ref.size)]
+        acc_ref = [np.zeros(n, np.float32) for _ in range(world)]
+        mine = ref.clone()
+        for i in range(ref.size):
+            O.ssgd_worker(np.float32(-0.05), 1e-4, ref.w[i], grads[i].copy(), acc_ref[i % world])
+        O.ssgd_sync(ref, acc_ref, wpc)
+        ids = D.local_replicas(mine.size, world, rank)
+        acc = np.zeros(n, np.float32)
+        for i in ids:
+            O.ssgd_worker(np.float32(-0.05), 1e-4, mine.w[i], grads[i].copy(), acc)
+        buf = torch.from_numpy(acc.copy())
+        dist.all_reduce(buf, op=dist.ReduceOp.SUM)
+        local = O.SmaState(1, len(ids), n, 0.1, 0.9, [mine.z[rank]], [mine.last[rank]],
+                           [mine.s[i] for i in ids], [mine.w[i] for i in ids])
+        O.ssgd_sync(local, [buf.numpy().copy()], wpc)
+        ok = bool(np.array_equal(local.z[0].view(np.uint32), ref.z[rank].view(np.uint32)))
+        ok &= bool(np.array_equal(local.last[0].view(np.uint32), ref.last[rank].view(np.uint32)))
+        for k, i in enumerate(ids):
+            ok &= bool(np.array_equal(local.w[k].view(np.uint32), ref.w[i].view(np.uint32)))
+        results.append(ok)
+
+        # Batch-norm statistics (cudnnbatchnormparams.c:157-222) the way the
+        # library packs them: [count slots | scale*mean | scale*var] per layer,
+        # one all-reduce, then * 1/count.  Rank 1 has updates on layer 0 only.
+        elements = [16, 40]
+        mean = [[O.fill_normal(e, 50 + 10 * g + l, 0.5) for l, e in enumerate(elements)] for g in range(world)]
+        var = [[O.fill_normal(e, 90 + 10 * g + l, 0.5) for l, e in enumerate(elements)] for g in range(world)]
+        updated = [[1, 1], [1, 0]]
+        ref_m = [[a.copy() for a in r] for r in mean]
+        ref_v = [[a.copy() for a in r] for r in var]
+        O.bn_average(ref_m, ref_v, updated)
+        L = len(elements)
+        scale = [1.0 if (rank == 0 or updated[rank][l]) else 0.0 for l in range(L)]
+        parts = [np.array(scale, np.float32)]
+        for l in range(L):
+            parts += [np.float32(scale[l]) * mean[rank][l], np.float32(scale[l]) * var[rank][l]]
+        buf = torch.from_numpy(np.concatenate(parts))
+        dist.all_reduce(buf, op=dist.ReduceOp.SUM)
+        b = buf.numpy()
+        off = L
+        ok = True
+        for l, e in enumerate(elements):
+            count = float(b[l])
+            r = np.float32(1.0 / count) if count > 1 else np.float32(1.0)
+            m, v = r * b[off:off + e], r * b[off + e:off + 2 * e]
+            off += 2 * e
+            ok &= bool(np.array_equal(m.view(np.uint32), ref_m[rank][l].view(np.uint32)))
+            ok &= bool(np.array_equal(v.view(np.uint32), ref_v[rank][l].view(np.uint32)))
+        results.append(ok)
         D.barrier(world)
         D.finalize(world)
         q.put((rank, results, None))

@@ -345,3 +345,27 @@ def test_golden_fixtures_on_gpu():
             assert_bitexact(got.z[0], case["z_out"][0], f"{case['name']} z")
         finally:
             g.free()
+
+
+def test_batchnorm_stats_single_device():
+    # One device: the reference returns at once (cudnnbatchnormparams.c:165-166).
+    # With the split pipeline forced, the pack / one-rank all-reduce / unpack
+    # path runs with count 1 on every layer and must be the identity.
+    import torch
+    n, R = 4096, 1
+    g = make_gpu(n, R, 0.1, 0.0)
+    try:
+        elements = [64, 256, 2048, 3]
+        mean = [torch.from_numpy(O.fill_normal(e, 950 + l, 0.5)).cuda() for l, e in enumerate(elements)]
+        var = [torch.from_numpy(O.fill_normal(e, 960 + l, 0.5)).cuda() for l, e in enumerate(elements)]
+        before = [t.cpu().numpy().copy() for t in mean + var]
+        args = (elements, [t.data_ptr() for t in mean], [t.data_ptr() for t in var], [0] * len(elements))
+        torch.cuda.synchronize()
+        g.average_batchnorm_stats(*args)
+        g.set_force_split(True)
+        g.average_batchnorm_stats(*args)
+        torch.cuda.synchronize()
+        for t, b in zip(mean + var, before):
+            assert_bitexact(t.cpu().numpy(), b, "batch-norm statistics with one device")
+    finally:
+        g.free()

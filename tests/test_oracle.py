@@ -203,3 +203,32 @@ def test_ssgd_restatement_equals_openblas_sequence(G, momentum):
     assert _eq(a.w[0], st.w[0]), "unlocked replica keeps its data"
     for i in range(1, a.size):
         assert _eq(a.w[i], a.z[i % G])
+
+
+def test_bn_average_matches_formula():
+    # cudnnbatchnormparams.c:157-222 over 3 layers and 4 devices.
+    G, elements = 4, [64, 256, 3]
+    mean = [[O.fill_normal(e, 700 + 10 * g + l, 0.5) for l, e in enumerate(elements)] for g in range(G)]
+    var = [[np.abs(O.fill_normal(e, 800 + 10 * g + l, 1.0)) for l, e in enumerate(elements)] for g in range(G)]
+    updated = [[1, 1, 1], [1, 0, 1], [0, 0, 1], [1, 0, 0]]
+    want_m, want_v = [], []
+    for l in range(len(elements)):
+        cnt = [0] + [g for g in range(1, G) if updated[g][l]]
+        m = sum(mean[g][l].astype(np.float64) for g in cnt) / len(cnt)
+        v = sum(var[g][l].astype(np.float64) for g in cnt) / len(cnt)
+        want_m.append(m)
+        want_v.append(v)
+    O.bn_average(mean, var, updated)
+    for g in range(G):
+        for l in range(len(elements)):
+            np.testing.assert_allclose(mean[g][l], want_m[l], rtol=2e-6, atol=1e-7)
+            np.testing.assert_allclose(var[g][l], want_v[l], rtol=2e-6, atol=1e-7)
+            assert _eq(mean[g][l], mean[0][l]) and _eq(var[g][l], var[0][l])
+
+
+def test_bn_average_single_device_is_noop():
+    m = [[O.fill_normal(32, 900, 0.5)]]
+    v = [[O.fill_normal(32, 901, 0.5)]]
+    m0, v0 = m[0][0].copy(), v[0][0].copy()
+    O.bn_average(m, v, [[0]])
+    assert _eq(m[0][0], m0) and _eq(v[0][0], v0)
