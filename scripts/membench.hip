@@ -221,6 +221,55 @@ __global__ void fillk(uint32_t *p, size_t nwords, uint32_t seed) {
   }
 }
 
+
+// ---- v6: persistent, software-pipelined: the next element's 18 loads are
+// issued before the current element's 10 stores.
+__device__ __forceinline__ void load18(const Args &a, uint32_t i, v4f &z, v4f &l, v4f *sv, v4f *wv) {
+  z = ldo<1>(a.z, i);
+  l = ldo<1>(a.last, i);
+#pragma unroll
+  for (int r = 0; r < R; ++r) sv[r] = ldo<1>(a.s[r], i);
+#pragma unroll
+  for (int r = 0; r < R; ++r) wv[r] = ldo<1>(a.w[r], i);
+}
+__device__ __forceinline__ void comp_store(const Args &a, uint32_t i, v4f z, v4f l, v4f *sv, v4f *wv) {
+  const v4f al = a.alpha, nal = -a.alpha, mb = 0.9f, one = 1.0f, mone = -1.0f;
+  v4f acc = 0.0f;
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    v4f d = vfma(mone, z, sv[r]);
+    wv[r] = vfma(nal, d, wv[r]);
+    acc = vfma(al, d, acc);
+  }
+#pragma unroll
+  for (int r = 0; r < R; ++r) sto<1>(a.w[r], i, wv[r]);
+  v4f D = vfma(mb, l, acc);
+  sto<1>(a.last, i, D);
+  sto<1>(a.z, i, vfma(one, D, z));
+}
+__global__ __launch_bounds__(256) void fused_pipe(const Args a) {
+  const uint32_t stride = gridDim.x * blockDim.x;
+  uint32_t e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= a.n4) return;
+  v4f z0, l0, s0[R], w0[R];
+  load18(a, e * 16u, z0, l0, s0, w0);
+  while (true) {
+    const uint32_t en = e + stride;
+    if (en < a.n4) {
+      v4f z1, l1, s1[R], w1[R];
+      load18(a, en * 16u, z1, l1, s1, w1);
+      __builtin_amdgcn_sched_barrier(0);
+      comp_store(a, e * 16u, z0, l0, s0, w0);
+      z0 = z1; l0 = l1;
+#pragma unroll
+      for (int r = 0; r < R; ++r) { s0[r] = s1[r]; w0[r] = w1[r]; }
+      e = en;
+    } else {
+      comp_store(a, e * 16u, z0, l0, s0, w0);
+      break;
+    }
+  }
+}
 static hipEvent_t e0, e1;
 
 template <typename F>
@@ -344,6 +393,32 @@ int main(int argc, char **argv) {
         float t1 = time_ms([&] { hipLaunchKernelGGL((fused3<1, false, true>), dim3(grid), dim3(blk), 0, 0, a); }, iters);
         std::printf("{\"v5\":%d,\"block\":%d,\"base_GBs\":%.1f,\"schedbar_GBs\":%.1f}\n", round, blk, alg / t0 / 1e6, alg / t1 / 1e6);
       }
+    return 0;
+  }
+
+  if (argc > 2 && std::strcmp(argv[2], "v6") == 0) {
+    const size_t stride = (buf + (2u << 20) - 1) / (2u << 20) * (2u << 20) + 4096;
+    Args a;
+    a.z = (v4f *)arena;
+    a.last = (v4f *)(arena + stride);
+    for (int r = 0; r < R; ++r) {
+      a.s[r] = (const v4f *)(arena + (2 + 2 * r) * stride);
+      a.w[r] = (v4f *)(arena + (3 + 2 * r) * stride);
+    }
+    a.n4 = n4;
+    a.alpha = 0.1f;
+    hipLaunchKernelGGL(fillk, dim3(8192), dim3(256), 0, 0, (uint32_t *)arena, nbuf * stride / 4, 12345u);
+    CK(hipDeviceSynchronize());
+    for (int round = 0; round < 2; ++round) {
+      float t = time_ms([&] { hipLaunchKernelGGL((fused3<1, false, true>), dim3(n4 / 128), dim3(128), 0, 0, a); }, iters);
+      std::printf("{\"v6\":%d,\"kind\":\"onetrip-128\",\"GBs\":%.1f}\n", round, alg / t / 1e6);
+      for (int blk : {128, 256})
+        for (int wpc : {1, 2, 3, 4, 6}) {
+          const unsigned grid = cus * wpc * (256 / blk);
+          float tp = time_ms([&] { hipLaunchKernelGGL(fused_pipe, dim3(grid), dim3(blk), 0, 0, a); }, iters);
+          std::printf("{\"v6\":%d,\"kind\":\"pipe\",\"block\":%d,\"wg256_per_cu\":%d,\"GBs\":%.1f}\n", round, blk, wpc, alg / tp / 1e6);
+        }
+    }
     return 0;
   }
   // Ceilings on the same arena (1 GiB copy).
