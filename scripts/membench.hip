@@ -270,6 +270,43 @@ __global__ __launch_bounds__(256) void fused_pipe(const Args a) {
     }
   }
 }
+
+// ---- v7: buffer_load/store through ONE descriptor over the arena, stream
+// base in soffset, with explicit cache-policy bits (aux: sc0=1 nt=2 sc1=16).
+typedef unsigned v4u __attribute__((ext_vector_type(4)));
+struct BArgs {
+  uint32_t off_s[R], off_w[R], off_z, off_last;
+  uint32_t n4;
+  float alpha;
+};
+template <int LA, int SA>
+__global__ __launch_bounds__(128) void fused_buf(const BArgs a, char *arena, uint32_t bytes) {
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(arena, 0, bytes, 0x00020000);
+  const uint32_t e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= a.n4) return;
+  const uint32_t i = e * 16u;
+  auto L = [&](uint32_t so) { v4u x = __builtin_amdgcn_raw_buffer_load_b128(rs, i, so, LA); return __builtin_bit_cast(v4f, x); };
+  auto S = [&](uint32_t so, v4f v) { __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, v), rs, i, so, SA); };
+  const v4f al = a.alpha, nal = -a.alpha, mb = 0.9f, one = 1.0f, mone = -1.0f;
+  v4f zv = L(a.off_z), lv = L(a.off_last), acc = 0.0f;
+  v4f sv[R], wv[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) sv[r] = L(a.off_s[r]);
+#pragma unroll
+  for (int r = 0; r < R; ++r) wv[r] = L(a.off_w[r]);
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    v4f d = vfma(mone, zv, sv[r]);
+    wv[r] = vfma(nal, d, wv[r]);
+    acc = vfma(al, d, acc);
+  }
+#pragma unroll
+  for (int r = 0; r < R; ++r) S(a.off_w[r], wv[r]);
+  v4f D = vfma(mb, lv, acc);
+  S(a.off_last, D);
+  S(a.off_z, vfma(one, D, zv));
+}
 static hipEvent_t e0, e1;
 
 template <typename F>
@@ -418,6 +455,37 @@ int main(int argc, char **argv) {
           float tp = time_ms([&] { hipLaunchKernelGGL(fused_pipe, dim3(grid), dim3(blk), 0, 0, a); }, iters);
           std::printf("{\"v6\":%d,\"kind\":\"pipe\",\"block\":%d,\"wg256_per_cu\":%d,\"GBs\":%.1f}\n", round, blk, wpc, alg / tp / 1e6);
         }
+    }
+    return 0;
+  }
+
+  if (argc > 2 && std::strcmp(argv[2], "v7") == 0) {
+    const size_t stride = (buf + (2u << 20) - 1) / (2u << 20) * (2u << 20) + 4096;
+    Args a;
+    BArgs b;
+    a.z = (v4f *)arena;
+    a.last = (v4f *)(arena + stride);
+    b.off_z = 0;
+    b.off_last = (uint32_t)stride;
+    for (int r = 0; r < R; ++r) {
+      a.s[r] = (const v4f *)(arena + (2 + 2 * r) * stride);
+      a.w[r] = (v4f *)(arena + (3 + 2 * r) * stride);
+      b.off_s[r] = (uint32_t)((2 + 2 * r) * stride);
+      b.off_w[r] = (uint32_t)((3 + 2 * r) * stride);
+    }
+    a.n4 = b.n4 = n4;
+    a.alpha = b.alpha = 0.1f;
+    const uint32_t bytes = (uint32_t)std::min<size_t>(nbuf * stride, 0xFFFFFFF0u);
+    hipLaunchKernelGGL(fillk, dim3(8192), dim3(256), 0, 0, (uint32_t *)arena, nbuf * stride / 4, 12345u);
+    CK(hipDeviceSynchronize());
+    const unsigned grid = n4 / 128;
+    for (int round = 0; round < 2; ++round) {
+      float t = time_ms([&] { hipLaunchKernelGGL((fused3<1, false, true>), dim3(grid), dim3(128), 0, 0, a); }, iters);
+      std::printf("{\"v7\":%d,\"kind\":\"global-nt\",\"GBs\":%.1f}\n", round, alg / t / 1e6);
+#define RUNB(LA, SA) { float tb = time_ms([&] { hipLaunchKernelGGL((fused_buf<LA, SA>), dim3(grid), dim3(128), 0, 0, b, arena, bytes); }, iters); \
+      std::printf("{\"v7\":%d,\"kind\":\"buffer\",\"ld_aux\":%d,\"st_aux\":%d,\"GBs\":%.1f}\n", round, LA, SA, alg / tb / 1e6); }
+      RUNB(2, 2) RUNB(2, 16) RUNB(2, 18) RUNB(2, 17) RUNB(2, 19) RUNB(2, 0) RUNB(0, 2) RUNB(16, 2) RUNB(18, 18) RUNB(3, 3) RUNB(17, 17) RUNB(0, 0)
+#undef RUNB
     }
     return 0;
   }
