@@ -186,6 +186,11 @@ struct Device {
   char *host = nullptr;  // pinned mirror, same layout (lazy)
   size_t arena_bytes = 0;
   size_t stride = 0;  // bytes per buffer slot
+  int base_slots = 0;  // replica slots inside the arena (replicas per device at creation)
+  // Replica slots added by autotune (modelmanager.c:362-470) beyond the arena:
+  // one block of kReplicaSlots buffers each, so existing pointers stay valid.
+  std::vector<char *> extra;
+  std::vector<char *> extra_host;
   std::vector<int> replicas;  // global ids, increasing
   hipEvent_t synched = nullptr;     // end-of-step marker when timing is off
   hipEvent_t step_event = nullptr;  // end of the last step (cbx_step_event)
@@ -279,7 +284,11 @@ float *base_ctrl(const Device &d, int kind) {
   return reinterpret_cast<float *>(d.arena + slot_index_base(kind) * d.stride);
 }
 
+size_t replica_kind_index(int kind) { return slot_index_replica(0, kind) - kBaseSlots; }
+
 float *replica_dev(const Device &d, const Replica &r, int kind) {
+  if (r.slot >= d.base_slots)
+    return reinterpret_cast<float *>(d.extra[r.slot - d.base_slots] + replica_kind_index(kind) * d.stride);
   return slot_ptr(d.arena, d, slot_index_replica(r.slot, kind), false);
 }
 
@@ -289,6 +298,8 @@ float *base_host(const Device &d, int kind) {
 }
 
 float *replica_host(const Device &d, const Replica &r, int kind) {
+  if (r.slot >= d.base_slots)
+    return reinterpret_cast<float *>(d.extra_host[r.slot - d.base_slots] + replica_kind_index(kind) * d.stride);
   return slot_ptr(d.host, d, slot_index_replica(r.slot, kind), false);
 }
 
@@ -367,6 +378,10 @@ void close_device(Device &d) {
   if (d.comm_stream) (void)hipStreamSynchronize(d.comm_stream);
   if (d.comm) (void)ncclCommDestroy(d.comm);
   if (d.arena) (void)hipFree(d.arena);
+  for (char *p : d.extra)
+    if (p) (void)hipFree(p);
+  for (char *p : d.extra_host)
+    if (p) (void)hipHostFree(p);
   if (d.bn_table) (void)hipFree(d.bn_table);
   if (d.bn_scratch) (void)hipFree(d.bn_scratch);
   if (d.host) (void)hipHostFree(d.host);
@@ -766,10 +781,18 @@ int load_buffer(float *dev, size_t bytes, const std::string &path, std::vector<c
 
 int alloc_host_mirror(cbx_context *c) {
   for (Device &d : c->devs) {
-    if (d.host) continue;
     HIP_TRY(hipSetDevice(d.hip_id));
-    HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&d.host), d.arena_bytes, hipHostMallocDefault));
-    std::memset(d.host, 0, d.arena_bytes);
+    if (!d.host) {
+      HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&d.host), d.arena_bytes, hipHostMallocDefault));
+      std::memset(d.host, 0, d.arena_bytes);
+    }
+    d.extra_host.resize(d.extra.size(), nullptr);
+    for (size_t k = 0; k < d.extra.size(); ++k) {
+      if (!d.extra[k] || d.extra_host[k]) continue;
+      const size_t bytes = d.stride * kReplicaSlots;
+      HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&d.extra_host[k]), bytes, hipHostMallocDefault));
+      std::memset(d.extra_host[k], 0, bytes);
+    }
   }
   return CBX_OK;
 }
@@ -1065,6 +1088,7 @@ int cbx_set_model_manager(cbx_context *c, int replicas, int type) {
   for (Device &d : c->devs) {
     HIP_TRY(hipSetDevice(d.hip_id));
     d.stride = stride;
+    d.base_slots = replicas;
     d.arena_bytes = stride * (size_t)(kBaseSlots + kReplicaSlots * replicas);
     hipError_t e = hipMalloc(reinterpret_cast<void **>(&d.arena), d.arena_bytes);
     if (e != hipSuccess)
@@ -1229,14 +1253,98 @@ int cbx_override_model_data(cbx_context *c, const char *dir) {
   return CBX_OK;
 }
 
+// crossbowModelManagerAddModel, modelmanager.c:362-470: one new replica per
+// device, ids size .. size+G-1 (id size+g on device g, keeping the round-robin
+// placement), each a copy of the first replica on its device (data, gradient,
+// last, diff and solver state: model.c:202-306), locked so that the barrier's
+// unlockAny releases it.
 int cbx_add_model(cbx_context *c) {
   TRY(check_manager(c));
-  return fail(CBX_ERR_UNSUPPORTED, "autotune addModel is not implemented (DESIGN.md, out of scope for round 1)");
+  if (c->R + 1 > cbx::kMaxReplicas) return fail(CBX_ERR_UNSUPPORTED, "at most %d replicas per device", cbx::kMaxReplicas);
+  const int size_ = c->size + c->G;
+  const int slot = c->R;  // id / G of every new replica
+  for (Device &d : c->devs) {
+    HIP_TRY(hipSetDevice(d.hip_id));
+    HIP_TRY(hipStreamSynchronize(d.stream));  // :417 cudaDeviceSynchronize
+    if (slot >= d.base_slots) {
+      const size_t k = (size_t)(slot - d.base_slots);
+      if (d.extra.size() <= k) d.extra.resize(k + 1, nullptr);
+      if (!d.extra[k]) {
+        hipError_t e = hipMalloc(reinterpret_cast<void **>(&d.extra[k]), d.stride * kReplicaSlots);
+        if (e != hipSuccess) {
+          d.extra[k] = nullptr;
+          return fail(CBX_ERR_HIP, "hipMalloc for a new replica: %s", hipGetErrorString(e));
+        }
+      }
+      if (d.host) TRY(alloc_host_mirror(c));
+    }
+  }
+  c->replicas.resize(size_, nullptr);
+  c->locked.resize(size_, 0);
+  for (int g = 0; g < c->G; ++g) {
+    const int id = c->size + g;
+    Replica *r = new Replica();
+    r->id = id;
+    r->g = g;
+    r->local = local_of(c, g);
+    r->slot = slot;
+    // :420-425: the first replica on the device is the template.
+    const Replica &src = *c->replicas[g];
+    r->conf = src.conf;  // crossbowSolverConfReplicate
+    r->clock = src.clock;
+    r->updates = src.updates;
+    pthread_mutex_init(&r->lock, nullptr);
+    c->replicas[id] = r;
+    if (r->local >= 0) {
+      Device &d = c->devs[r->local];
+      HIP_TRY(hipSetDevice(d.hip_id));
+      for (int kind : {CBX_BUF_DATA, CBX_BUF_GRADIENT, CBX_BUF_DIFF, CBX_BUF_LAST})
+        HIP_TRY(hipMemcpyAsync(replica_dev(d, *r, kind), replica_dev(d, src, kind), d.stride, hipMemcpyDeviceToDevice,
+                               d.stream));
+      HIP_TRY(hipStreamSynchronize(d.stream));
+      pthread_mutex_lock(&r->lock);  // :433-435
+      c->locked[id] = 1;
+    }
+  }
+  for (Device &d : c->devs) d.replicas.push_back(c->size + d.g);
+  c->size = size_;
+  c->R += 1;
+  return CBX_OK;
 }
 
+// crossbowModelManagerDelModel, modelmanager.c:473-557: drop the last replica
+// of every device (ids size-G .. size-1).
 int cbx_del_model(cbx_context *c) {
   TRY(check_manager(c));
-  return fail(CBX_ERR_UNSUPPORTED, "autotune delModel is not implemented (DESIGN.md, out of scope for round 1)");
+  if (c->R <= 1) return fail(CBX_ERR_STATE, "cannot delete the last replica of a device");  // :511
+  const int size_ = c->size - c->G;
+  for (int id = size_; id < c->size; ++id) {
+    Replica *r = c->replicas[id];
+    if (r->local >= 0) {
+      Device &d = c->devs[r->local];
+      HIP_TRY(hipSetDevice(d.hip_id));
+      HIP_TRY(hipStreamSynchronize(d.stream));  // :530
+      if (r->slot >= d.base_slots) {
+        const size_t k = (size_t)(r->slot - d.base_slots);
+        HIP_TRY(hipFree(d.extra[k]));
+        d.extra[k] = nullptr;
+        if (k < d.extra_host.size() && d.extra_host[k]) {
+          HIP_TRY(hipHostFree(d.extra_host[k]));
+          d.extra_host[k] = nullptr;
+        }
+      }
+      if (r->client) (void)hipEventDestroy(r->client);
+      d.replicas.erase(std::remove(d.replicas.begin(), d.replicas.end(), id), d.replicas.end());
+    }
+    if (c->locked[id]) pthread_mutex_unlock(&r->lock);
+    pthread_mutex_destroy(&r->lock);
+    delete r;
+  }
+  c->replicas.resize(size_);
+  c->locked.resize(size_);
+  c->size = size_;
+  c->R -= 1;
+  return CBX_OK;
 }
 
 // ---- replica optimiser step (kernels/optimisers/sma.cu:3-100) -------------

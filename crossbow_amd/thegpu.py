@@ -224,6 +224,23 @@ class TheGPU:
         return [i for i in range(self.num_replicas()) if self.replica_is_local(i)]
 
     # ---- buffers -----------------------------------------------------------
+    def replica_buffer(self, id: int, kind: int) -> int:
+        """Device pointer of a replica buffer (what the task-side kernels use)."""
+        p = ctypes.c_void_p()
+        check(self._L.cbx_replica_buffer(self._ctx, id, kind, ctypes.byref(p)))
+        return p.value
+
+    def base_buffer(self, device: int, kind: int) -> int:
+        p = ctypes.c_void_p()
+        check(self._L.cbx_base_buffer(self._ctx, device, kind, ctypes.byref(p)))
+        return p.value
+
+    def step_event(self, local: int = 0) -> int:
+        """The hipEvent_t (as an int) that marks the end of the last synchronise()."""
+        p = ctypes.c_void_p()
+        check(self._L.cbx_step_event(self._ctx, local, ctypes.byref(p)))
+        return p.value
+
     def replica_write(self, id: int, kind: int, values: np.ndarray) -> None:
         a = np.ascontiguousarray(values, dtype=np.float32)
         check(self._L.cbx_replica_write(self._ctx, id, kind, _ptr(a), a.nbytes))

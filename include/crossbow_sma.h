@@ -133,7 +133,14 @@ int cbx_unlock_any (cbx_context *ctx);
 int cbx_checkpoint_model (cbx_context *ctx, const char *dir);
 /* TheGPU.overrideModelData(String) GPU.c:1165-1176 -> executioncontext.c:2369-2388 */
 int cbx_override_model_data (cbx_context *ctx, const char *dir);
-/* TheGPU.addModel() / delModel()   GPU.c:1178-1199 (autotune)            */
+/* TheGPU.addModel() / delModel()   GPU.c:1178-1199 (autotune; also called
+ * by cbx_synchronise for autotune > 0 / < 0, executioncontext.c:2321-2328).
+ * add: one new replica per device, ids size .. size+G-1 (id size+g on device
+ * g), each a copy of device g's first replica (all four buffers and its
+ * solver state, modelmanager.c:362-470, model.c:202-306), left locked for the
+ * barrier's unlockAny.  New buffers get their own allocation: pointers
+ * returned earlier stay valid.  del: drops ids size-G .. size-1
+ * (modelmanager.c:473-557); CBX_ERR_STATE if that would leave none.      */
 int cbx_add_model (cbx_context *ctx);
 int cbx_del_model (cbx_context *ctx);
 

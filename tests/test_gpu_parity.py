@@ -369,3 +369,42 @@ def test_batchnorm_stats_single_device():
             assert_bitexact(t.cpu().numpy(), b, "batch-norm statistics with one device")
     finally:
         g.free()
+
+
+def test_autotune_add_and_del_model():
+    # modelmanager.c:362-557 via synchronise(autotune = +1 / -1): the new
+    # replica (id R on the single device) copies replica 0's buffers, is
+    # locked through the barrier, and takes part in the next SMA step.
+    from crossbow_amd import BUF_DATA, BUF_DIFF
+    n, R = 20_011, 2
+    st = O.make_state(n, 1, R, 0.1, 0.9)
+    g = make_gpu(n, R, 0.1, 0.9)
+    try:
+        upload(g, st)
+        ptr0 = g.replica_buffer(0, BUF_DATA)
+        g.lockAny()
+        g.synchronise(0, 1, 1, False)  # autotune > 0: step, then add one replica per GPU
+        assert g.unlockAny() == R + 1
+        assert g.num_replicas() == R + 1
+        O.sma_step(st)
+        # the new replica is a copy of replica 0 after the step
+        st2 = O.SmaState(1, R + 1, n, 0.1, 0.9, st.z, st.last, st.s + [st.s[0].copy()], st.w + [st.w[0].copy()])
+        g.wait()
+        assert_bitexact(g.replica_read(R, BUF_DATA), st2.w[R], "new replica data")
+        assert_bitexact(g.replica_read(R, BUF_DIFF), st2.s[R], "new replica snapshot")
+        assert g.replica_buffer(0, BUF_DATA) == ptr0, "existing buffers must not move"
+        g.lockAny()
+        g.synchronise(0, 2, 0, False)
+        g.unlockAny()
+        O.sma_step(st2)
+        compare_states(download(g, st2), st2)
+        g.lockAny()
+        g.synchronise(0, 3, -1, False)  # autotune < 0: step, then drop the last replica
+        g.unlockAny()
+        O.sma_step(st2)
+        assert g.num_replicas() == R
+        g.wait()
+        for i in range(R):
+            assert_bitexact(g.replica_read(i, BUF_DATA), st2.w[i], f"w[{i}] after del")
+    finally:
+        g.free()
