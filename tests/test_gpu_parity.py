@@ -408,3 +408,31 @@ def test_autotune_add_and_del_model():
             assert_bitexact(g.replica_read(i, BUF_DATA), st2.w[i], f"w[{i}] after del")
     finally:
         g.free()
+
+
+def test_randomised_configurations_bitexact():
+    # 40 random configurations of everything the barrier path takes as input:
+    # n (ragged), replicas (1-12, i.e. unrolled and chunked kernels), alpha,
+    # momentum, SSP partial locks, `first`, Phase-D copy flags, launch shape,
+    # fused vs split pipeline, bucket size, several steps.  Bit-exact.
+    import random
+    rng = random.Random(20190701)
+    for case in range(40):
+        n = rng.choice([1, 3, 1023, 4096, 65_537, 131_071, 300_007])
+        R = rng.randint(1, 12)
+        alpha = rng.choice([0.1, 0.5, 0.25, 1.0])
+        momentum = rng.choice([0.0, 0.9])
+        held = tuple(sorted(rng.sample(range(R), rng.randint(0, R - 1)))) if R > 1 else ()
+        first = rng.randint(0, R - 1) if rng.random() < 0.2 else 0
+        copy_ids = tuple(i for i in range(first, R) if i not in held and rng.random() < 0.15)
+        split = rng.random() < 0.4
+        bucket = rng.choice([0, 4096, 65_536]) if split else 0
+        config = rng.choice([None, dict(block=64, blocks_per_cu=0, policy=1, unroll=2),
+                             dict(block=256, blocks_per_cu=4, policy=0, unroll=1)])
+        try:
+            _run(n, R, alpha, momentum, copy_ids=copy_ids, first=first, held=held,
+                 sync=1 if held else 0, config=config, split=split, bucket=bucket, steps=rng.randint(1, 3))
+        except AssertionError as e:
+            raise AssertionError(f"case {case}: n={n} R={R} alpha={alpha} mu={momentum} held={held} "
+                                 f"copy={copy_ids} first={first} split={split} bucket={bucket} "
+                                 f"config={config}: {e}") from e
