@@ -102,6 +102,33 @@ def cpu_baseline_threads(args, n_full, threads):
                       f"OpenBLAS on {threads} threads"}
 
 
+def cpu_c1(seconds=3.0):
+    """BASELINE configs[0] (C1): LeNet (n = 1,111,946), 2 replicas, alpha 0.1,
+    mu 0 -- the reference's own CPU-runnable case -- replayed on OpenBLAS,
+    1 thread pinned to core 0, at full size."""
+    from oracle import oracle as O
+    n, R = 1_111_946, 2
+    O.blas_open()
+    O.blas_set_threads(1)
+    st = O.make_state(n, 1, R, 0.1, 0.0)
+    O.bind_core(0)
+    try:
+        O.sma_step_blas(st)
+        steps, t0 = 0, O.now()
+        while True:
+            O.sma_step_blas(st)
+            steps += 1
+            el = O.now() - t0
+            if el >= seconds:
+                break
+    finally:
+        O.unbind()
+    b = (12 * R + 8) * n
+    return {"value": round(b * steps / el / 1e9, 3), "unit": "GB/s", "cores": 1, "kind": "port",
+            "ms_per_step": round(el * 1e3 / steps, 3),
+            "sample": f"C1 LeNet n={n}, 2 replicas, mu 0, full size, {steps} steps in {el:.1f} s"}
+
+
 def cpu_baseline(args, n_full):
     """The reference's call sequence (memset, memcpy + 3 saxpy per replica,
     momentum, apply) on OpenBLAS, 1 thread bound to core 0 like TheCPU.bind(0)
@@ -327,6 +354,7 @@ def main():
             mt = cpu_baseline_threads(args, n, threads)
             result["cpu_baseline"] = cpu_baseline(args, n)
             result["cpu_baseline_multithread"] = mt
+            result["cpu_c1_lenet"] = cpu_c1()
         else:
             result["cpu_baseline"] = None
 
