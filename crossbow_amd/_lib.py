@@ -70,6 +70,7 @@ SIGNATURES = {
     "cbx_set_model": (_I, [_P, _I, _I]),
     "cbx_set_model_variable": (_I, [_P, _I, _I, _I, _IP, _I]),
     "cbx_set_model_variable_buffer": (_I, [_P, _I, _I, _P]),
+    "cbx_set_model_variable_learning_rate_multiplier": (_I, [_P, _I, _I, _F]),
     "cbx_set_model_work_per_clock": (_I, [_P, _I]),
     "cbx_set_update_model_type": (_I, [_P, _I]),
     "cbx_set_learning_rate_decay_policy_fixed": (_I, [_P, _F]),
@@ -77,6 +78,7 @@ SIGNATURES = {
     "cbx_set_learning_rate_decay_policy_step": (_I, [_P, _F, _D, _I]),
     "cbx_set_learning_rate_decay_policy_multistep": (_I, [_P, _F, _D, _I, _I, _IP]),
     "cbx_set_learning_rate_decay_policy_exp": (_I, [_P, _F, _D]),
+    "cbx_set_learning_rate_decay_policy_circular": (_I, [_P, _FP, _I, _FP, _I]),
     "cbx_set_base_model_momentum": (_I, [_P, _F]),
     "cbx_set_momentum": (_I, [_P, _F, _I]),
     "cbx_set_weight_decay": (_I, [_P, _F]),

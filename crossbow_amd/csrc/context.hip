@@ -92,6 +92,10 @@ struct SolverConf {
   float weightDecay = 0.0f;
   float baseModelMomentum = 0.0f;
   unsigned copy = 0;  // `_copy`, solverconfiguration.h:41-52
+  int irregular = 0;  // variables with a learning-rate multiplier != 1 (executioncontext.c:1602)
+  float circularLearningRate[3] = {0, 0, 0};  // CLR (executioncontext.c:1701-1718)
+  float circularMomentum[3] = {0, 0, 0};
+  int superConvergence = 0;
 
   // crossbowSolverConfGetLearningRate, solverconfiguration.c:116-162.
   int learning_rate(int task, float *out) {
@@ -123,6 +127,7 @@ struct SolverConf {
         }
         break;
       case LR_EXP: rate = learningRate * (float)std::pow(gamma, (double)(task + 1)); break;
+      case LR_CLR: return fail(CBX_ERR_UNSUPPORTED, "circular learning rate is unsupported");  // :155-157
       default: return fail(CBX_ERR_UNSUPPORTED, "learning-rate policy %d unsupported", (int)policy);
     }
     *out = rate;
@@ -137,6 +142,7 @@ struct Variable {
   int64_t offset_bytes;
   int64_t bytes;
   int64_t elements;
+  float lr_multiplier = 1.0f;  // variable.c; read only by per-variable optimisers, not by SMA's
 };
 
 struct ModelDef {
@@ -949,6 +955,15 @@ int cbx_set_model_variable_buffer(cbx_context *c, int id, int order, const void 
   return CBX_OK;
 }
 
+int cbx_set_model_variable_learning_rate_multiplier(cbx_context *c, int id, int order, float multiplier) {
+  TRY(check_ctx(c));
+  auto it = c->model.vars.find({id, order});
+  if (it == c->model.vars.end()) return fail(CBX_ERR_INVALID, "model variable not found (id %d, order %d)", id, order);
+  it->second.lr_multiplier = multiplier;
+  if (multiplier != 1.0f) c->model.conf.irregular++;  // executioncontext.c:1602-1603
+  return CBX_OK;
+}
+
 int cbx_set_model_work_per_clock(cbx_context *c, int wpc) {
   TRY(check_ctx(c));
   c->model.wpc = wpc;
@@ -1006,6 +1021,21 @@ int cbx_set_learning_rate_decay_policy_exp(cbx_context *c, float rate, double ga
   c->model.conf.policy = LR_EXP;
   c->model.conf.learningRate = rate;
   c->model.conf.gamma = gamma;
+  return CBX_OK;
+}
+
+int cbx_set_learning_rate_decay_policy_circular(cbx_context *c, const float *rate, int superconvergence,
+                                                 const float *momentum, int step) {
+  TRY(check_ctx(c));
+  if (!rate || !momentum) return fail(CBX_ERR_INVALID, "circular policy needs 3 rates and 3 momenta");
+  SolverConf &s = c->model.conf;
+  s.policy = LR_CLR;  // executioncontext.c:1701-1718
+  s.superConvergence = superconvergence;
+  for (int i = 0; i < 3; ++i) {
+    s.circularLearningRate[i] = rate[i];
+    s.circularMomentum[i] = momentum[i];
+  }
+  s.size = step;
   return CBX_OK;
 }
 

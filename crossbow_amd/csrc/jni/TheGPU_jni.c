@@ -69,6 +69,11 @@ NATIVE(jint, setModelVariableBuffer) (JNIEnv *env, jobject obj, jint id, jint or
 	return fatal_or (cbx_set_model_variable_buffer (theGPU, id, order, (*env)->GetDirectBufferAddress (env, buffer)));
 }
 
+NATIVE(jint, setModelVariableLearningRateMultiplier) (JNIEnv *env, jobject obj, jint id, jint order, jfloat multiplier) {
+	(void) env; (void) obj;
+	return fatal_or (cbx_set_model_variable_learning_rate_multiplier (theGPU, id, order, multiplier));
+}
+
 NATIVE(jint, setModelWorkPerClock) (JNIEnv *env, jobject obj, jint wpc) {
 	(void) env; (void) obj;
 	return fatal_or (cbx_set_model_work_per_clock (theGPU, wpc));
@@ -107,6 +112,23 @@ NATIVE(jint, setLearningRateDecayPolicyMultiStep) (JNIEnv *env, jobject obj, jfl
 NATIVE(jint, setLearningRateDecayPolicyExp) (JNIEnv *env, jobject obj, jfloat rate, jdouble gamma) {
 	(void) env; (void) obj;
 	return fatal_or (cbx_set_learning_rate_decay_policy_exp (theGPU, rate, gamma));
+}
+
+/* GPU.c:803-822 */
+NATIVE(jint, setLearningRateDecayPolicyCircular) (JNIEnv *env, jobject obj, jfloatArray rate, jint superconvergence,
+		jfloatArray momentum, jint step) {
+	(void) obj;
+	if ((*env)->GetArrayLength (env, rate) != 3 || (*env)->GetArrayLength (env, momentum) != 3) {
+		fprintf (stderr, "error: circular learning rate policy needs 3 rates and 3 momenta\n");
+		exit (1);
+	}
+	jfloat *H = (*env)->GetFloatArrayElements (env, rate, 0);
+	jfloat *M = (*env)->GetFloatArrayElements (env, momentum, 0);
+	int rc = cbx_set_learning_rate_decay_policy_circular (theGPU, (const float *) H, superconvergence,
+			(const float *) M, step);
+	(*env)->ReleaseFloatArrayElements (env, rate, H, JNI_ABORT);
+	(*env)->ReleaseFloatArrayElements (env, momentum, M, JNI_ABORT);
+	return fatal_or (rc);
 }
 
 NATIVE(jint, setBaseModelMomentum) (JNIEnv *env, jobject obj, jfloat momentum) {

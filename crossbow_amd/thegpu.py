@@ -85,6 +85,9 @@ class TheGPU:
         a = np.ascontiguousarray(np.frombuffer(memoryview(buffer), dtype=np.uint8))
         return check(self._L.cbx_set_model_variable_buffer(self._ctx, id, order, _ptr(a)))
 
+    def setModelVariableLearningRateMultiplier(self, id: int, order: int, multiplier: float) -> int:
+        return check(self._L.cbx_set_model_variable_learning_rate_multiplier(self._ctx, id, order, multiplier))
+
     def setModelWorkPerClock(self, wpc: int) -> int:
         return check(self._L.cbx_set_model_work_per_clock(self._ctx, wpc))
 
@@ -108,6 +111,14 @@ class TheGPU:
 
     def setLearningRateDecayPolicyExp(self, rate: float, gamma: float) -> int:
         return check(self._L.cbx_set_learning_rate_decay_policy_exp(self._ctx, rate, gamma))
+
+    def setLearningRateDecayPolicyCircular(self, rate: Sequence[float], superconvergence: int,
+                                           momentum: Sequence[float], step: int) -> int:
+        if len(rate) != 3 or len(momentum) != 3:
+            raise CbxError(_lib.CBX_ERR_INVALID, "circular policy needs 3 rates and 3 momenta")  # GPU.c:810
+        r = (ctypes.c_float * 3)(*rate)
+        m = (ctypes.c_float * 3)(*momentum)
+        return check(self._L.cbx_set_learning_rate_decay_policy_circular(self._ctx, r, superconvergence, m, step))
 
     def setBaseModelMomentum(self, momentum: float) -> int:
         return check(self._L.cbx_set_base_model_momentum(self._ctx, momentum))

@@ -80,6 +80,10 @@ int cbx_set_model_variable (cbx_context *ctx, int id, int order, int ndims,
 		const int *shape, int capacity);
 /* TheGPU.setModelVariableBuffer(IILjava/nio/ByteBuffer;)  GPU.c:698-708 */
 int cbx_set_model_variable_buffer (cbx_context *ctx, int id, int order, const void *src);
+/* TheGPU.setModelVariableLearningRateMultiplier(IIF)  GPU.c:710-719.  Stored
+ * (executioncontext.c:1592-1605); the SMA optimiser step ignores it, as the
+ * reference's does (optimisers/sma.cu uses the solver rate only).         */
+int cbx_set_model_variable_learning_rate_multiplier (cbx_context *ctx, int id, int order, float multiplier);
 /* TheGPU.setModelWorkPerClock(I)           GPU.c:721-730  */
 int cbx_set_model_work_per_clock (cbx_context *ctx, int wpc);
 /* TheGPU.setUpdateModelType(I)             GPU.c:732-741; 3 and 7 accepted */
@@ -93,6 +97,11 @@ int cbx_set_learning_rate_decay_policy_step (cbx_context *ctx, float rate, doubl
 int cbx_set_learning_rate_decay_policy_multistep (cbx_context *ctx, float rate, double gamma,
 		int warmuptasks, int nsteps, const int *steps);
 int cbx_set_learning_rate_decay_policy_exp (cbx_context *ctx, float rate, double gamma);
+/* TheGPU.setLearningRateDecayPolicyCircular([FI[FI)  GPU.c:803-822: rate[3],
+ * momentum[3]; stored, and a learning-rate query then fails with
+ * CBX_ERR_UNSUPPORTED as the reference's does (solverconfiguration.c:155-157). */
+int cbx_set_learning_rate_decay_policy_circular (cbx_context *ctx, const float *rate, int superconvergence,
+		const float *momentum, int step);
 /* TheGPU.setBaseModelMomentum(F)  GPU.c:823-832 (stored, unused: sma.c:152) */
 int cbx_set_base_model_momentum (cbx_context *ctx, float momentum);
 /* TheGPU.setMomentum(FI)          GPU.c:834-843 */

@@ -14,6 +14,7 @@ typedef uint8_t jboolean;
 typedef jint jsize;
 typedef struct _jobject *jobject;
 typedef jobject jintArray;
+typedef jobject jfloatArray;
 typedef jobject jstring;
 #define JNI_FALSE 0
 #define JNI_TRUE 1
@@ -26,6 +27,8 @@ struct JNINativeInterface_ {
 	jsize (*GetArrayLength) (JNIEnv *, jobject);
 	jint *(*GetIntArrayElements) (JNIEnv *, jintArray, jboolean *);
 	void (*ReleaseIntArrayElements) (JNIEnv *, jintArray, jint *, jint);
+	jfloat *(*GetFloatArrayElements) (JNIEnv *, jfloatArray, jboolean *);
+	void (*ReleaseFloatArrayElements) (JNIEnv *, jfloatArray, jfloat *, jint);
 	void *(*GetDirectBufferAddress) (JNIEnv *, jobject);
 	const char *(*GetStringUTFChars) (JNIEnv *, jstring, jboolean *);
 	void (*ReleaseStringUTFChars) (JNIEnv *, jstring, const char *);

@@ -71,7 +71,8 @@ def test_null_context_is_an_error_not_a_crash():
 
 # The model-path natives of TheGPU.java (:268-354) the shim must export.
 JNI_NATIVES = [
-    "init", "free", "setModel", "setModelVariable", "setModelVariableBuffer", "setModelWorkPerClock",
+    "init", "free", "setModel", "setModelVariable", "setModelVariableBuffer",
+    "setModelVariableLearningRateMultiplier", "setModelWorkPerClock", "setLearningRateDecayPolicyCircular",
     "setUpdateModelType", "setLearningRateDecayPolicyFixed", "setLearningRateDecayPolicyInv",
     "setLearningRateDecayPolicyStep", "setLearningRateDecayPolicyMultiStep", "setLearningRateDecayPolicyExp",
     "setBaseModelMomentum", "setMomentum", "setWeightDecay", "setEamsgdAlpha", "setEamsgdTau",
