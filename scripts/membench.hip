@@ -489,6 +489,39 @@ int main(int argc, char **argv) {
     }
     return 0;
   }
+
+  if (argc > 2 && std::strcmp(argv[2], "v8") == 0) {
+    // Allocation flavour: the default hipMalloc arena vs a physically
+    // contiguous one (hipDeviceMallocContiguous): fewer, larger TLB fragments
+    // for 28 streams spread over ~2 GB.
+    const size_t stride = (buf + (2u << 20) - 1) / (2u << 20) * (2u << 20) + 4096;
+    char *contig = nullptr;
+    hipError_t ce = hipExtMallocWithFlags((void **)&contig, nbuf * stride + (4u << 20), hipDeviceMallocContiguous);
+    std::printf("{\"v8\":\"contiguous-alloc\",\"ok\":%d}\n", ce == hipSuccess ? 1 : 0);
+    for (int round = 0; round < 2; ++round)
+      for (int which = 0; which < (ce == hipSuccess ? 2 : 1); ++which) {
+        char *base = which ? contig : arena;
+        Args a;
+        a.z = (v4f *)base;
+        a.last = (v4f *)(base + stride);
+        for (int r = 0; r < R; ++r) {
+          a.s[r] = (const v4f *)(base + (2 + 2 * r) * stride);
+          a.w[r] = (v4f *)(base + (3 + 2 * r) * stride);
+        }
+        a.n4 = n4;
+        a.alpha = 0.1f;
+        if (round == 0) {
+          hipLaunchKernelGGL(fillk, dim3(8192), dim3(256), 0, 0, (uint32_t *)base, nbuf * stride / 4, 12345u);
+          CK(hipDeviceSynchronize());
+        }
+        float t = time_ms([&] { hipLaunchKernelGGL((fused3<1, false, true>), dim3(n4 / 128), dim3(128), 0, 0, a); }, iters);
+        float tr = time_ms([&] { hipLaunchKernelGGL(readk<1>, dim3(n4 / 128), dim3(128), 0, 0, a, sink); }, iters);
+        std::printf("{\"v8\":%d,\"alloc\":\"%s\",\"fused_GBs\":%.1f,\"read18_GBs\":%.1f}\n", round,
+                    which ? "contiguous" : "default", alg / t / 1e6, 18.0 * n4 * 16 / tr / 1e6);
+      }
+    if (contig) CK(hipFree(contig));
+    return 0;
+  }
   // Ceilings on the same arena (1 GiB copy).
   {
     const uint32_t cn4 = (uint32_t)((1u << 30) / 16);
