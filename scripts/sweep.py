@@ -17,6 +17,37 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
+def interleaved(g, args, nbytes, m, rounds=4):
+    from crossbow_amd import _lib
+    configs = [(64, 1), (64, 2), (128, 1), (128, 2), (256, 1), (256, 2), (512, 1)]
+    res = {c: [] for c in configs}
+    clock = 0
+    for _ in range(rounds):
+        for (block, unroll) in configs:
+            g.set_kernel_config(block, 0, 1, unroll)
+            for _ in range(5 + args.steps):
+                clock += 1
+                g.lockAny()
+                g.synchronise(0, clock, 0, False)
+                g.unlockAny()
+            g.wait()
+            res[(block, unroll)].append(statistics.median(g.timing_history(_lib.T_KERNEL)[-args.steps:]))
+    rows = []
+    for (block, unroll), ms in res.items():
+        med = statistics.median(ms)
+        row = dict(block=block, unroll=unroll, kernel_ms=round(med, 4), per_round=[round(x, 4) for x in ms],
+                   GBs=round(nbytes / (med * 1e-3) / 1e9, 1))
+        rows.append(row)
+        print(json.dumps(row), flush=True)
+    best = min(rows, key=lambda r: r["kernel_ms"])
+    print("BEST", json.dumps(best), flush=True)
+    tag = f"{args.model}_R{args.replicas}_m{m}_interleaved"
+    os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
+    with open(os.path.join(ROOT, "gpurun_out", f"sweep_{tag}.json"), "w") as f:
+        json.dump(dict(rows=rows, best=best), f, indent=1)
+    g.free()
+
+
 def main():
     import argparse
     p = argparse.ArgumentParser()
@@ -26,6 +57,8 @@ def main():
     p.add_argument("--steps", type=int, default=30)
     p.add_argument("--split", action="store_true")
     p.add_argument("--quick", action="store_true")
+    p.add_argument("--interleave", action="store_true",
+                   help="a few promising configs, interleaved over several rounds (cancels drift)")
     args = p.parse_args()
 
     from crossbow_amd import SYNC_BSP, UPDATE_SMA, TheGPU, _lib
@@ -45,6 +78,8 @@ def main():
     m = 1 if args.momentum > 0 else 0
     nbytes = (12 * args.replicas + 8 + 8 * m) * n if not args.split else (12 * args.replicas + 8) * n
 
+    if args.interleave:
+        return interleaved(g, args, nbytes, m)
     blocks = [64, 128, 256] if not args.quick else [128]
     bpcs = [0, 4] if not args.quick else [0]
     policies = [0, 1]
