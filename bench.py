@@ -49,10 +49,10 @@ def parse():
     p.add_argument("--replicas", type=int, default=8, help="replicas per GPU")
     p.add_argument("--alpha", type=float, default=0.1)
     p.add_argument("--momentum", type=float, default=0.9)
-    p.add_argument("--block", type=int, default=128)
+    p.add_argument("--block", type=int, default=64)
     p.add_argument("--blocks-per-cu", type=int, default=0)
     p.add_argument("--policy", type=int, default=1, help="0 plain, 1 nontemporal loads/stores")
-    p.add_argument("--unroll", type=int, default=1)
+    p.add_argument("--unroll", type=int, default=2)
     p.add_argument("--bucket-mb", type=float, default=0.0,
                    help="G>1 pipeline bucket (MB of fp32): 0 = library default (8 buckets), <0 = one bucket")
     p.add_argument("--calib-steps", type=int, default=10,

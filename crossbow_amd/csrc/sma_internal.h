@@ -47,10 +47,10 @@ constexpr int64_t kPadFloat4 = 1024;
 constexpr int64_t kCtrlFloats = 64;
 
 struct LaunchConfig {
-  int block = 128;         // threads per workgroup (128 measured best on MI355X, profiles/r01)
+  int block = 64;          // threads per workgroup: 64 x unroll 2 measured best (scripts/sweep.py --interleave)
   int blocks_per_cu = 0;   // 0: one trip per thread; >0: grid-stride, this many WGs per CU
   int policy = 1;          // 0 plain, 1 nontemporal global loads/stores
-  int unroll = 1;          // float4s per thread per trip (1 or 2)
+  int unroll = 2;          // float4s per lane per trip (1 or 2), wave-contiguous
   int num_cus = 256;
 };
 

@@ -54,6 +54,16 @@ __device__ __forceinline__ void sto(v4f *base, uint32_t off, v4f v) {
   st<P>(reinterpret_cast<v4f *>(reinterpret_cast<char *>(base) + off), v);
 }
 
+// Wave-contiguous indexing: with U float4s per lane, wave w of block b owns
+// the 64*U consecutive float4s starting at (b * waves_per_block + w) * 64 * U,
+// lane l the float4s base + 64 u.  Each wave-instruction still moves one
+// contiguous KiB, and a wave's U instructions per stream cover U KiB in a
+// row (U = 2 at 64-thread blocks measured best: scripts/sweep.py --interleave).
+template <int U>
+__device__ __forceinline__ uint32_t first_elem() {
+  return (blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 64u * U + (threadIdx.x & 63u);
+}
+
 __device__ __forceinline__ v4f vfma(v4f a, v4f b, v4f c) {
   return __builtin_elementwise_fma(a, b, c);
 }
@@ -80,11 +90,11 @@ __global__ __launch_bounds__(512) void sma_fused_kernel(const SmaArgs a) {
   const v4f mb = kBaseMomentum;
   const v4f one = 1.0f;
   const v4f mone = -1.0f;
-  for (uint32_t base = blockIdx.x * blockDim.x * U + threadIdx.x; base < n4; base += trip) {
+  for (uint32_t base = first_elem<U>(); base < n4; base += trip) {
     v4f zv[U], lv[U], acc[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const uint32_t i = (base + u * blockDim.x) * 16u;
+      const uint32_t i = (base + u * 64u) * 16u;
       zv[u] = ldo<P>(a.z, i);
       if constexpr (MOM) lv[u] = ldo<P>(a.last, i);
       acc[u] = 0.0f;
@@ -97,7 +107,7 @@ __global__ __launch_bounds__(512) void sma_fused_kernel(const SmaArgs a) {
         if (R < 0 && c + r >= nrep) break;
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-          const uint32_t i = (base + u * blockDim.x) * 16u;
+          const uint32_t i = (base + u * 64u) * 16u;
           sv[u][r] = ldo<P>(a.s[c + r], i);
           if constexpr (!COPY) wv[u][r] = ldo<P>(a.w[c + r], i);
         }
@@ -122,14 +132,14 @@ __global__ __launch_bounds__(512) void sma_fused_kernel(const SmaArgs a) {
         for (int r = 0; r < RR; ++r) {
           if (R < 0 && c + r >= nrep) break;
 #pragma unroll
-          for (int u = 0; u < U; ++u) sto<P>(a.w[c + r], (base + u * blockDim.x) * 16u, wv[u][r]);
+          for (int u = 0; u < U; ++u) sto<P>(a.w[c + r], (base + u * 64u) * 16u, wv[u][r]);
         }
       }
       if constexpr (R >= 0) break;
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const uint32_t i = (base + u * blockDim.x) * 16u;
+      const uint32_t i = (base + u * 64u) * 16u;
       v4f D = acc[u];
       if constexpr (MOM) {
         D = vfma(mb, lv[u], D);
@@ -141,7 +151,7 @@ __global__ __launch_bounds__(512) void sma_fused_kernel(const SmaArgs a) {
     if constexpr (COPY) {
       for (int r = 0; r < nrep; ++r) {
 #pragma unroll
-        for (int u = 0; u < U; ++u) sto<P>(a.w[r], (base + u * blockDim.x) * 16u, zv[u]);
+        for (int u = 0; u < U; ++u) sto<P>(a.w[r], (base + u * 64u) * 16u, zv[u]);
       }
     }
   }
@@ -160,13 +170,13 @@ __global__ __launch_bounds__(512) void sma_accumulate_kernel(const SmaArgs a) {
   const v4f al = a.alpha;
   const v4f nal = -a.alpha;
   const v4f mone = -1.0f;
-  for (uint32_t base = blockIdx.x * blockDim.x * U + threadIdx.x; base < n4; base += trip) {
+  for (uint32_t base = first_elem<U>(); base < n4; base += trip) {
     v4f zv[U], acc[U];
     const int nrep = (R >= 0) ? R : a.nrep;
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       acc[u] = 0.0f;
-      if (nrep > 0) zv[u] = ldo<P>(a.z, (base + u * blockDim.x) * 16u);
+      if (nrep > 0) zv[u] = ldo<P>(a.z, (base + u * 64u) * 16u);
     }
     for (int c = 0; c < nrep; c += RR) {
       v4f sv[U][RR], wv[U][RR];
@@ -175,7 +185,7 @@ __global__ __launch_bounds__(512) void sma_accumulate_kernel(const SmaArgs a) {
         if (R < 0 && c + r >= nrep) break;
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-          const uint32_t i = (base + u * blockDim.x) * 16u;
+          const uint32_t i = (base + u * 64u) * 16u;
           sv[u][r] = ldo<P>(a.s[c + r], i);
           wv[u][r] = ldo<P>(a.w[c + r], i);
         }
@@ -195,12 +205,12 @@ __global__ __launch_bounds__(512) void sma_accumulate_kernel(const SmaArgs a) {
       for (int r = 0; r < RR; ++r) {
         if (R < 0 && c + r >= nrep) break;
 #pragma unroll
-        for (int u = 0; u < U; ++u) sto<P>(a.w[c + r], (base + u * blockDim.x) * 16u, wv[u][r]);
+        for (int u = 0; u < U; ++u) sto<P>(a.w[c + r], (base + u * 64u) * 16u, wv[u][r]);
       }
       if constexpr (R >= 0) break;
     }
 #pragma unroll
-    for (int u = 0; u < U; ++u) sto<P>(a.acc, (base + u * blockDim.x) * 16u, acc[u]);
+    for (int u = 0; u < U; ++u) sto<P>(a.acc, (base + u * 64u) * 16u, acc[u]);
   }
 }
 
@@ -215,18 +225,18 @@ __global__ __launch_bounds__(512) void sma_apply_kernel(const SmaArgs a) {
   const uint32_t n4 = (uint32_t)a.n4;
   const v4f mb = kBaseMomentum;
   const v4f one = 1.0f;
-  for (uint32_t base = blockIdx.x * blockDim.x * U + threadIdx.x; base < n4; base += trip) {
+  for (uint32_t base = first_elem<U>(); base < n4; base += trip) {
     v4f Dv[U], zv[U], lv[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const uint32_t i = (base + u * blockDim.x) * 16u;
+      const uint32_t i = (base + u * 64u) * 16u;
       Dv[u] = ldo<P>(a.D, i);
       zv[u] = ldo<P>(a.z, i);
       if constexpr (MOM) lv[u] = ldo<P>(a.last, i);
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const uint32_t i = (base + u * blockDim.x) * 16u;
+      const uint32_t i = (base + u * 64u) * 16u;
       if constexpr (MOM) {
         Dv[u] = vfma(mb, lv[u], Dv[u]);
         sto<P>(a.last, i, Dv[u]);
@@ -237,7 +247,7 @@ __global__ __launch_bounds__(512) void sma_apply_kernel(const SmaArgs a) {
     if (copy) {
       for (int r = 0; r < a.nrep; ++r) {
 #pragma unroll
-        for (int u = 0; u < U; ++u) sto<P>(a.w[r], (base + u * blockDim.x) * 16u, zv[u]);
+        for (int u = 0; u < U; ++u) sto<P>(a.w[r], (base + u * 64u) * 16u, zv[u]);
       }
     }
   }
@@ -390,6 +400,10 @@ __global__ __launch_bounds__(512) void copy_kernel(v4f *dst, const v4f *src, int
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) st<P>(dst + i, ld<P>(src + i));
 }
 
+// One-float4-per-lane kernels (optimiser step, S-SGD) run 128-thread blocks:
+// 6.0 TB/s measured for the optimiser step (profiles/r01).
+constexpr int kAuxBlock = 128;
+
 // Grid for a range of n4 float4s (a multiple of block*unroll).
 inline dim3 grid_for(int64_t n4, const LaunchConfig &cfg) {
   const int64_t per_block = (int64_t)cfg.block * cfg.unroll;
@@ -492,6 +506,7 @@ hipError_t launch_sma_apply(const SmaArgs &a, bool momentum, const LaunchConfig 
 hipError_t launch_sma_optimise(const OptArgs &a, const LaunchConfig &cfg, hipStream_t stream, Timing t) {
   LaunchConfig c = cfg;
   c.unroll = 1;
+  c.block = kAuxBlock;
   const dim3 g = grid_for(a.n4, c);
   const dim3 b(c.block);
   const bool mom = a.momentum > 0.0f, wd = a.wd > 0.0f;
@@ -518,6 +533,7 @@ hipError_t launch_sma_optimise(const OptArgs &a, const LaunchConfig &cfg, hipStr
 hipError_t launch_ssgd_accumulate(const SsgdArgs &a, const LaunchConfig &cfg, hipStream_t stream, Timing t) {
   LaunchConfig c = cfg;
   c.unroll = 1;
+  c.block = kAuxBlock;
   const dim3 g = grid_for(a.n4, c);
   const dim3 b(c.block);
   const bool wd = a.wd > 0.0f;
@@ -534,6 +550,7 @@ hipError_t launch_ssgd_accumulate(const SsgdArgs &a, const LaunchConfig &cfg, hi
 hipError_t launch_ssgd_apply(const SsgdArgs &a, const LaunchConfig &cfg, hipStream_t stream, Timing t) {
   LaunchConfig c = cfg;
   c.unroll = 1;
+  c.block = kAuxBlock;
   const dim3 g = grid_for(a.n4, c);
   const dim3 b(c.block);
   const bool mom = a.momentum > 0.0f;

@@ -303,7 +303,7 @@ class TheGPU:
         k = check(self._L.cbx_timing_history(self._ctx, local, which, ms, max_steps))
         return np.array(ms[:k], dtype=np.float64)
 
-    def set_kernel_config(self, block: int = 256, blocks_per_cu: int = 0, policy: int = 1, unroll: int = 1) -> None:
+    def set_kernel_config(self, block: int = 64, blocks_per_cu: int = 0, policy: int = 1, unroll: int = 2) -> None:
         check(self._L.cbx_set_kernel_config(self._ctx, block, blocks_per_cu, policy, unroll))
 
     def set_bucket_elements(self, elements: int) -> None:

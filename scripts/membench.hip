@@ -307,6 +307,48 @@ __global__ __launch_bounds__(128) void fused_buf(const BArgs a, char *arena, uin
   S(a.off_last, D);
   S(a.off_z, vfma(one, D, zv));
 }
+
+// ---- v9: wave-contiguous U float4 per lane per stream (a wave covers
+// U KiB of each stream), all loads in flight before the first FMA.
+template <int U>
+__global__ __launch_bounds__(256) void fused_wc(const Args a) {
+  const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+  const uint32_t e0 = (blockIdx.x * (blockDim.x >> 6) + wave) * 64u * U + lane;
+  if (e0 >= a.n4) return;
+  const v4f al = a.alpha, nal = -a.alpha, mb = 0.9f, one = 1.0f, mone = -1.0f;
+  v4f zv[U], lv[U], sv[U][R], wv[U][R];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const uint32_t i = (e0 + 64u * u) * 16u;
+    zv[u] = ldo<1>(a.z, i);
+    lv[u] = ldo<1>(a.last, i);
+  }
+#pragma unroll
+  for (int r = 0; r < R; ++r)
+#pragma unroll
+    for (int u = 0; u < U; ++u) sv[u][r] = ldo<1>(a.s[r], (e0 + 64u * u) * 16u);
+#pragma unroll
+  for (int r = 0; r < R; ++r)
+#pragma unroll
+    for (int u = 0; u < U; ++u) wv[u][r] = ldo<1>(a.w[r], (e0 + 64u * u) * 16u);
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const uint32_t i = (e0 + 64u * u) * 16u;
+    v4f acc = 0.0f;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      v4f d = vfma(mone, zv[u], sv[u][r]);
+      wv[u][r] = vfma(nal, d, wv[u][r]);
+      acc = vfma(al, d, acc);
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) sto<1>(a.w[r], i, wv[u][r]);
+    v4f D = vfma(mb, lv[u], acc);
+    sto<1>(a.last, i, D);
+    sto<1>(a.z, i, vfma(one, D, zv[u]));
+  }
+}
 static hipEvent_t e0, e1;
 
 template <typename F>
@@ -520,6 +562,34 @@ int main(int argc, char **argv) {
                     which ? "contiguous" : "default", alg / t / 1e6, 18.0 * n4 * 16 / tr / 1e6);
       }
     if (contig) CK(hipFree(contig));
+    return 0;
+  }
+
+  if (argc > 2 && std::strcmp(argv[2], "v9") == 0) {
+    const size_t stride = (buf + (2u << 20) - 1) / (2u << 20) * (2u << 20) + 4096;
+    Args a;
+    a.z = (v4f *)arena;
+    a.last = (v4f *)(arena + stride);
+    for (int r = 0; r < R; ++r) {
+      a.s[r] = (const v4f *)(arena + (2 + 2 * r) * stride);
+      a.w[r] = (v4f *)(arena + (3 + 2 * r) * stride);
+    }
+    a.n4 = n4;
+    a.alpha = 0.1f;
+    hipLaunchKernelGGL(fillk, dim3(8192), dim3(256), 0, 0, (uint32_t *)arena, nbuf * stride / 4, 12345u);
+    CK(hipDeviceSynchronize());
+    for (int round = 0; round < 3; ++round)
+      for (int blk : {64, 128, 256}) {
+        auto go = [&](auto kern, int U) {
+          const unsigned grid = (n4 + blk * U - 1) / (blk * U);
+          float t = time_ms([&] { hipLaunchKernelGGL(kern, dim3(grid), dim3(blk), 0, 0, a); }, iters);
+          std::printf("{\"v9\":%d,\"block\":%d,\"U\":%d,\"GBs\":%.1f}\n", round, blk, U, alg / t / 1e6);
+        };
+        go(fused_wc<1>, 1);
+        go(fused_wc<2>, 2);
+        go(fused_wc<3>, 3);
+        go(fused_wc<4>, 4);
+      }
     return 0;
   }
   // Ceilings on the same arena (1 GiB copy).

@@ -19,7 +19,7 @@ sys.path.insert(0, ROOT)
 
 def interleaved(g, args, nbytes, m, rounds=4):
     from crossbow_amd import _lib
-    configs = [(64, 1), (64, 2), (128, 1), (128, 2), (256, 1), (256, 2), (512, 1)]
+    configs = [(64, 1), (64, 2), (128, 1), (128, 2), (256, 2), (512, 2)]
     res = {c: [] for c in configs}
     clock = 0
     for _ in range(rounds):
