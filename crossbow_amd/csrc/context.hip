@@ -1832,6 +1832,13 @@ int cbx_set_kernel_config(cbx_context *c, int block, int blocks_per_cu, int poli
   return CBX_OK;
 }
 
+int cbx_set_kernel_occupancy(cbx_context *c, int waves_per_simd) {
+  TRY(check_ctx(c));
+  if (waves_per_simd < 0 || waves_per_simd > 8) return fail(CBX_ERR_INVALID, "waves per SIMD must be 0..8");
+  c->cfg.waves_per_simd = waves_per_simd;
+  return CBX_OK;
+}
+
 int cbx_set_bucket_elements(cbx_context *c, long long bucket_elements) {
   TRY(check_ctx(c));
   if (bucket_elements < 0) return fail(CBX_ERR_INVALID, "negative bucket size");

@@ -420,9 +420,9 @@ template <int R, bool MOM, bool COPY, int P>
 hipError_t fused_u(const SmaArgs &a, const LaunchConfig &cfg, hipStream_t s, Timing t) {
   const dim3 g = grid_for(a.n4, cfg);
   if (cfg.unroll == 2)
-    hipExtLaunchKernelGGL((sma_fused_kernel<R, MOM, COPY, P, 2>), g, dim3(cfg.block), 0, s, t.start, t.stop, 0, a);
+    hipExtLaunchKernelGGL((sma_fused_kernel<R, MOM, COPY, P, 2>), g, dim3(cfg.block), lds_for_occupancy(cfg), s, t.start, t.stop, 0, a);
   else
-    hipExtLaunchKernelGGL((sma_fused_kernel<R, MOM, COPY, P, 1>), g, dim3(cfg.block), 0, s, t.start, t.stop, 0, a);
+    hipExtLaunchKernelGGL((sma_fused_kernel<R, MOM, COPY, P, 1>), g, dim3(cfg.block), lds_for_occupancy(cfg), s, t.start, t.stop, 0, a);
   return hipGetLastError();
 }
 
@@ -446,9 +446,9 @@ template <int R, int P>
 hipError_t acc_u(const SmaArgs &a, const LaunchConfig &cfg, hipStream_t s, Timing t) {
   const dim3 g = grid_for(a.n4, cfg);
   if (cfg.unroll == 2)
-    hipExtLaunchKernelGGL((sma_accumulate_kernel<R, P, 2>), g, dim3(cfg.block), 0, s, t.start, t.stop, 0, a);
+    hipExtLaunchKernelGGL((sma_accumulate_kernel<R, P, 2>), g, dim3(cfg.block), lds_for_occupancy(cfg), s, t.start, t.stop, 0, a);
   else
-    hipExtLaunchKernelGGL((sma_accumulate_kernel<R, P, 1>), g, dim3(cfg.block), 0, s, t.start, t.stop, 0, a);
+    hipExtLaunchKernelGGL((sma_accumulate_kernel<R, P, 1>), g, dim3(cfg.block), lds_for_occupancy(cfg), s, t.start, t.stop, 0, a);
   return hipGetLastError();
 }
 
@@ -472,9 +472,9 @@ template <bool MOM, int P>
 hipError_t apply_u(const SmaArgs &a, const LaunchConfig &cfg, hipStream_t s, Timing t) {
   const dim3 g = grid_for(a.n4, cfg);
   if (cfg.unroll == 2)
-    hipExtLaunchKernelGGL((sma_apply_kernel<MOM, P, 2>), g, dim3(cfg.block), 0, s, t.start, t.stop, 0, a);
+    hipExtLaunchKernelGGL((sma_apply_kernel<MOM, P, 2>), g, dim3(cfg.block), lds_for_occupancy(cfg), s, t.start, t.stop, 0, a);
   else
-    hipExtLaunchKernelGGL((sma_apply_kernel<MOM, P, 1>), g, dim3(cfg.block), 0, s, t.start, t.stop, 0, a);
+    hipExtLaunchKernelGGL((sma_apply_kernel<MOM, P, 1>), g, dim3(cfg.block), lds_for_occupancy(cfg), s, t.start, t.stop, 0, a);
   return hipGetLastError();
 }
 

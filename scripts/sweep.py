@@ -17,25 +17,28 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
-def interleaved(g, args, nbytes, m, rounds=4):
+def interleaved(g, args, nbytes, m, rounds=3):
     from crossbow_amd import _lib
-    configs = [(64, 1), (64, 2), (128, 1), (128, 2), (256, 2), (512, 2)]
+    configs = [(64, 1, 0), (64, 2, 0), (128, 1, 0), (64, 1, 2), (64, 1, 3), (64, 1, 4), (64, 2, 1), (64, 2, 2),
+               (128, 1, 2), (128, 1, 3), (128, 2, 2), (256, 1, 2)]
     res = {c: [] for c in configs}
     clock = 0
     for _ in range(rounds):
-        for (block, unroll) in configs:
+        for (block, unroll, occ) in configs:
             g.set_kernel_config(block, 0, 1, unroll)
+            g.set_kernel_occupancy(occ)
             for _ in range(5 + args.steps):
                 clock += 1
                 g.lockAny()
                 g.synchronise(0, clock, 0, False)
                 g.unlockAny()
             g.wait()
-            res[(block, unroll)].append(statistics.median(g.timing_history(_lib.T_KERNEL)[-args.steps:]))
+            res[(block, unroll, occ)].append(statistics.median(g.timing_history(_lib.T_KERNEL)[-args.steps:]))
     rows = []
-    for (block, unroll), ms in res.items():
+    for (block, unroll, occ), ms in res.items():
         med = statistics.median(ms)
-        row = dict(block=block, unroll=unroll, kernel_ms=round(med, 4), per_round=[round(x, 4) for x in ms],
+        row = dict(block=block, unroll=unroll, waves_per_simd_cap=occ, kernel_ms=round(med, 4),
+                   per_round=[round(x, 4) for x in ms],
                    GBs=round(nbytes / (med * 1e-3) / 1e9, 1))
         rows.append(row)
         print(json.dumps(row), flush=True)
