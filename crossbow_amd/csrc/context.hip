@@ -1819,8 +1819,10 @@ int cbx_timing_history(cbx_context *c, int local, int which, float *ms, int max)
 
 int cbx_set_kernel_config(cbx_context *c, int block, int blocks_per_cu, int policy, int unroll) {
   TRY(check_ctx(c));
-  if (block < 64 || block > 512 || block % 64 != 0) return fail(CBX_ERR_INVALID, "block must be 64..512, multiple of 64");
-  if (unroll != 1 && unroll != 2) return fail(CBX_ERR_INVALID, "unroll must be 1 or 2");
+  // __launch_bounds__(256): at most one wave per SIMD per workgroup, so an
+  // unroll-4 wave may hold its 72 float4s in the 512-entry VGPR+AGPR file.
+  if (block < 64 || block > 256 || block % 64 != 0) return fail(CBX_ERR_INVALID, "block must be 64..256, multiple of 64");
+  if (unroll != 1 && unroll != 2 && unroll != 4) return fail(CBX_ERR_INVALID, "unroll must be 1, 2 or 4");
   if (policy != 0 && policy != 1) return fail(CBX_ERR_INVALID, "policy must be 0 or 1");
   if (blocks_per_cu < 0) return fail(CBX_ERR_INVALID, "blocks_per_cu must be >= 0");
   if ((int64_t)block * unroll > cbx::kPadFloat4 || cbx::kPadFloat4 % ((int64_t)block * unroll) != 0)

@@ -81,7 +81,7 @@ __device__ __forceinline__ v4f vfma(v4f a, v4f b, v4f c) {
 //   w_i = z                            :185-227 (if any replica asked to copy)
 // ---------------------------------------------------------------------------
 template <int R, bool MOM, bool COPY, int P, int U>
-__global__ __launch_bounds__(512) void sma_fused_kernel(const SmaArgs a) {
+__global__ __launch_bounds__(256) void sma_fused_kernel(const SmaArgs a) {
   constexpr int RR = (R > 0) ? R : kChunk;
   const uint32_t trip = gridDim.x * blockDim.x * U;
   const uint32_t n4 = (uint32_t)a.n4;
@@ -161,7 +161,7 @@ __global__ __launch_bounds__(512) void sma_fused_kernel(const SmaArgs a) {
 // Kernel A (G > 1): Phase A on this device's locked replicas -> acc.
 // ---------------------------------------------------------------------------
 template <int R, int P, int U>
-__global__ __launch_bounds__(512) void sma_accumulate_kernel(const SmaArgs a) {
+__global__ __launch_bounds__(256) void sma_accumulate_kernel(const SmaArgs a) {
   constexpr int RR = (R > 0) ? R : kChunk;
   if (a.ctrl_out != nullptr && blockIdx.x == 0 && threadIdx.x < kCtrlFloats)
     a.ctrl_out[threadIdx.x] = (threadIdx.x == 0) ? a.copies : 0.0f;
@@ -219,7 +219,7 @@ __global__ __launch_bounds__(512) void sma_accumulate_kernel(const SmaArgs a) {
 // reduced control block says any device had a copy request.
 // ---------------------------------------------------------------------------
 template <bool MOM, int P, int U>
-__global__ __launch_bounds__(512) void sma_apply_kernel(const SmaArgs a) {
+__global__ __launch_bounds__(256) void sma_apply_kernel(const SmaArgs a) {
   const bool copy = a.ctrl_in[0] > 0.0f;
   const uint32_t trip = gridDim.x * blockDim.x * U;
   const uint32_t n4 = (uint32_t)a.n4;
@@ -419,10 +419,13 @@ inline dim3 grid_for(int64_t n4, const LaunchConfig &cfg) {
 template <int R, bool MOM, bool COPY, int P>
 hipError_t fused_u(const SmaArgs &a, const LaunchConfig &cfg, hipStream_t s, Timing t) {
   const dim3 g = grid_for(a.n4, cfg);
-  if (cfg.unroll == 2)
-    hipExtLaunchKernelGGL((sma_fused_kernel<R, MOM, COPY, P, 2>), g, dim3(cfg.block), lds_for_occupancy(cfg), s, t.start, t.stop, 0, a);
+  const unsigned lds = lds_for_occupancy(cfg);
+  if (cfg.unroll == 4)
+    hipExtLaunchKernelGGL((sma_fused_kernel<R, MOM, COPY, P, 4>), g, dim3(cfg.block), lds, s, t.start, t.stop, 0, a);
+  else if (cfg.unroll == 2)
+    hipExtLaunchKernelGGL((sma_fused_kernel<R, MOM, COPY, P, 2>), g, dim3(cfg.block), lds, s, t.start, t.stop, 0, a);
   else
-    hipExtLaunchKernelGGL((sma_fused_kernel<R, MOM, COPY, P, 1>), g, dim3(cfg.block), lds_for_occupancy(cfg), s, t.start, t.stop, 0, a);
+    hipExtLaunchKernelGGL((sma_fused_kernel<R, MOM, COPY, P, 1>), g, dim3(cfg.block), lds, s, t.start, t.stop, 0, a);
   return hipGetLastError();
 }
 
@@ -445,10 +448,13 @@ hipError_t fused_r(const SmaArgs &a, const LaunchConfig &cfg, hipStream_t s, Tim
 template <int R, int P>
 hipError_t acc_u(const SmaArgs &a, const LaunchConfig &cfg, hipStream_t s, Timing t) {
   const dim3 g = grid_for(a.n4, cfg);
-  if (cfg.unroll == 2)
-    hipExtLaunchKernelGGL((sma_accumulate_kernel<R, P, 2>), g, dim3(cfg.block), lds_for_occupancy(cfg), s, t.start, t.stop, 0, a);
+  const unsigned lds = lds_for_occupancy(cfg);
+  if (cfg.unroll == 4)
+    hipExtLaunchKernelGGL((sma_accumulate_kernel<R, P, 4>), g, dim3(cfg.block), lds, s, t.start, t.stop, 0, a);
+  else if (cfg.unroll == 2)
+    hipExtLaunchKernelGGL((sma_accumulate_kernel<R, P, 2>), g, dim3(cfg.block), lds, s, t.start, t.stop, 0, a);
   else
-    hipExtLaunchKernelGGL((sma_accumulate_kernel<R, P, 1>), g, dim3(cfg.block), lds_for_occupancy(cfg), s, t.start, t.stop, 0, a);
+    hipExtLaunchKernelGGL((sma_accumulate_kernel<R, P, 1>), g, dim3(cfg.block), lds, s, t.start, t.stop, 0, a);
   return hipGetLastError();
 }
 
@@ -471,10 +477,13 @@ hipError_t acc_r(const SmaArgs &a, const LaunchConfig &cfg, hipStream_t s, Timin
 template <bool MOM, int P>
 hipError_t apply_u(const SmaArgs &a, const LaunchConfig &cfg, hipStream_t s, Timing t) {
   const dim3 g = grid_for(a.n4, cfg);
-  if (cfg.unroll == 2)
-    hipExtLaunchKernelGGL((sma_apply_kernel<MOM, P, 2>), g, dim3(cfg.block), lds_for_occupancy(cfg), s, t.start, t.stop, 0, a);
+  const unsigned lds = lds_for_occupancy(cfg);
+  if (cfg.unroll == 4)
+    hipExtLaunchKernelGGL((sma_apply_kernel<MOM, P, 4>), g, dim3(cfg.block), lds, s, t.start, t.stop, 0, a);
+  else if (cfg.unroll == 2)
+    hipExtLaunchKernelGGL((sma_apply_kernel<MOM, P, 2>), g, dim3(cfg.block), lds, s, t.start, t.stop, 0, a);
   else
-    hipExtLaunchKernelGGL((sma_apply_kernel<MOM, P, 1>), g, dim3(cfg.block), lds_for_occupancy(cfg), s, t.start, t.stop, 0, a);
+    hipExtLaunchKernelGGL((sma_apply_kernel<MOM, P, 1>), g, dim3(cfg.block), lds, s, t.start, t.stop, 0, a);
   return hipGetLastError();
 }
 

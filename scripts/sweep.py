@@ -19,8 +19,8 @@ sys.path.insert(0, ROOT)
 
 def interleaved(g, args, nbytes, m, rounds=3):
     from crossbow_amd import _lib
-    configs = [(64, 1, 0), (64, 2, 0), (128, 1, 0), (64, 1, 2), (64, 1, 3), (64, 1, 4), (64, 2, 1), (64, 2, 2),
-               (128, 1, 2), (128, 1, 3), (128, 2, 2), (256, 1, 2)]
+    configs = [(64, 2, 0), (64, 1, 1), (64, 2, 1), (64, 4, 1), (64, 4, 0), (128, 2, 1), (128, 4, 1),
+               (256, 2, 1), (128, 1, 2), (64, 1, 2)]
     res = {c: [] for c in configs}
     clock = 0
     for _ in range(rounds):
