@@ -52,23 +52,22 @@ struct LaunchConfig {
   int policy = 1;          // 0 plain, 1 nontemporal global loads/stores
   int unroll = 2;          // float4s per lane per trip (1 or 2), wave-contiguous
   int num_cus = 256;
-  // Occupancy cap, in waves per SIMD (0 = none): enforced by reserving
-  // dynamic LDS per workgroup so that at most that many waves fit on a CU.
-  // Fewer concurrent waves means fewer DRAM pages open at once.
-  int waves_per_simd = 0;
+  // Occupancy cap, in waves per CU (0 = none): enforced by reserving
+  // dynamic LDS per workgroup so that only that many waves fit on a CU.
+  // Fewer concurrent waves means fewer DRAM pages open at once; with 18
+  // read streams per wave the fused kernel is fastest at ~4 waves per CU.
+  int waves_per_cu = 0;
 };
 
-// Dynamic LDS bytes per workgroup that cap a CU at cfg.waves_per_simd waves
-// per SIMD (160 KiB of LDS per CU on gfx950).
+// Dynamic LDS bytes per workgroup that cap a CU at cfg.waves_per_cu waves
+// (160 KiB of LDS per CU, at most 64 KiB per workgroup on gfx950).
 inline unsigned lds_for_occupancy(const LaunchConfig &cfg) {
-  if (cfg.waves_per_simd <= 0) return 0;
+  if (cfg.waves_per_cu <= 0) return 0;
   const int waves_per_wg = (cfg.block + 63) / 64;
-  int wgs_per_cu = (4 * cfg.waves_per_simd) / waves_per_wg;
+  int wgs_per_cu = cfg.waves_per_cu / waves_per_wg;
   if (wgs_per_cu < 1) wgs_per_cu = 1;
-  const unsigned lds_cu = 160u * 1024u;
-  // Largest multiple of 1 KiB such that wgs_per_cu fit and one more does not.
-  unsigned per = (lds_cu / (unsigned)wgs_per_cu) / 1024u * 1024u;
-  if (per > 64u * 1024u) per = 64u * 1024u;  // max LDS per workgroup
+  unsigned per = (160u * 1024u / (unsigned)wgs_per_cu) / 1024u * 1024u;
+  if (per > 64u * 1024u) per = 64u * 1024u;
   return per;
 }
 

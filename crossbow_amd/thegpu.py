@@ -306,8 +306,8 @@ class TheGPU:
     def set_kernel_config(self, block: int = 64, blocks_per_cu: int = 0, policy: int = 1, unroll: int = 2) -> None:
         check(self._L.cbx_set_kernel_config(self._ctx, block, blocks_per_cu, policy, unroll))
 
-    def set_kernel_occupancy(self, waves_per_simd: int) -> None:
-        check(self._L.cbx_set_kernel_occupancy(self._ctx, waves_per_simd))
+    def set_kernel_occupancy(self, waves_per_cu: int) -> None:
+        check(self._L.cbx_set_kernel_occupancy(self._ctx, waves_per_cu))
 
     def set_bucket_elements(self, elements: int) -> None:
         check(self._L.cbx_set_bucket_elements(self._ctx, elements))

@@ -19,8 +19,9 @@ sys.path.insert(0, ROOT)
 
 def interleaved(g, args, nbytes, m, rounds=3):
     from crossbow_amd import _lib
-    configs = [(64, 2, 0), (64, 1, 1), (64, 2, 1), (64, 4, 1), (64, 4, 0), (128, 2, 1), (128, 4, 1),
-               (256, 2, 1), (128, 1, 2), (64, 1, 2)]
+    # (block, unroll, waves-per-CU cap)
+    configs = [(64, 1, 0), (64, 1, 2), (64, 1, 3), (64, 1, 4), (64, 1, 5), (64, 1, 6), (64, 1, 8),
+               (64, 2, 2), (64, 2, 3), (64, 2, 4), (128, 1, 4), (128, 1, 6), (256, 1, 4)]
     res = {c: [] for c in configs}
     clock = 0
     for _ in range(rounds):
@@ -37,7 +38,7 @@ def interleaved(g, args, nbytes, m, rounds=3):
     rows = []
     for (block, unroll, occ), ms in res.items():
         med = statistics.median(ms)
-        row = dict(block=block, unroll=unroll, waves_per_simd_cap=occ, kernel_ms=round(med, 4),
+        row = dict(block=block, unroll=unroll, waves_per_cu_cap=occ, kernel_ms=round(med, 4),
                    per_round=[round(x, 4) for x in ms],
                    GBs=round(nbytes / (med * 1e-3) / 1e9, 1))
         rows.append(row)

@@ -114,9 +114,10 @@ def test_bsp_barrier_failure():
     dict(block=256, blocks_per_cu=0, policy=0, unroll=1),
     dict(block=256, blocks_per_cu=8, policy=1, unroll=1),
     dict(block=256, blocks_per_cu=4, policy=1, unroll=2),
-    dict(block=64, blocks_per_cu=0, policy=1, unroll=4, occupancy=1),
+    dict(block=64, blocks_per_cu=0, policy=1, unroll=4, occupancy=4),
     dict(block=128, blocks_per_cu=0, policy=1, unroll=4, occupancy=0),
     dict(block=64, blocks_per_cu=0, policy=1, unroll=1, occupancy=2),
+    dict(block=128, blocks_per_cu=0, policy=1, unroll=1, occupancy=4),
     dict(block=128, blocks_per_cu=0, policy=1, unroll=2),
 ])
 def test_launch_configs_identical(config):
@@ -434,7 +435,7 @@ def test_randomised_configurations_bitexact():
         split = rng.random() < 0.4
         bucket = rng.choice([0, 4096, 65_536]) if split else 0
         config = rng.choice([None, dict(block=64, blocks_per_cu=0, policy=1, unroll=2),
-                             dict(block=64, blocks_per_cu=0, policy=1, unroll=4, occupancy=1),
+                             dict(block=64, blocks_per_cu=0, policy=1, unroll=1, occupancy=4),
                              dict(block=256, blocks_per_cu=4, policy=0, unroll=1)])
         try:
             _run(n, R, alpha, momentum, copy_ids=copy_ids, first=first, held=held,
