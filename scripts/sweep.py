@@ -19,14 +19,15 @@ sys.path.insert(0, ROOT)
 
 def interleaved(g, args, nbytes, m, rounds=3):
     from crossbow_amd import _lib
-    # (block, unroll, waves-per-CU cap)
-    configs = [(64, 1, 0), (64, 1, 2), (64, 1, 3), (64, 1, 4), (64, 1, 5), (64, 1, 6), (64, 1, 8),
-               (64, 2, 2), (64, 2, 3), (64, 2, 4), (128, 1, 4), (128, 1, 6), (256, 1, 4)]
+    # (block, unroll, waves-per-CU cap, workgroups per CU for a grid-stride launch; 0 = one trip)
+    configs = [(64, 2, 2, 0), (64, 2, 3, 0), (64, 4, 2, 0), (64, 4, 3, 0), (64, 4, 4, 0), (128, 2, 4, 0),
+               (128, 2, 6, 0), (64, 1, 3, 0), (128, 1, 6, 0), (64, 2, 2, 2), (64, 2, 3, 3), (64, 4, 2, 2),
+               (128, 2, 4, 2)]
     res = {c: [] for c in configs}
     clock = 0
     for _ in range(rounds):
-        for (block, unroll, occ) in configs:
-            g.set_kernel_config(block, 0, 1, unroll)
+        for (block, unroll, occ, bpc) in configs:
+            g.set_kernel_config(block, bpc, 1, unroll)
             g.set_kernel_occupancy(occ)
             for _ in range(5 + args.steps):
                 clock += 1
@@ -34,11 +35,11 @@ def interleaved(g, args, nbytes, m, rounds=3):
                 g.synchronise(0, clock, 0, False)
                 g.unlockAny()
             g.wait()
-            res[(block, unroll, occ)].append(statistics.median(g.timing_history(_lib.T_KERNEL)[-args.steps:]))
+            res[(block, unroll, occ, bpc)].append(statistics.median(g.timing_history(_lib.T_KERNEL)[-args.steps:]))
     rows = []
-    for (block, unroll, occ), ms in res.items():
+    for (block, unroll, occ, bpc), ms in res.items():
         med = statistics.median(ms)
-        row = dict(block=block, unroll=unroll, waves_per_cu_cap=occ, kernel_ms=round(med, 4),
+        row = dict(block=block, unroll=unroll, waves_per_cu_cap=occ, blocks_per_cu=bpc, kernel_ms=round(med, 4),
                    per_round=[round(x, 4) for x in ms],
                    GBs=round(nbytes / (med * 1e-3) / 1e9, 1))
         rows.append(row)
