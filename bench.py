@@ -53,6 +53,8 @@ def parse():
     p.add_argument("--blocks-per-cu", type=int, default=0)
     p.add_argument("--policy", type=int, default=1, help="0 plain, 1 nontemporal loads/stores")
     p.add_argument("--unroll", type=int, default=2)
+    p.add_argument("--waves-per-cu", type=int, default=2,
+                   help="occupancy cap for the SMA kernels (0 = none); 2 measured best (profiles/r01/sweep_occupancy_*.log)")
     p.add_argument("--bucket-mb", type=float, default=0.0,
                    help="G>1 pipeline bucket (MB of fp32): 0 = library default (8 buckets), <0 = one bucket")
     p.add_argument("--calib-steps", type=int, default=10,
@@ -216,6 +218,7 @@ def main():
     gpu.setLearningRateDecayPolicyMultiStep(0.1, 0.1, 0, [1 << 30])
     gpu.setModelManager(args.replicas, SYNC_BSP)
     gpu.set_kernel_config(args.block, args.blocks_per_cu, args.policy, args.unroll)
+    gpu.set_kernel_occupancy(args.waves_per_cu)
     one_bucket = 1 << 62
     bucket_elems = int(args.bucket_mb * (1 << 20) / 4) if args.bucket_mb > 0 else (one_bucket if args.bucket_mb < 0 else 0)
     if args.force_split:
@@ -290,7 +293,7 @@ def main():
             "parallelism": f"sma-dp{G}",
             "pipeline": "fused" if not split else "accumulate+rccl-allreduce+apply, bucketed on two streams",
             "kernel_config": dict(block=args.block, blocks_per_cu=args.blocks_per_cu, policy=args.policy,
-                                  unroll=args.unroll, bucket_mb=args.bucket_mb),
+                                  unroll=args.unroll, waves_per_cu=args.waves_per_cu, bucket_mb=args.bucket_mb),
         },
     }
     kname = "sma_fused_kernel" if not split else "sma_accumulate_kernel"

@@ -47,7 +47,7 @@ constexpr int64_t kPadFloat4 = 1024;
 constexpr int64_t kCtrlFloats = 64;
 
 struct LaunchConfig {
-  int block = 64;          // threads per workgroup: 64 x unroll 2 measured best (scripts/sweep.py --interleave)
+  int block = 64;          // threads per workgroup: 64 x unroll 2 at 2 waves/CU measured best (sweep.py --interleave)
   int blocks_per_cu = 0;   // 0: one trip per thread; >0: grid-stride, this many WGs per CU
   int policy = 1;          // 0 plain, 1 nontemporal global loads/stores
   int unroll = 2;          // float4s per lane per trip (1 or 2), wave-contiguous
@@ -56,7 +56,7 @@ struct LaunchConfig {
   // dynamic LDS per workgroup so that only that many waves fit on a CU.
   // Fewer concurrent waves means fewer DRAM pages open at once; with 18
   // read streams per wave the fused kernel is fastest at ~4 waves per CU.
-  int waves_per_cu = 0;
+  int waves_per_cu = 2;
 };
 
 // Dynamic LDS bytes per workgroup that cap a CU at cfg.waves_per_cu waves
