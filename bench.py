@@ -53,8 +53,8 @@ def parse():
     p.add_argument("--blocks-per-cu", type=int, default=0)
     p.add_argument("--policy", type=int, default=1, help="0 plain, 1 nontemporal loads/stores")
     p.add_argument("--unroll", type=int, default=2)
-    p.add_argument("--waves-per-cu", type=int, default=2,
-                   help="occupancy cap for the SMA kernels (0 = none); 2 measured best (profiles/r01/sweep_occupancy_*.log)")
+    p.add_argument("--waves-per-cu", type=int, default=-1,
+                   help="occupancy cap for the SMA kernels: -1 auto (library default), 0 none, else waves per CU")
     p.add_argument("--bucket-mb", type=float, default=0.0,
                    help="G>1 pipeline bucket (MB of fp32): 0 = library default (8 buckets), <0 = one bucket")
     p.add_argument("--calib-steps", type=int, default=10,

@@ -1836,7 +1836,7 @@ int cbx_set_kernel_config(cbx_context *c, int block, int blocks_per_cu, int poli
 
 int cbx_set_kernel_occupancy(cbx_context *c, int waves_per_cu) {
   TRY(check_ctx(c));
-  if (waves_per_cu < 0 || waves_per_cu > 32) return fail(CBX_ERR_INVALID, "waves per CU must be 0..32");
+  if (waves_per_cu < -1 || waves_per_cu > 32) return fail(CBX_ERR_INVALID, "waves per CU must be -1 (auto) or 0..32");
   c->cfg.waves_per_cu = waves_per_cu;
   return CBX_OK;
 }

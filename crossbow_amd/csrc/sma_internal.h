@@ -52,19 +52,34 @@ struct LaunchConfig {
   int policy = 1;          // 0 plain, 1 nontemporal global loads/stores
   int unroll = 2;          // float4s per lane per trip (1 or 2), wave-contiguous
   int num_cus = 256;
-  // Occupancy cap, in waves per CU (0 = none): enforced by reserving
-  // dynamic LDS per workgroup so that only that many waves fit on a CU.
-  // Fewer concurrent waves means fewer DRAM pages open at once; with 18
-  // read streams per wave the fused kernel is fastest at ~4 waves per CU.
-  int waves_per_cu = 2;
+  // Occupancy cap, in waves per CU: 0 = none, -1 = auto (below).  Enforced
+  // by reserving dynamic LDS per workgroup so that only that many waves fit.
+  // Fewer concurrent waves keep fewer DRAM pages open: the SMA kernels run
+  // fastest with about kReadStreamsPerCU read streams in flight per CU
+  // (scripts/occupancy_sweep.py, profiles/r01/occupancy.json).
+  int waves_per_cu = -1;
 };
 
-// Dynamic LDS bytes per workgroup that cap a CU at cfg.waves_per_cu waves
+constexpr int kReadStreamsPerCU = 36;
+
+// Waves per CU for a kernel whose lanes read `reads` streams each.
+inline int auto_waves_per_cu(int reads) {
+  if (reads < 1) reads = 1;
+  int w = (kReadStreamsPerCU + reads / 2) / reads;
+  return w < 2 ? 2 : (w > 12 ? 12 : w);
+}
+
+// Dynamic LDS bytes per workgroup that cap a CU at the configured waves
 // (160 KiB of LDS per CU, at most 64 KiB per workgroup on gfx950).
-inline unsigned lds_for_occupancy(const LaunchConfig &cfg) {
-  if (cfg.waves_per_cu <= 0) return 0;
+// In auto mode a launch too small to fill the chip many times over (under
+// 16 waves per CU, e.g. LeNet's 4 MB buffers) is latency-bound and runs
+// uncapped.
+inline unsigned lds_for_occupancy(const LaunchConfig &cfg, int reads, unsigned grid) {
   const int waves_per_wg = (cfg.block + 63) / 64;
-  int wgs_per_cu = cfg.waves_per_cu / waves_per_wg;
+  if (cfg.waves_per_cu < 0 && (int64_t)grid * waves_per_wg < 16ll * cfg.num_cus) return 0;
+  const int cap = cfg.waves_per_cu < 0 ? auto_waves_per_cu(reads) : cfg.waves_per_cu;
+  if (cap <= 0) return 0;
+  int wgs_per_cu = cap / waves_per_wg;
   if (wgs_per_cu < 1) wgs_per_cu = 1;
   unsigned per = (160u * 1024u / (unsigned)wgs_per_cu) / 1024u * 1024u;
   if (per > 64u * 1024u) per = 64u * 1024u;

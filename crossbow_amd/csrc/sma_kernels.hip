@@ -419,7 +419,7 @@ inline dim3 grid_for(int64_t n4, const LaunchConfig &cfg) {
 template <int R, bool MOM, bool COPY, int P>
 hipError_t fused_u(const SmaArgs &a, const LaunchConfig &cfg, hipStream_t s, Timing t) {
   const dim3 g = grid_for(a.n4, cfg);
-  const unsigned lds = lds_for_occupancy(cfg);
+  const unsigned lds = lds_for_occupancy(cfg, (COPY ? 1 : 2) * a.nrep + 1 + (MOM ? 1 : 0), g.x);
   if (cfg.unroll == 4)
     hipExtLaunchKernelGGL((sma_fused_kernel<R, MOM, COPY, P, 4>), g, dim3(cfg.block), lds, s, t.start, t.stop, 0, a);
   else if (cfg.unroll == 2)
@@ -448,7 +448,7 @@ hipError_t fused_r(const SmaArgs &a, const LaunchConfig &cfg, hipStream_t s, Tim
 template <int R, int P>
 hipError_t acc_u(const SmaArgs &a, const LaunchConfig &cfg, hipStream_t s, Timing t) {
   const dim3 g = grid_for(a.n4, cfg);
-  const unsigned lds = lds_for_occupancy(cfg);
+  const unsigned lds = lds_for_occupancy(cfg, 2 * a.nrep + 1, g.x);
   if (cfg.unroll == 4)
     hipExtLaunchKernelGGL((sma_accumulate_kernel<R, P, 4>), g, dim3(cfg.block), lds, s, t.start, t.stop, 0, a);
   else if (cfg.unroll == 2)
@@ -477,7 +477,7 @@ hipError_t acc_r(const SmaArgs &a, const LaunchConfig &cfg, hipStream_t s, Timin
 template <bool MOM, int P>
 hipError_t apply_u(const SmaArgs &a, const LaunchConfig &cfg, hipStream_t s, Timing t) {
   const dim3 g = grid_for(a.n4, cfg);
-  const unsigned lds = lds_for_occupancy(cfg);
+  const unsigned lds = lds_for_occupancy(cfg, MOM ? 3 : 2, g.x);
   if (cfg.unroll == 4)
     hipExtLaunchKernelGGL((sma_apply_kernel<MOM, P, 4>), g, dim3(cfg.block), lds, s, t.start, t.stop, 0, a);
   else if (cfg.unroll == 2)

@@ -251,9 +251,10 @@ int cbx_timing_history (cbx_context *ctx, int local, int which, float *ms, int m
  * workgroups per CU for the grid-stride loop (0 = one float4 per thread),
  * load/store policy (0 plain, 1 nontemporal), float4s per thread per trip. */
 int cbx_set_kernel_config (cbx_context *ctx, int block, int blocks_per_cu, int policy, int unroll);
-/* Occupancy cap for the SMA kernels, in waves per CU (1..32; 0 = none),
- * enforced through reserved LDS per workgroup (the smallest reachable cap
- * is 2 workgroups per CU: at most 64 KiB of LDS per workgroup).          */
+/* Occupancy cap for the SMA kernels, in waves per CU: 1..32, 0 = none, -1
+ * = auto (the default: about 36 read streams in flight per CU, i.e. 2 waves
+ * for the R = 8 step, 12 for kernel B).  Enforced through reserved LDS per
+ * workgroup (so the smallest reachable cap is 2 workgroups per CU).      */
 int cbx_set_kernel_occupancy (cbx_context *ctx, int waves_per_cu);
 /* Bucketed pipeline for G > 1: kernel A / all-reduce / kernel B per bucket
  * of `bucket_elements` floats; 0 (default) = 8 buckets when G > 1, one at

@@ -17,7 +17,7 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
-CAPS = [0, 2, 3, 4, 6, 8, 12]
+CAPS = [-1, 0, 2, 3, 4, 6, 8, 12]
 
 
 def main():
