@@ -519,21 +519,22 @@ hipError_t launch_sma_optimise(const OptArgs &a, const LaunchConfig &cfg, hipStr
   const dim3 g = grid_for(a.n4, c);
   const dim3 b(c.block);
   const bool mom = a.momentum > 0.0f, wd = a.wd > 0.0f;
+  const unsigned l = lds_for_occupancy(c, mom ? 3 : 2, g.x);
   if (cfg.policy == 1) {
     if (mom) {
-      if (wd) hipExtLaunchKernelGGL((sma_optimise_kernel<true, true, 1>), g, b, 0, stream, t.start, t.stop, 0, a);
-      else hipExtLaunchKernelGGL((sma_optimise_kernel<true, false, 1>), g, b, 0, stream, t.start, t.stop, 0, a);
+      if (wd) hipExtLaunchKernelGGL((sma_optimise_kernel<true, true, 1>), g, b, l, stream, t.start, t.stop, 0, a);
+      else hipExtLaunchKernelGGL((sma_optimise_kernel<true, false, 1>), g, b, l, stream, t.start, t.stop, 0, a);
     } else {
-      if (wd) hipExtLaunchKernelGGL((sma_optimise_kernel<false, true, 1>), g, b, 0, stream, t.start, t.stop, 0, a);
-      else hipExtLaunchKernelGGL((sma_optimise_kernel<false, false, 1>), g, b, 0, stream, t.start, t.stop, 0, a);
+      if (wd) hipExtLaunchKernelGGL((sma_optimise_kernel<false, true, 1>), g, b, l, stream, t.start, t.stop, 0, a);
+      else hipExtLaunchKernelGGL((sma_optimise_kernel<false, false, 1>), g, b, l, stream, t.start, t.stop, 0, a);
     }
   } else {
     if (mom) {
-      if (wd) hipExtLaunchKernelGGL((sma_optimise_kernel<true, true, 0>), g, b, 0, stream, t.start, t.stop, 0, a);
-      else hipExtLaunchKernelGGL((sma_optimise_kernel<true, false, 0>), g, b, 0, stream, t.start, t.stop, 0, a);
+      if (wd) hipExtLaunchKernelGGL((sma_optimise_kernel<true, true, 0>), g, b, l, stream, t.start, t.stop, 0, a);
+      else hipExtLaunchKernelGGL((sma_optimise_kernel<true, false, 0>), g, b, l, stream, t.start, t.stop, 0, a);
     } else {
-      if (wd) hipExtLaunchKernelGGL((sma_optimise_kernel<false, true, 0>), g, b, 0, stream, t.start, t.stop, 0, a);
-      else hipExtLaunchKernelGGL((sma_optimise_kernel<false, false, 0>), g, b, 0, stream, t.start, t.stop, 0, a);
+      if (wd) hipExtLaunchKernelGGL((sma_optimise_kernel<false, true, 0>), g, b, l, stream, t.start, t.stop, 0, a);
+      else hipExtLaunchKernelGGL((sma_optimise_kernel<false, false, 0>), g, b, l, stream, t.start, t.stop, 0, a);
     }
   }
   return hipGetLastError();
