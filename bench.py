@@ -65,6 +65,8 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-staged", action="store_true")
     p.add_argument("--no-copy-ceiling", action="store_true")
+    p.add_argument("--staged-buckets", type=int, default=8,
+                   help="buckets of the pipelined host-staged step (cbx_synchronise_staged)")
     p.add_argument("--no-optimiser", action="store_true", help="skip the replica optimiser-step measurement")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
                    help="PMC-derived HBM bytes per launch (written by scripts/pmc_traffic.py)")
@@ -351,6 +353,22 @@ def main():
                 "d2h_GBs": round(d2h / (t[_lib.T_D2H] * 1e-3) / 1e9, 2),
                 "end_to_end_GBs": round(step_bytes / tot / 1e9, 2),
             }
+            # The same step through cbx_synchronise_staged: uploads, kernels and
+            # downloads pipelined over buckets on three streams.
+            piped = []
+            for _ in range(3):
+                clock += 1
+                gpu.lockAny()
+                gpu.synchronise_staged(0, clock, 0, args.staged_buckets)
+                gpu.unlockAny()
+                gpu.wait()
+                piped.append(gpu.last_timing(0))
+            p = sorted(piped, key=lambda x: x[_lib.T_STEP])[1]
+            result["host_staged"]["pipelined"] = {
+                "buckets": args.staged_buckets, "step_ms": round(p[_lib.T_STEP], 3),
+                "h2d_ms": round(p[_lib.T_H2D], 3), "d2h_ms": round(p[_lib.T_D2H], 3),
+                "end_to_end_GBs": round(step_bytes / (p[_lib.T_STEP] * 1e-3) / 1e9, 2),
+                "timed": "HIP events: sync stream at entry to sync stream after the last download"}
         if not args.no_cpu_baseline:
             # multithreaded first: OpenBLAS's pool must not start out bound to core 0
             threads = max(1, min(16, len(os.sched_getaffinity(0))))

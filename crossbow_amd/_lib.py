@@ -88,6 +88,7 @@ SIGNATURES = {
     "cbx_lock_any": (_I, [_P]),
     "cbx_merge": (_I, [_P, _I, _IP]),
     "cbx_synchronise": (_I, [_P, _I, _I, _I, _I]),
+    "cbx_synchronise_staged": (_I, [_P, _I, _I, _I, _I]),
     "cbx_unlock_any": (_I, [_P]),
     "cbx_checkpoint_model": (_I, [_P, _CP]),
     "cbx_override_model_data": (_I, [_P, _CP]),

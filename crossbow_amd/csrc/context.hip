@@ -178,6 +178,15 @@ struct Device {
   int g = 0;  // global device index
   hipStream_t stream = nullptr;       // model synchronisation stream (kernels)
   hipStream_t comm_stream = nullptr;  // RCCL all-reduce of the bucketed pipeline (G > 1)
+  // Pipelined host-staged step (cbx_synchronise_staged): pinned H2D and D2H
+  // run on their own streams (separate DMA engines, both PCIe directions at
+  // once) beside the kernels on `stream`.  Created on first use.
+  hipStream_t h2d_stream = nullptr;
+  hipStream_t d2h_stream = nullptr;
+  hipEvent_t stage_entry = nullptr;       // sync stream -> h2d stream at entry
+  hipEvent_t stage_done = nullptr;        // d2h stream -> sync stream at exit
+  std::vector<hipEvent_t> stage_h2d;      // per bucket: inputs landed
+  std::vector<hipEvent_t> stage_k;        // per bucket: outputs computed
   std::vector<hipEvent_t> bucket_acc;  // per bucket: kernel A done (stream -> comm_stream)
   std::vector<hipEvent_t> bucket_red;  // per bucket: all-reduce done (comm_stream -> stream)
   ncclComm_t comm = nullptr;
@@ -397,6 +406,14 @@ void close_device(Device &d) {
   for (hipEvent_t e : d.ring) (void)hipEventDestroy(e);
   for (hipEvent_t e : d.bucket_acc) (void)hipEventDestroy(e);
   for (hipEvent_t e : d.bucket_red) (void)hipEventDestroy(e);
+  for (hipStream_t st : {d.h2d_stream, d.d2h_stream})
+    if (st) (void)hipStreamSynchronize(st);
+  for (hipEvent_t e : d.stage_h2d) (void)hipEventDestroy(e);
+  for (hipEvent_t e : d.stage_k) (void)hipEventDestroy(e);
+  if (d.stage_entry) (void)hipEventDestroy(d.stage_entry);
+  if (d.stage_done) (void)hipEventDestroy(d.stage_done);
+  if (d.h2d_stream) (void)hipStreamDestroy(d.h2d_stream);
+  if (d.d2h_stream) (void)hipStreamDestroy(d.d2h_stream);
   if (d.stream) (void)hipStreamDestroy(d.stream);
   if (d.comm_stream) (void)hipStreamDestroy(d.comm_stream);
   d = Device();
@@ -505,6 +522,17 @@ int finish_step(cbx_context *c) {
   return CBX_OK;
 }
 
+// cbx_set_force_split at G = 1: the split pipeline runs over a one-rank
+// communicator so a single-GPU host exercises kernel A + RCCL + kernel B.
+int ensure_one_rank_comm(cbx_context *c) {
+  if (c->G != 1 || !c->force_split || c->devs[0].comm != nullptr) return CBX_OK;
+  Device &d = c->devs[0];
+  HIP_TRY(hipSetDevice(d.hip_id));
+  int dev = d.hip_id;
+  NCCL_TRY(ncclCommInitAll(&d.comm, 1, &dev));
+  return CBX_OK;
+}
+
 int sma_step(cbx_context *c, int first) {
   const bool mom = c->has_last && c->model.conf.momentum > 0;  // sma.c:150 (base conf)
   std::vector<cbx::SmaArgs> args(c->devs.size());
@@ -515,12 +543,7 @@ int sma_step(cbx_context *c, int first) {
     copies_total += cp;
   }
 
-  if (c->G == 1 && c->force_split && c->devs[0].comm == nullptr) {
-    Device &d = c->devs[0];
-    HIP_TRY(hipSetDevice(d.hip_id));
-    int dev = d.hip_id;
-    NCCL_TRY(ncclCommInitAll(&d.comm, 1, &dev));
-  }
+  TRY(ensure_one_rank_comm(c));
   if (c->G == 1 && !c->force_split) {
     // Single GPU: Phase B is the identity, so A + C (+ D) fuse into one pass.
     // (sma.c:63 waits on base->updated; every producer of z is this stream,
@@ -659,6 +682,170 @@ int sma_step(cbx_context *c, int first) {
     for (int id : d.replicas) {
       if (id < first || !c->locked[id]) continue;
       c->replicas[id]->conf.copy = 0;  // sma.c:220 (a no-op unless a copy happened)
+    }
+  return CBX_OK;
+}
+
+// ---------------------------------------------------------------------------
+// Host-staged SMA step, pipelined (cbx_synchronise_staged).  Same result as
+// cbx_stage_in + cbx_synchronise + cbx_stage_out, bit for bit (every phase is
+// elementwise, and the all-reduce of a bucket sums the same elements), but the
+// flat buffers are cut into `nb` buckets and, per device,
+//   h2d_stream : H2D(0) H2D(1) H2D(2) ...
+//   stream     :   [h2d 0] K(0) [h2d 1] K(1) ...
+//   d2h_stream :            [k 0] D2H(0)   [k 1] D2H(1) ...
+// so the PCIe uploads of bucket k+1 and the downloads of bucket k-1 run at
+// the same time (PCIe is full duplex; separate DMA engines) and the step
+// costs about max(H2D, D2H) instead of their sum.  K(b) is the fused kernel
+// at G = 1, else kernel A + RCCL all-reduce + kernel B of the bucket, in
+// order on the sync stream (bucket 0 carries the control block, so every
+// later kernel B sees the Phase-D decision).
+// ---------------------------------------------------------------------------
+int alloc_host_mirror(cbx_context *c);
+
+int ensure_stage_streams(Device &d, int64_t nb) {
+  if (!d.h2d_stream) {
+    HIP_TRY(hipStreamCreateWithFlags(&d.h2d_stream, hipStreamNonBlocking));
+    HIP_TRY(hipStreamCreateWithFlags(&d.d2h_stream, hipStreamNonBlocking));
+    HIP_TRY(hipEventCreateWithFlags(&d.stage_entry, hipEventDisableTiming));
+    HIP_TRY(hipEventCreateWithFlags(&d.stage_done, hipEventDisableTiming));
+  }
+  while ((int64_t)d.stage_h2d.size() < nb) {
+    hipEvent_t a, b;
+    HIP_TRY(hipEventCreateWithFlags(&a, hipEventDisableTiming));
+    HIP_TRY(hipEventCreateWithFlags(&b, hipEventDisableTiming));
+    d.stage_h2d.push_back(a);
+    d.stage_k.push_back(b);
+  }
+  return CBX_OK;
+}
+
+// Copy floats [start4*4, start4*4 + len4*4) of one buffer, clipped to the
+// model's n elements (the device pad beyond n stays zero and never travels).
+int stage_range(cbx_context *c, void *dst, const void *src, int64_t start4, int64_t len4, hipMemcpyKind kind,
+                hipStream_t st) {
+  const int64_t lo = start4 * 4, hi = std::min<int64_t>((start4 + len4) * 4, c->n);
+  if (hi <= lo) return CBX_OK;
+  HIP_TRY(hipMemcpyAsync(static_cast<float *>(dst) + lo, static_cast<const float *>(src) + lo,
+                         (size_t)(hi - lo) * sizeof(float), kind, st));
+  return CBX_OK;
+}
+
+int sma_step_staged(cbx_context *c, int first, int buckets) {
+  const bool mom = c->has_last && c->model.conf.momentum > 0;  // sma.c:150
+  std::vector<cbx::SmaArgs> args(c->devs.size());
+  int copies_total = 0;
+  for (size_t k = 0; k < c->devs.size(); ++k) {
+    int cp = 0;
+    TRY(build_args(c, c->devs[k], first, args[k], &cp));
+    copies_total += cp;
+  }
+  TRY(ensure_one_rank_comm(c));
+  TRY(alloc_host_mirror(c));
+  const bool fused = c->G == 1 && !c->force_split;
+  const int64_t pad = cbx::kPadFloat4;
+  int64_t b4 = ((c->n4 / buckets + pad - 1) / pad) * pad;
+  if (b4 <= 0 || b4 > c->n4) b4 = c->n4;
+  const int64_t nb = (c->n4 + b4 - 1) / b4;
+
+  for (Device &d : c->devs) {
+    HIP_TRY(hipSetDevice(d.hip_id));
+    TRY(ensure_stage_streams(d, nb));
+    TRY(mark(c, d, EV_START));
+    HIP_TRY(hipEventRecord(d.stage_entry, d.stream));  // everything enqueued before this call
+    HIP_TRY(hipStreamWaitEvent(d.h2d_stream, d.stage_entry, 0));
+    if (c->timing) {
+      HIP_TRY(hipEventRecord(d.ev[EV_H2D0], d.h2d_stream));
+      d.ev_valid[EV_H2D0] = true;
+    }
+  }
+  for (int64_t b = 0; b < nb; ++b) {
+    const int64_t s4 = b * b4, l4 = std::min(b4, c->n4 - s4);
+    // inputs: z, last, s_i, w_i (cbx_stage_in's set)
+    for (Device &d : c->devs) {
+      HIP_TRY(hipSetDevice(d.hip_id));
+      const auto H2D = hipMemcpyHostToDevice;
+      TRY(stage_range(c, base_dev(c, d, CBX_BUF_DATA), base_host(d, CBX_BUF_DATA), s4, l4, H2D, d.h2d_stream));
+      if (c->has_last)
+        TRY(stage_range(c, base_dev(c, d, CBX_BUF_LAST), base_host(d, CBX_BUF_LAST), s4, l4, H2D, d.h2d_stream));
+      for (int id : d.replicas) {
+        Replica &r = *c->replicas[id];
+        TRY(stage_range(c, replica_dev(d, r, CBX_BUF_DIFF), replica_host(d, r, CBX_BUF_DIFF), s4, l4, H2D, d.h2d_stream));
+        TRY(stage_range(c, replica_dev(d, r, CBX_BUF_DATA), replica_host(d, r, CBX_BUF_DATA), s4, l4, H2D, d.h2d_stream));
+      }
+      HIP_TRY(hipEventRecord(d.stage_h2d[b], d.h2d_stream));
+      HIP_TRY(hipStreamWaitEvent(d.stream, d.stage_h2d[b], 0));
+    }
+    // compute the bucket on every device's sync stream
+    for (size_t k = 0; k < c->devs.size(); ++k) {
+      Device &d = c->devs[k];
+      HIP_TRY(hipSetDevice(d.hip_id));
+      cbx::LaunchConfig cfg = c->cfg;
+      cfg.num_cus = d.num_cus;
+      const cbx::SmaArgs a = offset_args(args[k], s4, l4);
+      if (fused) HIP_TRY(cbx::launch_sma_fused(a, mom, copies_total > 0, cfg, d.stream));
+      else HIP_TRY(cbx::launch_sma_accumulate(a, b == 0, cfg, d.stream));
+    }
+    if (!fused) {
+      NCCL_TRY(ncclGroupStart());
+      for (Device &d : c->devs) {
+        HIP_TRY(hipSetDevice(d.hip_id));
+        const float *src = base_dev(c, d, CBX_BUF_GRADIENT) + s4 * 4;
+        float *dst = base_dev(c, d, CBX_BUF_DIFF) + s4 * 4;
+        size_t count = (size_t)l4 * 4;
+        if (b == 0) {  // the control block rides with bucket 0 (common.c:45-52 + sma.c:113-120)
+          src -= cbx::kCtrlFloats;
+          dst -= cbx::kCtrlFloats;
+          count += cbx::kCtrlFloats;
+        }
+        NCCL_TRY(ncclAllReduce(src, dst, count, ncclFloat, ncclSum, d.comm, d.stream));
+      }
+      NCCL_TRY(ncclGroupEnd());
+      for (size_t k = 0; k < c->devs.size(); ++k) {
+        Device &d = c->devs[k];
+        HIP_TRY(hipSetDevice(d.hip_id));
+        cbx::LaunchConfig cfg = c->cfg;
+        cfg.num_cus = d.num_cus;
+        HIP_TRY(cbx::launch_sma_apply(offset_args(args[k], s4, l4), mom, cfg, d.stream));
+      }
+    }
+    // outputs: z, last, w_i (cbx_stage_out's set)
+    for (Device &d : c->devs) {
+      HIP_TRY(hipSetDevice(d.hip_id));
+      HIP_TRY(hipEventRecord(d.stage_k[b], d.stream));
+      HIP_TRY(hipStreamWaitEvent(d.d2h_stream, d.stage_k[b], 0));
+      if (b == 0 && c->timing) {
+        HIP_TRY(hipEventRecord(d.ev[EV_D2H0], d.d2h_stream));
+        d.ev_valid[EV_D2H0] = true;
+      }
+      const auto D2H = hipMemcpyDeviceToHost;
+      TRY(stage_range(c, base_host(d, CBX_BUF_DATA), base_dev(c, d, CBX_BUF_DATA), s4, l4, D2H, d.d2h_stream));
+      if (c->has_last)
+        TRY(stage_range(c, base_host(d, CBX_BUF_LAST), base_dev(c, d, CBX_BUF_LAST), s4, l4, D2H, d.d2h_stream));
+      for (int id : d.replicas) {
+        Replica &r = *c->replicas[id];
+        TRY(stage_range(c, replica_host(d, r, CBX_BUF_DATA), replica_dev(d, r, CBX_BUF_DATA), s4, l4, D2H, d.d2h_stream));
+      }
+    }
+  }
+  for (Device &d : c->devs) {
+    HIP_TRY(hipSetDevice(d.hip_id));
+    if (c->timing) {
+      HIP_TRY(hipEventRecord(d.ev[EV_H2D1], d.h2d_stream));
+      HIP_TRY(hipEventRecord(d.ev[EV_D2H1], d.d2h_stream));
+      d.ev_valid[EV_H2D1] = d.ev_valid[EV_D2H1] = true;
+    }
+    HIP_TRY(hipEventRecord(d.stage_done, d.d2h_stream));
+    HIP_TRY(hipStreamWaitEvent(d.stream, d.stage_done, 0));
+    TRY(mark(c, d, EV_B));
+    ring_advance(c, d, 2);
+  }
+  c->last_step_split = !fused;
+  TRY(finish_step(c));
+  for (Device &d : c->devs)
+    for (int id : d.replicas) {
+      if (id < first || !c->locked[id]) continue;
+      c->replicas[id]->conf.copy = 0;  // sma.c:220
     }
   return CBX_OK;
 }
@@ -1194,8 +1381,9 @@ int cbx_merge(cbx_context *c, int pull, int *first_out) {
   return CBX_OK;
 }
 
-int cbx_synchronise(cbx_context *c, int first, int clock, int autotune, int push) {
-  (void)push;
+// staged: 0 = device-resident step; > 0 = host-staged step over that many
+// buckets (cbx_synchronise_staged).
+static int synchronise_impl(cbx_context *c, int first, int clock, int autotune, int staged) {
   TRY(check_manager(c));
   if (first < 0 || first > c->size) return fail(CBX_ERR_INVALID, "first replica %d out of range", first);
   // executioncontext.c:2287-2315: SYNCHRONOUSEAMSGD (3) routes to SMA because
@@ -1205,9 +1393,11 @@ int cbx_synchronise(cbx_context *c, int first, int clock, int autotune, int push
   // the base-model buffers and the all-reduce.
   const int type = c->model.type;
   if (type == CBX_UPDATE_WORKER) {
+    if (staged) TRY(cbx_stage_in(c));
     TRY(ssgd_step(c, first));
+    if (staged) TRY(cbx_stage_out(c));
   } else if (type == CBX_UPDATE_SMA || type == CBX_UPDATE_SYNCHRONOUSEAMSGD) {
-    TRY(sma_step(c, first));
+    TRY(staged ? sma_step_staged(c, first, staged) : sma_step(c, first));
   } else {
     return fail(CBX_ERR_UNSUPPORTED, "update model %d is not on this library's path (SMA, SYNCHRONOUSEAMSGD, WORKER)", type);
   }
@@ -1220,6 +1410,17 @@ int cbx_synchronise(cbx_context *c, int first, int clock, int autotune, int push
       c->replicas[i]->updates = 0;
     }
   return CBX_OK;
+}
+
+int cbx_synchronise(cbx_context *c, int first, int clock, int autotune, int push) {
+  // push is unused by the reference too (executioncontext.c:2264).
+  (void)push;
+  return synchronise_impl(c, first, clock, autotune, 0);
+}
+
+int cbx_synchronise_staged(cbx_context *c, int first, int clock, int autotune, int buckets) {
+  if (buckets < 1 || buckets > 4096) return fail(CBX_ERR_INVALID, "staged buckets must be 1..4096, got %d", buckets);
+  return synchronise_impl(c, first, clock, autotune, buckets);
 }
 
 int cbx_unlock_any(cbx_context *c) {

@@ -150,6 +150,12 @@ class TheGPU:
     def synchronise(self, first: int, clock: int, autotune: int, push: bool) -> int:
         return check(self._L.cbx_synchronise(self._ctx, first, clock, autotune, 1 if push else 0))
 
+    def synchronise_staged(self, first: int, clock: int, autotune: int = 0, buckets: int = 8) -> int:
+        """stage_in + synchronise + stage_out in one call, pipelined over
+        `buckets` so uploads, kernels and downloads overlap (host mirrors
+        in, host mirrors out; include/crossbow_sma.h)."""
+        return check(self._L.cbx_synchronise_staged(self._ctx, first, clock, autotune, buckets))
+
     def unlockAny(self) -> int:
         return check(self._L.cbx_unlock_any(self._ctx))
 

@@ -134,6 +134,17 @@ int cbx_merge (cbx_context *ctx, int pull, int *first);
  * synchronous-SGD barrier (synch/synchronoussgd.c:13-106, needs the work
  * per clock); any other is CBX_ERR_UNSUPPORTED.                          */
 int cbx_synchronise (cbx_context *ctx, int first, int clock, int autotune, int push);
+/* The same step for a model manager whose buffers live in host memory
+ * (north_star: "starts and ends in host memory", databuffer.c:95-122):
+ * result-identical to cbx_stage_in + cbx_synchronise + cbx_stage_out, but
+ * the flat buffers are cut into `buckets` (1..4096) and the pinned H2D of
+ * bucket k+1 and the D2H of bucket k-1 run beside the kernels of bucket k
+ * on their own streams, so the step costs about max(H2D, D2H) of PCIe time
+ * instead of the sum.  Async like cbx_synchronise; cbx_wait / the step
+ * event cover the downloads.  The reference has no such call (its `push`
+ * argument is unused, executioncontext.c:2264); update model WORKER runs
+ * the three calls unpipelined.                                            */
+int cbx_synchronise_staged (cbx_context *ctx, int first, int clock, int autotune, int buckets);
 /* TheGPU.unlockAny() GPU.c:1142-1149 -> modelmanager.c:233-245           */
 int cbx_unlock_any (cbx_context *ctx);
 
@@ -234,9 +245,9 @@ int cbx_step_event (cbx_context *ctx, int local, void **event);
 #define CBX_T_KERNEL    0   /* fused kernel, or kernel A (G > 1)       */
 #define CBX_T_ALLREDUCE 1   /* RCCL all-reduce (G > 1)                 */
 #define CBX_T_APPLY     2   /* kernel B (G > 1)                        */
-#define CBX_T_STEP      3   /* whole synchronise() on the device       */
-#define CBX_T_H2D       4   /* last cbx_stage_in                       */
-#define CBX_T_D2H       5   /* last cbx_stage_out                      */
+#define CBX_T_STEP      3   /* whole synchronise() on the device (staged: incl. copies) */
+#define CBX_T_H2D       4   /* last cbx_stage_in, or uploads of the last staged step   */
+#define CBX_T_D2H       5   /* last cbx_stage_out, or downloads of the last staged step */
 #define CBX_T_COUNT     6
 /* When enabled, HIP events bracket each launch on the sync stream.       */
 int cbx_set_timing (cbx_context *ctx, int enable);

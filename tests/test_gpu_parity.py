@@ -287,6 +287,53 @@ def test_staged_roundtrip():
         g.free()
 
 
+@pytest.mark.parametrize("n,buckets,split,copy_step", [
+    (4099, 1, False, None), (4099, 7, False, 1), (300_001, 16, False, None), (300_001, 4096, False, 0),
+    (300_001, 5, True, None), (300_001, 16, True, 1), (1_111_946, 16, False, None),
+])
+def test_staged_pipelined(n, buckets, split, copy_step):
+    # cbx_synchronise_staged: host mirrors in, host mirrors out, uploads /
+    # kernels / downloads overlapped per bucket.  Two steps back to back: the
+    # second uploads what the first downloaded.  Bit-exact with the oracle.
+    from crossbow_amd import BUF_DATA, BUF_DIFF, BUF_LAST
+    R = 4
+    st = O.make_state(n, 1, R, 0.1, 0.9)
+    g = make_gpu(n, R, 0.1, 0.9)
+    try:
+        if split:
+            g.set_force_split(True)
+        g.base_host_view(0, BUF_DATA)[:] = st.z[0]
+        g.base_host_view(0, BUF_LAST)[:] = st.last[0]
+        for i in range(R):
+            g.replica_host_view(i, BUF_DIFF)[:] = st.s[i]
+            g.replica_host_view(i, BUF_DATA)[:] = st.w[i]
+        g.set_timing(True)
+        want = st.clone()
+        for step in range(2):
+            if copy_step == step:
+                g.set_replica_copy(1, True)
+                want.copy[1] = 1
+            g.lockAny()
+            g.synchronise_staged(0, step + 1, 0, buckets)
+            g.unlockAny()
+            O.sma_step(want)
+        g.wait()
+        t = g.last_timing(0)
+        assert t[3] > 0 and t[4] > 0 and t[5] > 0, t
+        assert t[3] >= max(t[4], t[5]) * 0.99, "the step span covers uploads and downloads"
+        assert_bitexact(g.base_host_view(0, BUF_DATA), want.z[0], "z staged out")
+        assert_bitexact(g.base_host_view(0, BUF_LAST), want.last[0], "last staged out")
+        for i in range(R):
+            assert_bitexact(g.replica_host_view(i, BUF_DATA), want.w[i], f"w[{i}] staged out")
+            assert_bitexact(g.replica_host_view(i, BUF_DIFF), st.s[i], f"s[{i}] host mirror untouched")
+        # the device copy equals the host copy after the step
+        assert_bitexact(g.base_read(0, BUF_DATA), want.z[0], "z on device")
+        if copy_step is not None:
+            assert g.replica_copy(1) == 0
+    finally:
+        g.free()
+
+
 def test_resnet50_full_size_sampled_parity_and_conservation():
     """C3 at full size (n = 25,557,032, R = 8, mu = 0.9): the step is elementwise,
     so the oracle run on a random sample of element positions must match the
