@@ -179,6 +179,14 @@ NATIVE(jint, synchronise) (JNIEnv *env, jobject obj, jint first, jint clock, jin
 	return fatal_or (cbx_synchronise (theGPU, first, clock, autotune, push == JNI_TRUE ? 1 : 0));
 }
 
+/* Not in the reference: the pipelined host-staged step (cbx_synchronise_staged).
+ * Java side: `public native int synchroniseStaged (int first, int clock,
+ * int autotune, int buckets);` next to synchronise (TheGPU.java:346). */
+NATIVE(jint, synchroniseStaged) (JNIEnv *env, jobject obj, jint first, jint clock, jint autotune, jint buckets) {
+	(void) env; (void) obj;
+	return fatal_or (cbx_synchronise_staged (theGPU, first, clock, autotune, buckets));
+}
+
 NATIVE(jint, unlockAny) (JNIEnv *env, jobject obj) {
 	(void) env; (void) obj;
 	return fatal_or (cbx_unlock_any (theGPU));
