@@ -81,7 +81,10 @@ inline unsigned lds_for_occupancy(const LaunchConfig &cfg, int reads, unsigned g
   if (cap <= 0) return 0;
   int wgs_per_cu = cap / waves_per_wg;
   if (wgs_per_cu < 1) wgs_per_cu = 1;
-  unsigned per = (160u * 1024u / (unsigned)wgs_per_cu) / 1024u * 1024u;
+  // The least LDS that still keeps a (wgs+1)-th workgroup out: the rest of
+  // the CU's LDS stays free for kernels running beside this one (the RCCL
+  // all-reduce on the comm stream of the G > 1 pipeline).
+  unsigned per = (160u / (unsigned)(wgs_per_cu + 1) + 1u) * 1024u;
   if (per > 64u * 1024u) per = 64u * 1024u;
   return per;
 }
