@@ -240,6 +240,8 @@ struct cbx_context {
   unsigned long long version = 0;
   bool timing = false;
   cbx::LaunchConfig cfg;
+  // Optimiser step and S-SGD kernels (one float4 stream per buffer, few reads).
+  cbx::LaunchConfig aux_cfg = cbx::aux_launch_config();
   int64_t bucket_elems = 0;
   bool force_split = false;
   bool last_step_split = false;
@@ -903,7 +905,7 @@ int ssgd_step(cbx_context *c, int first) {
   for (size_t k = 0; k < c->devs.size(); ++k) {
     Device &d = c->devs[k];
     HIP_TRY(hipSetDevice(d.hip_id));
-    cbx::LaunchConfig cfg = c->cfg;
+    cbx::LaunchConfig cfg = c->aux_cfg;
     cfg.num_cus = d.num_cus;
     cbx::Timing t;
     if (!split) t.start = ring_event(c, d, EV_START);
@@ -1602,7 +1604,7 @@ static int ssgd_worker_step(cbx_context *c, Replica &r, Device &d, int task, hip
     HIP_TRY(hipEventRecord(r.client, st));
     HIP_TRY(hipStreamWaitEvent(d.stream, r.client, 0));
   }
-  cbx::LaunchConfig cfg = c->cfg;
+  cbx::LaunchConfig cfg = c->aux_cfg;
   cfg.num_cus = d.num_cus;
   cfg.blocks_per_cu = 0;
   HIP_TRY(cbx::launch_ssgd_accumulate(a, cfg, d.stream, {}));
@@ -1637,7 +1639,7 @@ int cbx_replica_optimise(cbx_context *c, int id, int task, void *stream) {
   a.wd = conf.weightDecay;
   HIP_TRY(hipSetDevice(d.hip_id));
   hipStream_t st = stream ? reinterpret_cast<hipStream_t>(stream) : d.stream;
-  cbx::LaunchConfig cfg = c->cfg;
+  cbx::LaunchConfig cfg = c->aux_cfg;
   cfg.num_cus = d.num_cus;
   cfg.blocks_per_cu = 0;
   // The replica must not be updated while the last synchronise() still uses
@@ -2039,6 +2041,19 @@ int cbx_set_kernel_occupancy(cbx_context *c, int waves_per_cu) {
   TRY(check_ctx(c));
   if (waves_per_cu < -1 || waves_per_cu > 32) return fail(CBX_ERR_INVALID, "waves per CU must be -1 (auto) or 0..32");
   c->cfg.waves_per_cu = waves_per_cu;
+  return CBX_OK;
+}
+
+int cbx_set_aux_kernel_config(cbx_context *c, int block, int unroll, int waves_per_cu) {
+  TRY(check_ctx(c));
+  if (block < 64 || block > 512 || block % 64 != 0) return fail(CBX_ERR_INVALID, "block must be 64..512, multiple of 64");
+  if (unroll != 1 && unroll != 2) return fail(CBX_ERR_INVALID, "unroll must be 1 or 2");
+  if ((int64_t)block * unroll > cbx::kPadFloat4 || cbx::kPadFloat4 % ((int64_t)block * unroll) != 0)
+    return fail(CBX_ERR_INVALID, "block*unroll must divide %lld", (long long)cbx::kPadFloat4);
+  if (waves_per_cu < -1 || waves_per_cu > 32) return fail(CBX_ERR_INVALID, "waves per CU must be -1 (auto) or 0..32");
+  c->aux_cfg.block = block;
+  c->aux_cfg.unroll = unroll;
+  c->aux_cfg.waves_per_cu = waves_per_cu;
   return CBX_OK;
 }
 

@@ -54,18 +54,32 @@ struct LaunchConfig {
   int num_cus = 256;
   // Occupancy cap, in waves per CU: 0 = none, -1 = auto (below).  Enforced
   // by reserving dynamic LDS per workgroup so that only that many waves fit.
-  // Fewer concurrent waves keep fewer DRAM pages open: the SMA kernels run
-  // fastest with about kReadStreamsPerCU read streams in flight per CU
-  // (scripts/occupancy_sweep.py, profiles/r01/occupancy.json).
+  // Fewer concurrent waves keep fewer DRAM pages open: every streaming kernel
+  // here runs fastest with about kStreamsPerCU buffer streams (reads plus
+  // writes, one float4 per lane each) in flight per CU
+  // (scripts/occupancy_sweep.py, scripts/aux_sweep.py, profiles/r01/).
   int waves_per_cu = -1;
 };
 
-constexpr int kReadStreamsPerCU = 36;
+constexpr int kStreamsPerCU = 56;
 
-// Waves per CU for a kernel whose lanes read `reads` streams each.
-inline int auto_waves_per_cu(int reads) {
-  if (reads < 1) reads = 1;
-  int w = (kReadStreamsPerCU + reads / 2) / reads;
+// The optimiser-step and S-SGD kernels: one-wave workgroups, one float4 per
+// lane, auto occupancy (scripts/aux_sweep.py).
+inline LaunchConfig aux_launch_config() {
+  LaunchConfig c;
+  c.block = 64;
+  c.unroll = 1;
+  c.waves_per_cu = -1;
+  return c;
+}
+
+// Waves per CU for a kernel whose lanes stream `reads` + `writes` buffers:
+// 2 for the R = 8 SMA step (18 + 10), 8 for the optimiser step (3 + 4),
+// 11 for kernel B (3 + 2).
+inline int auto_waves_per_cu(int reads, int writes) {
+  int streams = reads + writes;
+  if (streams < 1) streams = 1;
+  int w = (kStreamsPerCU + streams / 2) / streams;
   return w < 2 ? 2 : (w > 12 ? 12 : w);
 }
 
@@ -74,10 +88,10 @@ inline int auto_waves_per_cu(int reads) {
 // In auto mode a launch too small to fill the chip many times over (under
 // 16 waves per CU, e.g. LeNet's 4 MB buffers) is latency-bound and runs
 // uncapped.
-inline unsigned lds_for_occupancy(const LaunchConfig &cfg, int reads, unsigned grid) {
+inline unsigned lds_for_occupancy(const LaunchConfig &cfg, int reads, int writes, unsigned grid) {
   const int waves_per_wg = (cfg.block + 63) / 64;
   if (cfg.waves_per_cu < 0 && (int64_t)grid * waves_per_wg < 16ll * cfg.num_cus) return 0;
-  const int cap = cfg.waves_per_cu < 0 ? auto_waves_per_cu(reads) : cfg.waves_per_cu;
+  const int cap = cfg.waves_per_cu < 0 ? auto_waves_per_cu(reads, writes) : cfg.waves_per_cu;
   if (cap <= 0) return 0;
   int wgs_per_cu = cap / waves_per_wg;
   if (wgs_per_cu < 1) wgs_per_cu = 1;

@@ -264,29 +264,36 @@ __global__ __launch_bounds__(256) void sma_apply_kernel(const SmaArgs a) {
 //   s = w                                :71 / :87
 //   w = fma(1, g, w)  or  fma(rate, g, w) without momentum  :74 / :90
 // ---------------------------------------------------------------------------
-template <bool MOM, bool WD, int P>
+template <bool MOM, bool WD, int P, int U>
 __global__ __launch_bounds__(512) void sma_optimise_kernel(const OptArgs a) {
-  const uint32_t trip = gridDim.x * blockDim.x;
+  const uint32_t trip = gridDim.x * blockDim.x * U;
   const uint32_t n4 = (uint32_t)a.n4;
   const v4f rate = a.rate, mu = a.momentum, wd = a.wd, one = 1.0f;
-  for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < n4; e += trip) {
-    const uint32_t i = e * 16u;
-    const v4f w = ldo<P>(a.w, i);
-    v4f g = ldo<P>(a.g, i);
-    v4f l;
-    if constexpr (MOM) l = ldo<P>(a.last, i);
+  for (uint32_t base = first_elem<U>(); base < n4; base += trip) {
+    v4f w[U], g[U], l[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t i = (base + u * 64u) * 16u;
+      w[u] = ldo<P>(a.w, i);
+      g[u] = ldo<P>(a.g, i);
+      if constexpr (MOM) l[u] = ldo<P>(a.last, i);
+    }
     __builtin_amdgcn_sched_barrier(0);
-    if constexpr (WD) g = vfma(wd, w, g);
-    sto<P>(a.s, i, w);
-    if constexpr (MOM) {
-      g = rate * g;
-      g = vfma(mu, l, g);
-      sto<P>(a.last, i, g);
-      sto<P>(a.w, i, vfma(one, g, w));
-      sto<P>(a.g, i, g);
-    } else {
-      sto<P>(a.w, i, vfma(rate, g, w));
-      if constexpr (WD) sto<P>(a.g, i, g);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t i = (base + u * 64u) * 16u;
+      if constexpr (WD) g[u] = vfma(wd, w[u], g[u]);
+      sto<P>(a.s, i, w[u]);
+      if constexpr (MOM) {
+        g[u] = rate * g[u];
+        g[u] = vfma(mu, l[u], g[u]);
+        sto<P>(a.last, i, g[u]);
+        sto<P>(a.w, i, vfma(one, g[u], w[u]));
+        sto<P>(a.g, i, g[u]);
+      } else {
+        sto<P>(a.w, i, vfma(rate, g[u], w[u]));
+        if constexpr (WD) sto<P>(a.g, i, g[u]);
+      }
     }
   }
 }
@@ -298,23 +305,30 @@ __global__ __launch_bounds__(512) void sma_optimise_kernel(const OptArgs a) {
 //   acc = fma(rate, g, acc)  :46-52
 // Reads g, acc (, w) and writes acc (, g): 12n B (+8n with weight decay).
 // ---------------------------------------------------------------------------
-template <bool WD, int P>
+template <bool WD, int P, int U>
 __global__ __launch_bounds__(512) void ssgd_accumulate_kernel(const SsgdArgs a) {
-  const uint32_t trip = gridDim.x * blockDim.x;
+  const uint32_t trip = gridDim.x * blockDim.x * U;
   const uint32_t n4 = (uint32_t)a.n4;
   const v4f rate = a.rate, wd = a.wd;
-  for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < n4; e += trip) {
-    const uint32_t i = e * 16u;
-    v4f g = ldo<P>(a.g, i);
-    const v4f acc = ldo<P>(a.acc, i);
-    v4f w;
-    if constexpr (WD) w = ldo<P>(a.wsrc, i);
-    __builtin_amdgcn_sched_barrier(0);
-    if constexpr (WD) {
-      g = vfma(wd, w, g);
-      sto<P>(a.g, i, g);
+  for (uint32_t base = first_elem<U>(); base < n4; base += trip) {
+    v4f g[U], acc[U], w[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t i = (base + u * 64u) * 16u;
+      g[u] = ldo<P>(a.g, i);
+      acc[u] = ldo<P>(a.acc, i);
+      if constexpr (WD) w[u] = ldo<P>(a.wsrc, i);
     }
-    sto<P>(a.acc, i, vfma(rate, g, acc));
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t i = (base + u * 64u) * 16u;
+      if constexpr (WD) {
+        g[u] = vfma(wd, w[u], g[u]);
+        sto<P>(a.g, i, g[u]);
+      }
+      sto<P>(a.acc, i, vfma(rate, g[u], acc[u]));
+    }
   }
 }
 
@@ -325,27 +339,37 @@ __global__ __launch_bounds__(512) void ssgd_accumulate_kernel(const SsgdArgs a) 
 //   acc = 0                           :103
 //   w_i = z for locked replicas       common.c:198-220
 // Reads D, z (, last) and writes z, acc, R x w (, last).
-template <bool MOM, int P>
+template <bool MOM, int P, int U>
 __global__ __launch_bounds__(512) void ssgd_apply_kernel(const SsgdArgs a) {
-  const uint32_t trip = gridDim.x * blockDim.x;
+  const uint32_t trip = gridDim.x * blockDim.x * U;
   const uint32_t n4 = (uint32_t)a.n4;
   const v4f ratio = a.ratio, mu = a.momentum, one = 1.0f, zero = 0.0f;
-  for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < n4; e += trip) {
-    const uint32_t i = e * 16u;
-    v4f D = ldo<P>(a.D, i);
-    v4f z = ldo<P>(a.z, i);
-    v4f l;
-    if constexpr (MOM) l = ldo<P>(a.last, i);
-    __builtin_amdgcn_sched_barrier(0);
-    D = ratio * D;
-    if constexpr (MOM) {
-      D = vfma(mu, l, D);
-      sto<P>(a.last, i, D);
+  for (uint32_t base = first_elem<U>(); base < n4; base += trip) {
+    v4f D[U], z[U], l[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t i = (base + u * 64u) * 16u;
+      D[u] = ldo<P>(a.D, i);
+      z[u] = ldo<P>(a.z, i);
+      if constexpr (MOM) l[u] = ldo<P>(a.last, i);
     }
-    z = vfma(one, D, z);
-    sto<P>(a.z, i, z);
-    sto<P>(a.acc, i, zero);
-    for (int r = 0; r < a.nrep; ++r) sto<P>(a.w[r], i, z);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t i = (base + u * 64u) * 16u;
+      D[u] = ratio * D[u];
+      if constexpr (MOM) {
+        D[u] = vfma(mu, l[u], D[u]);
+        sto<P>(a.last, i, D[u]);
+      }
+      z[u] = vfma(one, D[u], z[u]);
+      sto<P>(a.z, i, z[u]);
+      sto<P>(a.acc, i, zero);
+    }
+    for (int r = 0; r < a.nrep; ++r) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) sto<P>(a.w[r], (base + u * 64u) * 16u, z[u]);
+    }
   }
 }
 
@@ -400,10 +424,6 @@ __global__ __launch_bounds__(512) void copy_kernel(v4f *dst, const v4f *src, int
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) st<P>(dst + i, ld<P>(src + i));
 }
 
-// One-float4-per-lane kernels (optimiser step, S-SGD) run 128-thread blocks:
-// 6.0 TB/s measured for the optimiser step (profiles/r01).
-constexpr int kAuxBlock = 128;
-
 // Grid for a range of n4 float4s (a multiple of block*unroll).
 inline dim3 grid_for(int64_t n4, const LaunchConfig &cfg) {
   const int64_t per_block = (int64_t)cfg.block * cfg.unroll;
@@ -419,7 +439,7 @@ inline dim3 grid_for(int64_t n4, const LaunchConfig &cfg) {
 template <int R, bool MOM, bool COPY, int P>
 hipError_t fused_u(const SmaArgs &a, const LaunchConfig &cfg, hipStream_t s, Timing t) {
   const dim3 g = grid_for(a.n4, cfg);
-  const unsigned lds = lds_for_occupancy(cfg, (COPY ? 1 : 2) * a.nrep + 1 + (MOM ? 1 : 0), g.x);
+  const unsigned lds = lds_for_occupancy(cfg, (COPY ? 1 : 2) * a.nrep + 1 + (MOM ? 1 : 0), a.nrep + 1 + (MOM ? 1 : 0), g.x);
   if (cfg.unroll == 4)
     hipExtLaunchKernelGGL((sma_fused_kernel<R, MOM, COPY, P, 4>), g, dim3(cfg.block), lds, s, t.start, t.stop, 0, a);
   else if (cfg.unroll == 2)
@@ -448,7 +468,7 @@ hipError_t fused_r(const SmaArgs &a, const LaunchConfig &cfg, hipStream_t s, Tim
 template <int R, int P>
 hipError_t acc_u(const SmaArgs &a, const LaunchConfig &cfg, hipStream_t s, Timing t) {
   const dim3 g = grid_for(a.n4, cfg);
-  const unsigned lds = lds_for_occupancy(cfg, 2 * a.nrep + 1, g.x);
+  const unsigned lds = lds_for_occupancy(cfg, 2 * a.nrep + 1, a.nrep + 1, g.x);
   if (cfg.unroll == 4)
     hipExtLaunchKernelGGL((sma_accumulate_kernel<R, P, 4>), g, dim3(cfg.block), lds, s, t.start, t.stop, 0, a);
   else if (cfg.unroll == 2)
@@ -477,7 +497,7 @@ hipError_t acc_r(const SmaArgs &a, const LaunchConfig &cfg, hipStream_t s, Timin
 template <bool MOM, int P>
 hipError_t apply_u(const SmaArgs &a, const LaunchConfig &cfg, hipStream_t s, Timing t) {
   const dim3 g = grid_for(a.n4, cfg);
-  const unsigned lds = lds_for_occupancy(cfg, MOM ? 3 : 2, g.x);
+  const unsigned lds = lds_for_occupancy(cfg, MOM ? 3 : 2, MOM ? 2 : 1, g.x);
   if (cfg.unroll == 4)
     hipExtLaunchKernelGGL((sma_apply_kernel<MOM, P, 4>), g, dim3(cfg.block), lds, s, t.start, t.stop, 0, a);
   else if (cfg.unroll == 2)
@@ -512,67 +532,62 @@ hipError_t launch_sma_apply(const SmaArgs &a, bool momentum, const LaunchConfig 
   return momentum ? apply_u<true, 0>(a, cfg, stream, t) : apply_u<false, 0>(a, cfg, stream, t);
 }
 
+// Launch `K<..., U>` for the configured unroll (1 or 2) with the occupancy
+// cap for `reads` + `writes` buffer streams.
+#define CBX_LAUNCH_U(KERNEL, ...)                                                                        \
+  do {                                                                                                   \
+    const dim3 g_ = grid_for(a.n4, cfg);                                                                 \
+    const unsigned l_ = lds_for_occupancy(cfg, reads, writes, g_.x);                                             \
+    if (cfg.unroll == 2)                                                                                 \
+      hipExtLaunchKernelGGL((KERNEL<__VA_ARGS__, 2>), g_, dim3(cfg.block), l_, stream, t.start, t.stop, 0, a); \
+    else                                                                                                 \
+      hipExtLaunchKernelGGL((KERNEL<__VA_ARGS__, 1>), g_, dim3(cfg.block), l_, stream, t.start, t.stop, 0, a); \
+  } while (0)
+
+template <bool MOM, bool WD, int P>
+hipError_t optimise_p(const OptArgs &a, const LaunchConfig &cfg, hipStream_t stream, Timing t) {
+  const int reads = 2 + (MOM ? 1 : 0), writes = MOM ? 4 : (WD ? 3 : 2);
+  CBX_LAUNCH_U(sma_optimise_kernel, MOM, WD, P);
+  return hipGetLastError();
+}
+
 hipError_t launch_sma_optimise(const OptArgs &a, const LaunchConfig &cfg, hipStream_t stream, Timing t) {
-  LaunchConfig c = cfg;
-  c.unroll = 1;
-  c.block = kAuxBlock;
-  const dim3 g = grid_for(a.n4, c);
-  const dim3 b(c.block);
   const bool mom = a.momentum > 0.0f, wd = a.wd > 0.0f;
-  const unsigned l = lds_for_occupancy(c, mom ? 3 : 2, g.x);
   if (cfg.policy == 1) {
-    if (mom) {
-      if (wd) hipExtLaunchKernelGGL((sma_optimise_kernel<true, true, 1>), g, b, l, stream, t.start, t.stop, 0, a);
-      else hipExtLaunchKernelGGL((sma_optimise_kernel<true, false, 1>), g, b, l, stream, t.start, t.stop, 0, a);
-    } else {
-      if (wd) hipExtLaunchKernelGGL((sma_optimise_kernel<false, true, 1>), g, b, l, stream, t.start, t.stop, 0, a);
-      else hipExtLaunchKernelGGL((sma_optimise_kernel<false, false, 1>), g, b, l, stream, t.start, t.stop, 0, a);
-    }
-  } else {
-    if (mom) {
-      if (wd) hipExtLaunchKernelGGL((sma_optimise_kernel<true, true, 0>), g, b, l, stream, t.start, t.stop, 0, a);
-      else hipExtLaunchKernelGGL((sma_optimise_kernel<true, false, 0>), g, b, l, stream, t.start, t.stop, 0, a);
-    } else {
-      if (wd) hipExtLaunchKernelGGL((sma_optimise_kernel<false, true, 0>), g, b, l, stream, t.start, t.stop, 0, a);
-      else hipExtLaunchKernelGGL((sma_optimise_kernel<false, false, 0>), g, b, l, stream, t.start, t.stop, 0, a);
-    }
+    if (mom) return wd ? optimise_p<true, true, 1>(a, cfg, stream, t) : optimise_p<true, false, 1>(a, cfg, stream, t);
+    return wd ? optimise_p<false, true, 1>(a, cfg, stream, t) : optimise_p<false, false, 1>(a, cfg, stream, t);
   }
+  if (mom) return wd ? optimise_p<true, true, 0>(a, cfg, stream, t) : optimise_p<true, false, 0>(a, cfg, stream, t);
+  return wd ? optimise_p<false, true, 0>(a, cfg, stream, t) : optimise_p<false, false, 0>(a, cfg, stream, t);
+}
+
+template <bool WD, int P>
+hipError_t ssgd_acc_p(const SsgdArgs &a, const LaunchConfig &cfg, hipStream_t stream, Timing t) {
+  const int reads = 2 + (WD ? 1 : 0), writes = 1 + (WD ? 1 : 0);
+  CBX_LAUNCH_U(ssgd_accumulate_kernel, WD, P);
   return hipGetLastError();
 }
 
 hipError_t launch_ssgd_accumulate(const SsgdArgs &a, const LaunchConfig &cfg, hipStream_t stream, Timing t) {
-  LaunchConfig c = cfg;
-  c.unroll = 1;
-  c.block = kAuxBlock;
-  const dim3 g = grid_for(a.n4, c);
-  const dim3 b(c.block);
   const bool wd = a.wd > 0.0f;
-  if (cfg.policy == 1) {
-    if (wd) hipExtLaunchKernelGGL((ssgd_accumulate_kernel<true, 1>), g, b, 0, stream, t.start, t.stop, 0, a);
-    else hipExtLaunchKernelGGL((ssgd_accumulate_kernel<false, 1>), g, b, 0, stream, t.start, t.stop, 0, a);
-  } else {
-    if (wd) hipExtLaunchKernelGGL((ssgd_accumulate_kernel<true, 0>), g, b, 0, stream, t.start, t.stop, 0, a);
-    else hipExtLaunchKernelGGL((ssgd_accumulate_kernel<false, 0>), g, b, 0, stream, t.start, t.stop, 0, a);
-  }
+  if (cfg.policy == 1) return wd ? ssgd_acc_p<true, 1>(a, cfg, stream, t) : ssgd_acc_p<false, 1>(a, cfg, stream, t);
+  return wd ? ssgd_acc_p<true, 0>(a, cfg, stream, t) : ssgd_acc_p<false, 0>(a, cfg, stream, t);
+}
+
+template <bool MOM, int P>
+hipError_t ssgd_apply_p(const SsgdArgs &a, const LaunchConfig &cfg, hipStream_t stream, Timing t) {
+  const int reads = 2 + (MOM ? 1 : 0), writes = 2 + (MOM ? 1 : 0) + a.nrep;
+  CBX_LAUNCH_U(ssgd_apply_kernel, MOM, P);
   return hipGetLastError();
 }
 
 hipError_t launch_ssgd_apply(const SsgdArgs &a, const LaunchConfig &cfg, hipStream_t stream, Timing t) {
-  LaunchConfig c = cfg;
-  c.unroll = 1;
-  c.block = kAuxBlock;
-  const dim3 g = grid_for(a.n4, c);
-  const dim3 b(c.block);
   const bool mom = a.momentum > 0.0f;
-  if (cfg.policy == 1) {
-    if (mom) hipExtLaunchKernelGGL((ssgd_apply_kernel<true, 1>), g, b, 0, stream, t.start, t.stop, 0, a);
-    else hipExtLaunchKernelGGL((ssgd_apply_kernel<false, 1>), g, b, 0, stream, t.start, t.stop, 0, a);
-  } else {
-    if (mom) hipExtLaunchKernelGGL((ssgd_apply_kernel<true, 0>), g, b, 0, stream, t.start, t.stop, 0, a);
-    else hipExtLaunchKernelGGL((ssgd_apply_kernel<false, 0>), g, b, 0, stream, t.start, t.stop, 0, a);
-  }
-  return hipGetLastError();
+  if (cfg.policy == 1) return mom ? ssgd_apply_p<true, 1>(a, cfg, stream, t) : ssgd_apply_p<false, 1>(a, cfg, stream, t);
+  return mom ? ssgd_apply_p<true, 0>(a, cfg, stream, t) : ssgd_apply_p<false, 0>(a, cfg, stream, t);
 }
+
+#undef CBX_LAUNCH_U
 
 hipError_t launch_bn_pack(const BnSegment *segs, int nseg, uint32_t maxlen, float *scratch, hipStream_t stream) {
   if (nseg <= 0 || maxlen == 0) return hipSuccess;

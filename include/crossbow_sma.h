@@ -263,10 +263,15 @@ int cbx_timing_history (cbx_context *ctx, int local, int which, float *ms, int m
  * load/store policy (0 plain, 1 nontemporal), float4s per thread per trip. */
 int cbx_set_kernel_config (cbx_context *ctx, int block, int blocks_per_cu, int policy, int unroll);
 /* Occupancy cap for the SMA kernels, in waves per CU: 1..32, 0 = none, -1
- * = auto (the default: about 36 read streams in flight per CU, i.e. 2 waves
- * for the R = 8 step, 12 for kernel B).  Enforced through reserved LDS per
+ * = auto (the default: about 56 buffer streams, reads plus writes, in
+ * flight per CU, i.e. 2 waves for the R = 8 step, 11 for kernel B, 8 for
+ * the optimiser step).  Enforced through reserved LDS per
  * workgroup (so the smallest reachable cap is 2 workgroups per CU).      */
 int cbx_set_kernel_occupancy (cbx_context *ctx, int waves_per_cu);
+/* Launch geometry of the per-task kernels (the replica optimiser step and
+ * the S-SGD task/barrier kernels): threads per block (64..512, multiple of
+ * 64), float4s per lane (1 or 2), occupancy cap in waves per CU as above. */
+int cbx_set_aux_kernel_config (cbx_context *ctx, int block, int unroll, int waves_per_cu);
 /* Bucketed pipeline for G > 1: kernel A / all-reduce / kernel B per bucket
  * of `bucket_elements` floats; 0 (default) = 8 buckets when G > 1, one at
  * G = 1; a value >= n = one bucket, all in order on the sync stream.  With

@@ -36,15 +36,21 @@ def _gpu(n, R, momentum, wd, alpha=0.1, policy=None):
     return g
 
 
+AUX_CONFIGS = [None, (64, 2, 2), (256, 1, 0), (512, 1, 8)]
+
+
 @pytest.mark.parametrize("momentum", [0.0, 0.9])
 @pytest.mark.parametrize("wd", [0.0, 5e-4])
 @pytest.mark.parametrize("on_torch_stream", [False, True])
-def test_optimise_bitexact(momentum, wd, on_torch_stream):
+@pytest.mark.parametrize("aux", AUX_CONFIGS)
+def test_optimise_bitexact(momentum, wd, on_torch_stream, aux):
     import torch
     from crossbow_amd import BUF_DATA, BUF_DIFF, BUF_GRADIENT, BUF_LAST
     n, R = 70_001, 2
     g = _gpu(n, R, momentum, wd)
     try:
+        if aux:
+            g.set_aux_kernel_config(*aux)
         stream = torch.cuda.Stream() if on_torch_stream else None
         for i in range(R):
             w = O.fill_normal(n, 300 + i, 0.05)
@@ -157,7 +163,8 @@ def test_nesterov_is_unsupported():
 
 @pytest.mark.parametrize("momentum", [0.0, 0.9])
 @pytest.mark.parametrize("split", [False, True])
-def test_ssgd_clock_loop_bitexact(momentum, split):
+@pytest.mark.parametrize("aux", AUX_CONFIGS)
+def test_ssgd_clock_loop_bitexact(momentum, split, aux):
     # Synchronous SGD (update model WORKER): task steps add
     # lr-scaled gradients into the base gradient; the barrier all-reduces it,
     # scales by 1/wpc, applies base momentum and copies z to every replica.
@@ -175,6 +182,8 @@ def test_ssgd_clock_loop_bitexact(momentum, split):
         g.setWeightDecay(1e-4)
         g.setLearningRateDecayPolicyFixed(0.05)
         g.setModelManager(R, 1)  # SSP: the barrier may skip a busy replica
+        if aux:
+            g.set_aux_kernel_config(*aux)
         if split:
             g.set_force_split(True)
         st = O.make_state(n, 1, R, 0.1, momentum)
