@@ -6,6 +6,6 @@ build (``build.py``), and the host-side mirror of Crossbow's interface for the
 path: ``TheGPU`` (the JNI natives) and ``ModelManager.trySynchronise``.
 """
 from ._lib import (BUF_DATA, BUF_DIFF, BUF_GRADIENT, BUF_LAST, SYNC_ASP, SYNC_BSP, SYNC_SSP,  # noqa: F401
-                   UPDATE_SMA, UPDATE_SYNCHRONOUSEAMSGD, UPDATE_WORKER, CbxError)
+                   UPDATE_DEFAULT, UPDATE_SMA, UPDATE_SYNCHRONOUSEAMSGD, UPDATE_WORKER, CbxError)
 from .modelmanager import ModelManager  # noqa: F401
 from .thegpu import TheGPU  # noqa: F401

@@ -37,7 +37,7 @@ ERROR_NAMES = {
 BUF_DATA, BUF_GRADIENT, BUF_DIFF, BUF_LAST = 0, 1, 2, 3
 T_KERNEL, T_ALLREDUCE, T_APPLY, T_STEP, T_H2D, T_D2H, T_COUNT = range(7)
 SYNC_BSP, SYNC_SSP, SYNC_ASP = 0, 1, 2
-UPDATE_WORKER, UPDATE_SYNCHRONOUSEAMSGD, UPDATE_SMA = 1, 3, 7
+UPDATE_DEFAULT, UPDATE_WORKER, UPDATE_SYNCHRONOUSEAMSGD, UPDATE_SMA = 0, 1, 3, 7
 
 
 class CbxError(RuntimeError):

@@ -1383,6 +1383,8 @@ int cbx_merge(cbx_context *c, int pull, int *first_out) {
   return CBX_OK;
 }
 
+static int default_step(cbx_context *c, int first);
+
 // staged: 0 = device-resident step; > 0 = host-staged step over that many
 // buckets (cbx_synchronise_staged).
 static int synchronise_impl(cbx_context *c, int first, int clock, int autotune, int staged) {
@@ -1394,14 +1396,14 @@ static int synchronise_impl(cbx_context *c, int first, int clock, int autotune, 
   // WORKER (1) is synchronous SGD (executioncontext.c:2277-2279), which shares
   // the base-model buffers and the all-reduce.
   const int type = c->model.type;
-  if (type == CBX_UPDATE_WORKER) {
+  if (type == CBX_UPDATE_WORKER || type == CBX_UPDATE_DEFAULT) {
     if (staged) TRY(cbx_stage_in(c));
-    TRY(ssgd_step(c, first));
+    TRY(type == CBX_UPDATE_WORKER ? ssgd_step(c, first) : default_step(c, first));
     if (staged) TRY(cbx_stage_out(c));
   } else if (type == CBX_UPDATE_SMA || type == CBX_UPDATE_SYNCHRONOUSEAMSGD) {
     TRY(staged ? sma_step_staged(c, first, staged) : sma_step(c, first));
   } else {
-    return fail(CBX_ERR_UNSUPPORTED, "update model %d is not on this library's path (SMA, SYNCHRONOUSEAMSGD, WORKER)", type);
+    return fail(CBX_ERR_UNSUPPORTED, "update model %d is not on this library's path (SMA, SYNCHRONOUSEAMSGD, WORKER, DEFAULT)", type);
   }
   if (autotune < 0) TRY(cbx_del_model(c));
   if (autotune > 0) TRY(cbx_add_model(c));
@@ -1581,6 +1583,74 @@ int cbx_del_model(cbx_context *c) {
 }
 
 // ---- replica optimiser step (kernels/optimisers/sma.cu:3-100) -------------
+// crossbowKernelOptimiserDefault, kernels/optimisers/default.cu:3-131: the
+// replica and its device's base model take the same step.  The reference
+// updates the replica on the task stream and the base model on the sync
+// stream after the gradient is ready (:84-99, :115-127); base-model updates
+// of concurrent tasks are ordered by that one stream.  Here the whole step is
+// one pass on the sync stream (it waits for the task stream first), and the
+// task stream then waits for it before using the replica again.
+static int default_task_step(cbx_context *c, Replica &r, Device &d, int task, hipStream_t st) {
+  SolverConf &conf = r.conf;
+  if (conf.momentum > 0 && conf.momentumMethod == 1)
+    return fail(CBX_ERR_UNSUPPORTED, "Nesterov's momentum has been disabled");  // default.cu:42-44
+  if (conf.momentum > 0 && !c->has_last)
+    return fail(CBX_ERR_STATE, "replica momentum without a `last` buffer (model.c:116-120)");
+  float lr = 0.0f;
+  TRY(conf.learning_rate(task, &lr));
+  cbx::OptArgs a;
+  std::memset(&a, 0, sizeof(a));
+  a.w = reinterpret_cast<cbx::v4f *>(replica_dev(d, r, CBX_BUF_DATA));
+  a.g = reinterpret_cast<cbx::v4f *>(replica_dev(d, r, CBX_BUF_GRADIENT));
+  a.last = conf.momentum > 0 ? reinterpret_cast<cbx::v4f *>(replica_dev(d, r, CBX_BUF_LAST)) : nullptr;
+  a.z = reinterpret_cast<cbx::v4f *>(base_dev(c, d, CBX_BUF_DATA));
+  a.n4 = c->n4;
+  a.rate = -lr;  // default.cu:38
+  a.momentum = conf.momentum;
+  a.wd = conf.weightDecay;
+  HIP_TRY(hipSetDevice(d.hip_id));
+  if (!r.client) HIP_TRY(hipEventCreateWithFlags(&r.client, hipEventDisableTiming));
+  if (st != d.stream) {
+    HIP_TRY(hipEventRecord(r.client, st));  // the gradient is ready (default.cu:64,101)
+    HIP_TRY(hipStreamWaitEvent(d.stream, r.client, 0));
+  }
+  cbx::LaunchConfig cfg = c->aux_cfg;
+  cfg.num_cus = d.num_cus;
+  cfg.blocks_per_cu = 0;
+  HIP_TRY(cbx::launch_default_optimise(a, cfg, d.stream, {}));
+  if (st != d.stream) {
+    HIP_TRY(hipEventRecord(r.client, d.stream));  // replica->server (:98,:127)
+    HIP_TRY(hipStreamWaitEvent(st, r.client, 0));
+  }
+  return CBX_OK;
+}
+
+// DEFAULT barrier, synch/default.c:5-43: copy the base model to every locked
+// replica i >= first.  Multi-GPU DEFAULT is err() in the reference (:46-51).
+static int default_step(cbx_context *c, int first) {
+  if (c->G > 1) return fail(CBX_ERR_UNSUPPORTED, "Multi-GPU default SGD model synchronisation is not supported yet");
+  Device &d = c->devs[0];
+  cbx::SmaArgs a;
+  std::memset(&a, 0, sizeof(a));
+  int k = 0;
+  for (int id : d.replicas) {
+    if (id < first || !c->locked[id]) continue;
+    if (k >= cbx::kMaxReplicas) return fail(CBX_ERR_UNSUPPORTED, "too many replicas on one device");
+    a.w[k++] = reinterpret_cast<cbx::v4f *>(replica_dev(d, *c->replicas[id], CBX_BUF_DATA));
+  }
+  a.nrep = k;
+  a.z = reinterpret_cast<cbx::v4f *>(base_dev(c, d, CBX_BUF_DATA));
+  a.n4 = c->n4;
+  HIP_TRY(hipSetDevice(d.hip_id));
+  cbx::LaunchConfig cfg = c->aux_cfg;
+  cfg.num_cus = d.num_cus;
+  cfg.blocks_per_cu = 0;
+  HIP_TRY(cbx::launch_broadcast(a, cfg, d.stream, {ring_event(c, d, EV_START), ring_event(c, d, EV_A)}));
+  ring_advance(c, d, 0);
+  c->last_step_split = false;
+  return finish_step(c);
+}
+
 // crossbowKernelOptimiserSynchronousSGD, kernels/optimisers/synchronoussgd.cu:3-56:
 // weight decay on the replica gradient, then the lr-scaled gradient is added
 // into the device's base-model gradient on the sync stream (:38-52).
@@ -1619,6 +1689,8 @@ int cbx_replica_optimise(cbx_context *c, int id, int task, void *stream) {
   const int type = c->model.type;
   if (type == CBX_UPDATE_WORKER)
     return ssgd_worker_step(c, r, d, task, stream ? reinterpret_cast<hipStream_t>(stream) : d.stream);
+  if (type == CBX_UPDATE_DEFAULT)
+    return default_task_step(c, r, d, task, stream ? reinterpret_cast<hipStream_t>(stream) : d.stream);
   if (type != CBX_UPDATE_SMA && type != CBX_UPDATE_SYNCHRONOUSEAMSGD)
     return fail(CBX_ERR_UNSUPPORTED, "update model %d has no optimiser step in this library", type);
   if (conf.momentum > 0 && conf.momentumMethod == 1)

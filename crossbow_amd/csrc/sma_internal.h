@@ -126,6 +126,7 @@ struct OptArgs {
   v4f *g;          // replica->gradient (updated in place, as the reference leaves it)
   v4f *last;       // replica->last (momentum > 0 only)
   v4f *s;          // replica->diff: the snapshot of w before the update
+  v4f *z;          // DEFAULT only: the device's base model (base->data), stepped too
   int64_t n4;      // float4s (multiple of kPadFloat4)
   float rate;      // -learning rate (sma.cu:43)
   float momentum;  // replica conf->momentum
@@ -133,6 +134,12 @@ struct OptArgs {
   int pad_;
 };
 hipError_t launch_sma_optimise(const OptArgs &a, const LaunchConfig &cfg, hipStream_t stream, Timing t = {});
+// DEFAULT update model (0, kernels/optimisers/default.cu:3-131): the task
+// step moves the replica and its device's base model by the same gradient.
+// Reads w, g (, last), z; writes g (if changed), last, w, z.
+hipError_t launch_default_optimise(const OptArgs &a, const LaunchConfig &cfg, hipStream_t stream, Timing t = {});
+// DEFAULT barrier (synch/default.c:5-43): w_i = z for a.nrep replicas a.w[].
+hipError_t launch_broadcast(const SmaArgs &a, const LaunchConfig &cfg, hipStream_t stream, Timing t = {});
 // Synchronous SGD (update model WORKER = 1), the other synchronous model that
 // shares the base-model buffers and the all-reduce.
 struct SsgdArgs {

@@ -299,6 +299,68 @@ __global__ __launch_bounds__(512) void sma_optimise_kernel(const OptArgs a) {
 }
 
 // ---------------------------------------------------------------------------
+// DEFAULT task step (kernels/optimisers/default.cu:3-131): the reference runs
+// up to 5 replica ops on the task stream and one base-model saxpy on the sync
+// stream; here one pass reads w, g (, last), z once and writes them once.
+//   g = fma(wd, w, g)                            :26-35 (wd > 0)
+//   g = rate * g ; g = fma(mu, last, g); last = g :46-73
+//   w = fma(1, g, w) ; z = fma(1, g, z)           :75-94
+//   without momentum: w = fma(rate, g, w) ; z = fma(rate, g, z)   :102-125
+// ---------------------------------------------------------------------------
+template <bool MOM, bool WD, int P, int U>
+__global__ __launch_bounds__(512) void default_optimise_kernel(const OptArgs a) {
+  const uint32_t trip = gridDim.x * blockDim.x * U;
+  const uint32_t n4 = (uint32_t)a.n4;
+  const v4f rate = a.rate, mu = a.momentum, wd = a.wd, one = 1.0f;
+  for (uint32_t base = first_elem<U>(); base < n4; base += trip) {
+    v4f w[U], g[U], l[U], z[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t i = (base + u * 64u) * 16u;
+      w[u] = ldo<P>(a.w, i);
+      g[u] = ldo<P>(a.g, i);
+      if constexpr (MOM) l[u] = ldo<P>(a.last, i);
+      z[u] = ldo<P>(a.z, i);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t i = (base + u * 64u) * 16u;
+      if constexpr (WD) g[u] = vfma(wd, w[u], g[u]);
+      if constexpr (MOM) {
+        g[u] = rate * g[u];
+        g[u] = vfma(mu, l[u], g[u]);
+        sto<P>(a.last, i, g[u]);
+        sto<P>(a.w, i, vfma(one, g[u], w[u]));
+        sto<P>(a.z, i, vfma(one, g[u], z[u]));
+        sto<P>(a.g, i, g[u]);
+      } else {
+        sto<P>(a.w, i, vfma(rate, g[u], w[u]));
+        sto<P>(a.z, i, vfma(rate, g[u], z[u]));
+        if constexpr (WD) sto<P>(a.g, i, g[u]);
+      }
+    }
+  }
+}
+
+// DEFAULT barrier (synch/default.c:19-37): the reference issues one D2D copy
+// per locked replica (8n B each); here z is read once: (4 + 4R) n B.
+template <int P, int U>
+__global__ __launch_bounds__(512) void broadcast_kernel(const SmaArgs a) {
+  const uint32_t trip = gridDim.x * blockDim.x * U;
+  const uint32_t n4 = (uint32_t)a.n4;
+  for (uint32_t base = first_elem<U>(); base < n4; base += trip) {
+    v4f z[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) z[u] = ldo<P>(a.z, (base + u * 64u) * 16u);
+    for (int r = 0; r < a.nrep; ++r) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) sto<P>(a.w[r], (base + u * 64u) * 16u, z[u]);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Synchronous SGD (WORKER).  Task step, on the sync stream so replicas add
 // into the device's one accumulator in enqueue order (synchronoussgd.cu:3-56):
 //   g = fma(wd, w, g)        :20-26 (wd > 0; g written back)
@@ -559,6 +621,34 @@ hipError_t launch_sma_optimise(const OptArgs &a, const LaunchConfig &cfg, hipStr
   }
   if (mom) return wd ? optimise_p<true, true, 0>(a, cfg, stream, t) : optimise_p<true, false, 0>(a, cfg, stream, t);
   return wd ? optimise_p<false, true, 0>(a, cfg, stream, t) : optimise_p<false, false, 0>(a, cfg, stream, t);
+}
+
+template <bool MOM, bool WD, int P>
+hipError_t default_p(const OptArgs &a, const LaunchConfig &cfg, hipStream_t stream, Timing t) {
+  const int reads = 3 + (MOM ? 1 : 0), writes = 2 + (MOM ? 2 : (WD ? 1 : 0));
+  CBX_LAUNCH_U(default_optimise_kernel, MOM, WD, P);
+  return hipGetLastError();
+}
+
+hipError_t launch_default_optimise(const OptArgs &a, const LaunchConfig &cfg, hipStream_t stream, Timing t) {
+  const bool mom = a.momentum > 0.0f, wd = a.wd > 0.0f;
+  if (cfg.policy == 1) {
+    if (mom) return wd ? default_p<true, true, 1>(a, cfg, stream, t) : default_p<true, false, 1>(a, cfg, stream, t);
+    return wd ? default_p<false, true, 1>(a, cfg, stream, t) : default_p<false, false, 1>(a, cfg, stream, t);
+  }
+  if (mom) return wd ? default_p<true, true, 0>(a, cfg, stream, t) : default_p<true, false, 0>(a, cfg, stream, t);
+  return wd ? default_p<false, true, 0>(a, cfg, stream, t) : default_p<false, false, 0>(a, cfg, stream, t);
+}
+
+template <int P>
+hipError_t broadcast_p(const SmaArgs &a, const LaunchConfig &cfg, hipStream_t stream, Timing t) {
+  const int reads = 1, writes = a.nrep;
+  CBX_LAUNCH_U(broadcast_kernel, P);
+  return hipGetLastError();
+}
+
+hipError_t launch_broadcast(const SmaArgs &a, const LaunchConfig &cfg, hipStream_t stream, Timing t) {
+  return cfg.policy == 1 ? broadcast_p<1>(a, cfg, stream, t) : broadcast_p<0>(a, cfg, stream, t);
 }
 
 template <bool WD, int P>

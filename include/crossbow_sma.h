@@ -37,6 +37,7 @@ extern "C" {
 #define CBX_ERR_UNSUPPORTED -8  /* outside this library's scope   */
 
 /* Update model ids, uk/ac/imperial/lsds/crossbow/types/UpdateModel.java:5 */
+#define CBX_UPDATE_DEFAULT           0   /* single GPU: synch/default.c, optimisers/default.cu */
 #define CBX_UPDATE_WORKER            1   /* synchronous SGD: synch/synchronoussgd.c */
 #define CBX_UPDATE_SYNCHRONOUSEAMSGD 3   /* routed to SMA: clib-multigpu/utils.h:56-57 */
 #define CBX_UPDATE_SMA               7
@@ -132,7 +133,9 @@ int cbx_merge (cbx_context *ctx, int pull, int *first);
  * synchronisation stream and returns without blocking the host.  Update
  * models SMA (7) and SYNCHRONOUSEAMSGD (3) run SMA; WORKER (1) runs the
  * synchronous-SGD barrier (synch/synchronoussgd.c:13-106, needs the work
- * per clock); any other is CBX_ERR_UNSUPPORTED.                          */
+ * per clock); DEFAULT (0) copies the base model to every locked replica
+ * (synch/default.c:5-43; one GPU only, as in the reference: more devices
+ * give CBX_ERR_UNSUPPORTED); any other is CBX_ERR_UNSUPPORTED.          */
 int cbx_synchronise (cbx_context *ctx, int first, int clock, int autotune, int push);
 /* The same step for a model manager whose buffers live in host memory
  * (north_star: "starts and ends in host memory", databuffer.c:95-122):
@@ -200,7 +203,10 @@ int cbx_replica_set_copy (cbx_context *ctx, int id, int flag);
  * Under update model WORKER the step is crossbowKernelOptimiserSynchronousSGD
  * (synchronoussgd.cu:3-56) instead: weight decay, then the lr-scaled
  * gradient is added into the device's base-model gradient on the sync
- * stream, to be all-reduced and applied at the next barrier.            */
+ * stream, to be all-reduced and applied at the next barrier.  Under
+ * DEFAULT it is crossbowKernelOptimiserDefault (default.cu:3-131): the
+ * replica and its device's base model take the same step, in one pass on
+ * the sync stream (the task stream waits for it).                       */
 int cbx_replica_optimise (cbx_context *ctx, int id, int task, void *stream);
 /* Global device index a replica lives on (id % G). */
 int cbx_replica_device (cbx_context *ctx, int id);

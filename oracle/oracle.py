@@ -63,6 +63,12 @@ def lib():
             f = getattr(L, name)
             f.restype = None if name == "cbo_sma_optimise" else ctypes.c_int
             f.argtypes = [ctypes.c_size_t, ctypes.c_float, ctypes.c_float, ctypes.c_float, fp, fp, fp, fp]
+        for name in ("cbo_default_task", "cbo_default_task_blas"):
+            f = getattr(L, name)
+            f.restype = None if name == "cbo_default_task" else ctypes.c_int
+            f.argtypes = [ctypes.c_size_t, ctypes.c_float, ctypes.c_float, ctypes.c_float, fp, fp, fp, fp]
+        L.cbo_default_sync.restype = None
+        L.cbo_default_sync.argtypes = [ctypes.c_int, ctypes.c_size_t, fp, fpp, ip, ctypes.c_int]
         for name in ("cbo_ssgd_worker", "cbo_ssgd_worker_blas"):
             f = getattr(L, name)
             f.restype = None if name == "cbo_ssgd_worker" else ctypes.c_int
@@ -210,6 +216,30 @@ def sma_optimise(rate: float, momentum: float, wd: float, w: np.ndarray, g: np.n
             raise RuntimeError("OpenBLAS replay unavailable")
     else:
         lib().cbo_sma_optimise(w.size, rate, momentum, wd, _fp(w), _fp(g), lp, _fp(s))
+
+
+def default_task(rate: float, momentum: float, wd: float, w: np.ndarray, g: np.ndarray,
+                 last: Optional[np.ndarray], z: np.ndarray, blas: bool = False) -> None:
+    """DEFAULT task step (kernels/optimisers/default.cu:3-131), in place on w, g,
+    last and the device's base model z.  ``rate`` is the negated learning rate."""
+    if momentum > 0 and last is None:
+        raise ValueError("momentum > 0 needs the replica's `last` buffer (model.c:116-120)")
+    lp = _fp(last) if last is not None else ctypes.POINTER(ctypes.c_float)()
+    if blas:
+        if not lib().cbo_blas_is_open():
+            blas_open()
+        if lib().cbo_default_task_blas(w.size, rate, momentum, wd, _fp(w), _fp(g), lp, _fp(z)) != 0:
+            raise RuntimeError("OpenBLAS replay unavailable")
+    else:
+        lib().cbo_default_task(w.size, rate, momentum, wd, _fp(w), _fp(g), lp, _fp(z))
+
+
+def default_sync(st: SmaState) -> None:
+    """DEFAULT barrier, single GPU (synch/default.c:5-43): w_i = z for locked i >= first."""
+    if st.G != 1:
+        raise ValueError("multi-GPU DEFAULT synchronisation is err() in the reference (default.c:46-51)")
+    lib().cbo_default_sync(st.size, st.n, _fp(st.z[0]), _fpp(st.w),
+                           st.locked.ctypes.data_as(ctypes.POINTER(ctypes.c_int)), st.first)
 
 
 def ssgd_worker(rate: float, wd: float, w: np.ndarray, g: np.ndarray, acc: np.ndarray, blas: bool = False) -> None:

@@ -307,6 +307,57 @@ int cbo_sma_optimise_blas (size_t n, float rate, float momentum, float wd,
 }
 
 /* ---------------------------------------------------------------------- */
+/* DEFAULT (update model 0).                                               */
+/* ---------------------------------------------------------------------- */
+void cbo_default_task (size_t n, float rate, float momentum, float wd,
+		float *w, float *g, float *last, float *z) {
+	size_t k;
+	for (k = 0; k < n; ++k) {
+		float gk = g[k];
+		if (wd > 0)
+			gk = fmaf (wd, w[k], gk);                                       /* default.cu:26-35   */
+		if (momentum > 0) {
+			gk = rate * gk;                                                 /* default.cu:46-53 sscal */
+			gk = fmaf (momentum, last[k], gk);                              /* default.cu:55-62   */
+			last[k] = gk;                                                   /* default.cu:68-73   */
+			w[k] = fmaf (1.0f, gk, w[k]);                                   /* default.cu:75-82   */
+			z[k] = fmaf (1.0f, gk, z[k]);                                   /* default.cu:87-94   */
+		} else {
+			w[k] = fmaf (rate, gk, w[k]);                                   /* default.cu:106-113 */
+			z[k] = fmaf (rate, gk, z[k]);                                   /* default.cu:118-125 */
+		}
+		g[k] = gk;
+	}
+}
+
+int cbo_default_task_blas (size_t n, float rate, float momentum, float wd,
+		float *w, float *g, float *last, float *z) {
+	int N = (int) n;
+	if (! blas_saxpy || ! blas_sscal)
+		return -1;
+	if (wd > 0)
+		blas_saxpy (N, wd, w, 1, g, 1);
+	if (momentum > 0) {
+		blas_sscal (N, rate, g, 1);
+		blas_saxpy (N, momentum, last, 1, g, 1);
+		memcpy (last, g, n * sizeof(float));
+		blas_saxpy (N, 1.0f, g, 1, w, 1);
+		blas_saxpy (N, 1.0f, g, 1, z, 1);
+	} else {
+		blas_saxpy (N, rate, g, 1, w, 1);
+		blas_saxpy (N, rate, g, 1, z, 1);
+	}
+	return 0;
+}
+
+void cbo_default_sync (int size, size_t n, const float *z, float **w, const int *locked, int first) {
+	int i;
+	for (i = first; i < size; ++i)
+		if (locked[i])
+			memcpy (w[i], z, n * sizeof(float));                           /* default.c:19-37 */
+}
+
+/* ---------------------------------------------------------------------- */
 /* Synchronous SGD (WORKER).                                               */
 /* ---------------------------------------------------------------------- */
 void cbo_ssgd_worker (size_t n, float rate, float wd, const float *w, float *g, float *acc) {

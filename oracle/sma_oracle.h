@@ -115,6 +115,22 @@ int cbo_ssgd_sync_blas (int G, int size, size_t n, int wpc, float momentum,
 		float **z, float **last, float **w, float **acc,
 		const int *locked, int first, float *scratch);
 
+/* DEFAULT update model (0), the reference apps' default (ModelConf.java:81). */
+/* Task step, crossbowKernelOptimiserDefault (kernels/optimisers/default.cu: */
+/* 3-131): the replica AND its device's base model take the step; rate is   */
+/* -learningRate(task).                                                      */
+/*   wd > 0      : g = fma(wd, w, g)                          default.cu:26-35   */
+/*   momentum > 0: g = rate * g; g = fma(mu, last, g);        default.cu:46-66   */
+/*                 last = g; w = fma(1, g, w); z = fma(1, g, z)  :69-99         */
+/*   else        : w = fma(rate, g, w); z = fma(rate, g, z)   default.cu:102-127 */
+void cbo_default_task (size_t n, float rate, float momentum, float wd,
+		float *w, float *g, float *last, float *z);
+int cbo_default_task_blas (size_t n, float rate, float momentum, float wd,
+		float *w, float *g, float *last, float *z);
+/* Barrier, single GPU only (synch/default.c:5-43): w_i = z for every locked */
+/* replica i >= first.  (Multi-GPU DEFAULT is err() in the reference, :46-51.) */
+void cbo_default_sync (int size, size_t n, const float *z, float **w, const int *locked, int first);
+
 /* Batch-norm running-statistics averaging across devices                  */
 /* (crossbowCudnnBatchNormParamsSynchroniseEstimatedMeanAndVariable,        */
 /* cudnn/cudnnbatchnormparams.c:157-222), for `layers` BN layers at once.   */

@@ -214,3 +214,65 @@ def test_ssgd_clock_loop_bitexact(momentum, split, aux):
             assert_bitexact(g.replica_read(i, BUF_DATA), st.w[i], f"w[{i}]")
     finally:
         g.free()
+
+
+@pytest.mark.parametrize("momentum", [0.0, 0.9])
+@pytest.mark.parametrize("on_torch_stream", [False, True])
+@pytest.mark.parametrize("aux", [None, (64, 2, 2)])
+def test_default_clock_loop_bitexact(momentum, on_torch_stream, aux):
+    # Update model DEFAULT (0), the reference apps' default: every task step
+    # moves the replica and the base model by the same gradient
+    # (kernels/optimisers/default.cu:3-131), the barrier copies the base model
+    # to the locked replicas (synch/default.c:5-43).  SSP holds replica 2.
+    import torch
+    from crossbow_amd import BUF_DATA, BUF_GRADIENT, BUF_LAST, UPDATE_DEFAULT, TheGPU
+    from tests.helpers import upload
+    n, R, tasks, clocks = 50_001, 3, 5, 2
+    g = TheGPU()
+    g.init([0])
+    try:
+        g.setModel(1, 4 * n)
+        g.setModelVariable(0, 1, [n], 4 * n)
+        g.setUpdateModelType(UPDATE_DEFAULT)
+        g.setMomentum(momentum, 0)
+        g.setWeightDecay(1e-4)
+        g.setLearningRateDecayPolicyFixed(0.05)
+        g.setModelManager(R, 1)
+        if aux:
+            g.set_aux_kernel_config(*aux)
+        st = O.make_state(n, 1, R, 0.1, momentum)
+        st.locked[2] = 0
+        upload(g, st)
+        lasts = [O.fill_normal(n, 700 + i, 0.001) if momentum > 0 else None for i in range(R)]
+        for i in range(R):
+            if lasts[i] is not None:
+                g.replica_write(i, BUF_LAST, lasts[i])
+        stream = torch.cuda.Stream() if on_torch_stream else None
+        task = 0
+        for clock in range(1, clocks + 1):
+            for k in range(tasks):
+                i = k % R
+                gr = O.fill_normal(n, 3000 + task, 0.01)
+                g.replica_write(i, BUF_GRADIENT, gr)
+                g.replica_optimise(i, task, stream.cuda_stream if stream else None)
+                O.default_task(np.float32(-0.05), momentum, 1e-4, st.w[i], gr, lasts[i], st.z[0])
+                if stream is not None:
+                    stream.synchronize()
+                g.wait()
+                assert_bitexact(g.replica_read(i, BUF_GRADIENT), gr, f"g[{i}] task {task}")
+                task += 1
+            g.replica_lock(2)
+            g.lockAny()
+            g.synchronise(0, clock, 0, False)
+            g.unlockAny()
+            g.replica_unlock(2)
+            O.default_sync(st)
+        g.wait()
+        assert_bitexact(g.base_read(0, BUF_DATA), st.z[0], "z")
+        for i in range(R):
+            assert_bitexact(g.replica_read(i, BUF_DATA), st.w[i], f"w[{i}]")
+            if lasts[i] is not None:
+                assert_bitexact(g.replica_read(i, BUF_LAST), lasts[i], f"last[{i}]")
+        assert not np.array_equal(st.w[2], st.z[0]), "the held replica is not copied"
+    finally:
+        g.free()

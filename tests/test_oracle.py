@@ -165,6 +165,40 @@ def test_optimiser_restatement_equals_openblas_sequence(momentum, wd):
     assert not _eq(a[0], w)
 
 
+@pytest.mark.parametrize("momentum", [0.0, 0.9])
+@pytest.mark.parametrize("wd", [0.0, 5e-4])
+def test_default_task_restatement_equals_openblas_sequence(momentum, wd):
+    # kernels/optimisers/default.cu:3-131: replica and base model take the same
+    # step; fmaf restatement == literal saxpy / sscal / memcpy sequence.
+    n = 4099
+    w = O.fill_normal(n, 110, 0.05)
+    g = O.fill_normal(n, 111, 0.01)
+    last = O.fill_normal(n, 112, 0.001) if momentum > 0 else None
+    z = O.fill_normal(n, 113, 0.05)
+    a = [x.copy() if x is not None else None for x in (w, g, last, z)]
+    b = [x.copy() if x is not None else None for x in (w, g, last, z)]
+    O.default_task(-0.1, momentum, wd, *a)
+    O.default_task(-0.1, momentum, wd, *b, blas=True)
+    for x, y in zip(a, b):
+        if x is not None:
+            assert _eq(x, y)
+    # both models moved by the same (scaled) gradient
+    np.testing.assert_allclose(a[0] - w, a[3] - z, rtol=0, atol=1e-6)
+
+
+def test_default_sync_copies_base_to_locked_replicas():
+    # synch/default.c:5-43: w_i = z for locked i >= first; others untouched.
+    st = O.make_state(1031, 1, 4, 0.1, 0.0)
+    st.locked[2] = 0
+    st.first = 1
+    w0 = [x.copy() for x in st.w]
+    O.default_sync(st)
+    assert _eq(st.w[0], w0[0]) and _eq(st.w[2], w0[2])
+    assert _eq(st.w[1], st.z[0]) and _eq(st.w[3], st.z[0])
+    with pytest.raises(ValueError):
+        O.default_sync(O.make_state(64, 2, 1, 0.1, 0.0))
+
+
 def test_optimiser_then_sma_moves_replicas_toward_base():
     # One clock of the whole loop on the oracle: local steps, then averaging.
     st = O.make_state(2053, 1, 4, 0.5, 0.9)
