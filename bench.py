@@ -32,7 +32,7 @@ if ROOT not in sys.path:
 
 METRIC = "GB/s device-resident SMA param-bucket reduce (ResNet-50, 8 replicas)"
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
-XGMI_PEAK_GBS = 7 * 153.0  # per GPU, 7 links
+XGMI_LINK_GBS = 153.0  # per xGMI link (7 per MI355X, one to each peer on an 8-GPU node)
 SEED = 20190701
 
 
@@ -320,7 +320,10 @@ def main():
         algbw = 4 * n / (ar_ms * 1e-3) / 1e9
         busbw = algbw * 2 * (G - 1) / G if G > 1 else 0.0
         result["allreduce"] = {"ms_median": round(ar_ms, 4), "algbw_GBs": round(algbw, 1),
-                               "busbw_GBs": round(busbw, 1), "xgmi_peak_GBs": XGMI_PEAK_GBS,
+                               "busbw_GBs": round(busbw, 1),
+                               # a G-GPU all-reduce can use the G-1 links from each GPU to its peers
+                               "xgmi_links": G - 1, "xgmi_peak_GBs": (G - 1) * XGMI_LINK_GBS,
+                               "xgmi_frac": round(busbw / ((G - 1) * XGMI_LINK_GBS), 4) if G > 1 else None,
                                "apply_ms_median": round(statistics.median(calib["apply"]), 4),
                                "unpipelined_step_ms_median": round(statistics.median(calib["step"]), 4),
                                "timed_in": "calibration steps (one bucket, in order)"}
