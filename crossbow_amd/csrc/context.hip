@@ -207,7 +207,8 @@ struct Device {
   std::vector<char *> extra;
   std::vector<char *> extra_host;
   std::vector<int> replicas;  // global ids, increasing
-  hipEvent_t synched = nullptr;     // end-of-step marker when timing is off
+  hipEvent_t synched = nullptr;     // end-of-step event when timing is off
+  bool synched_by_dispatch = false;  // the step's last dispatch completes `synched` itself
   hipEvent_t step_event = nullptr;  // end of the last step (cbx_step_event)
   hipEvent_t ev[EV_COUNT] = {};
   bool ev_valid[EV_COUNT] = {};
@@ -517,11 +518,21 @@ int finish_step(cbx_context *c) {
       const int prev = (d.ring_pos + Device::kRing - 1) % Device::kRing;
       d.step_event = d.ring[(size_t)prev * 4 + (d.ring_split[prev] == 0 ? EV_A : EV_B)];
     } else {
-      HIP_TRY(hipEventRecord(d.synched, d.stream));
+      if (!d.synched_by_dispatch) HIP_TRY(hipEventRecord(d.synched, d.stream));
       d.step_event = d.synched;
     }
+    d.synched_by_dispatch = false;
   }
   return CBX_OK;
+}
+
+// The stop event for a step's LAST dispatch: the ring event `ev` when timing,
+// else `synched`, which the dispatch then completes itself: no marker packet
+// between steps (a marker cost ~3 us per fused step, scripts/step_overhead.py).
+hipEvent_t step_stop_event(cbx_context *c, Device &d, int ev) {
+  if (c->timing && !d.ring.empty()) return d.ring[(size_t)d.ring_pos * 4 + ev];
+  d.synched_by_dispatch = true;
+  return d.synched;
 }
 
 // cbx_set_force_split at G = 1: the split pipeline runs over a one-rank
@@ -557,7 +568,7 @@ int sma_step(cbx_context *c, int first) {
     // The dispatch timestamps its own (start, stop) ring events: no marker
     // packets between steps (each costs ~3 us of stream time, membench v4).
     HIP_TRY(cbx::launch_sma_fused(args[0], mom, copies_total > 0, cfg, d.stream,
-                                  {ring_event(c, d, EV_START), ring_event(c, d, EV_A)}));
+                                  {ring_event(c, d, EV_START), step_stop_event(c, d, EV_A)}));
     ring_advance(c, d, 0);
     c->last_step_split = false;
   } else {
@@ -652,7 +663,7 @@ int sma_step(cbx_context *c, int first) {
         cbx::LaunchConfig cfg = c->cfg;
         cfg.num_cus = d.num_cus;
         cbx::Timing t;
-        if (b == nb - 1) t.stop = ring_event(c, d, EV_B);
+        if (b == nb - 1) t.stop = step_stop_event(c, d, EV_B);
         HIP_TRY(cbx::launch_sma_apply(offset_args(args[k], start, len), mom, cfg, d.stream, t));
       }
       return CBX_OK;
@@ -909,7 +920,7 @@ int ssgd_step(cbx_context *c, int first) {
     cfg.num_cus = d.num_cus;
     cbx::Timing t;
     if (!split) t.start = ring_event(c, d, EV_START);
-    t.stop = ring_event(c, d, split ? EV_B : EV_A);
+    t.stop = step_stop_event(c, d, split ? EV_B : EV_A);
     HIP_TRY(cbx::launch_ssgd_apply(args[k], cfg, d.stream, t));
     ring_advance(c, d, split ? 2 : 0);
   }
@@ -1645,7 +1656,7 @@ static int default_step(cbx_context *c, int first) {
   cbx::LaunchConfig cfg = c->aux_cfg;
   cfg.num_cus = d.num_cus;
   cfg.blocks_per_cu = 0;
-  HIP_TRY(cbx::launch_broadcast(a, cfg, d.stream, {ring_event(c, d, EV_START), ring_event(c, d, EV_A)}));
+  HIP_TRY(cbx::launch_broadcast(a, cfg, d.stream, {ring_event(c, d, EV_START), step_stop_event(c, d, EV_A)}));
   ring_advance(c, d, 0);
   c->last_step_split = false;
   return finish_step(c);

@@ -491,3 +491,43 @@ def test_randomised_configurations_bitexact():
             raise AssertionError(f"case {case}: n={n} R={R} alpha={alpha} mu={momentum} held={held} "
                                  f"copy={copy_ids} first={first} split={split} bucket={bucket} "
                                  f"config={config}: {e}") from e
+
+
+@pytest.mark.parametrize("mode", ["fused", "split", "default"])
+@pytest.mark.parametrize("timing", [False, True])
+def test_step_event_covers_the_step(mode, timing):
+    # cbx_step_event stands for base->updated / replica->updated (sma.c:177,204,
+    # default.c:32): once it has completed, the step's results are in memory.
+    # Checked from the host with hipEventSynchronize and a null-stream copy
+    # (the sync stream is non-blocking, so only the event orders the read).
+    import ctypes
+    from crossbow_amd import BUF_DATA, UPDATE_DEFAULT
+    hip = ctypes.CDLL("libamdhip64.so")
+    hip.hipEventSynchronize.argtypes = [ctypes.c_void_p]
+    hip.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+    n, R = 1 << 22, 8
+    st = O.make_state(n, 1, R, 0.1, 0.9)
+    g = make_gpu(n, R, 0.1, 0.9, update_type=UPDATE_DEFAULT if mode == "default" else 7)
+    try:
+        if mode == "split":
+            g.set_force_split(True)
+            g.set_bucket_elements(n // 3)
+        g.set_timing(timing)
+        upload(g, st)
+        g.wait()
+        want = st.clone()
+        for clock in (1, 2):
+            g.lockAny()
+            g.synchronise(0, clock, 0, False)
+            g.unlockAny()
+            O.default_sync(want) if mode == "default" else O.sma_step(want)
+        ev = g.step_event(0)
+        assert hip.hipEventSynchronize(ev) == 0
+        out = np.empty(n, np.float32)
+        for i in (0, R - 1):
+            assert hip.hipMemcpy(out.ctypes.data, g.replica_buffer(i, BUF_DATA), 4 * n, 2) == 0
+            assert_bitexact(out, want.w[i], f"w[{i}] after the step event")
+        assert hip.hipMemcpy(out.ctypes.data, g.base_buffer(0, BUF_DATA), 4 * n, 2) == 0
+        assert_bitexact(out, want.z[0], "z after the step event")
+    finally:
+        g.free()
