@@ -369,6 +369,57 @@ static float time_ms(F launch, int iters) {
   return t[t.size() / 2];
 }
 
+// ---- v10: ceilings in the library's launch shape (64-thread blocks, U = 2
+// wave-contiguous float4s per lane, nt) under the same dynamic-LDS occupancy
+// caps, so the fused kernel is compared with ceilings at ITS occupancy.
+__device__ __forceinline__ uint32_t wc2(uint32_t u) { return blockIdx.x * 128u + u * 64u + (threadIdx.x & 63u); }
+__global__ __launch_bounds__(64) void read18_u2(const Args a, float *sink) {
+  v4f t = 0.0f;
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const uint32_t i = wc2(u) * 16u;
+    t += ldo<1>(a.z, i) + ldo<1>(a.last, i);
+#pragma unroll
+    for (int r = 0; r < R; ++r) t += ldo<1>(a.s[r], i) + ldo<1>(a.w[r], i);
+  }
+  if (t.x == 12345.678f) sink[0] = t.y;
+}
+__global__ __launch_bounds__(64) void write10_u2(const Args a) {
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const uint32_t i = wc2(u) * 16u;
+    const v4f v = (float)i;
+    sto<1>(a.z, i, v);
+    sto<1>(a.last, i, v);
+#pragma unroll
+    for (int r = 0; r < R; ++r) sto<1>(a.w[r], i, v);
+  }
+}
+// 18 reads + 10 writes with no load->store dependency (stores write a constant).
+__global__ __launch_bounds__(64) void mix_u2(const Args a, float *sink) {
+  v4f t = 0.0f;
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const uint32_t i = wc2(u) * 16u;
+    t += ldo<1>(a.z, i) + ldo<1>(a.last, i);
+#pragma unroll
+    for (int r = 0; r < R; ++r) t += ldo<1>(a.s[r], i) + ldo<1>(a.w[r], i);
+    const v4f v = (float)i;
+#pragma unroll
+    for (int r = 0; r < R; ++r) sto<1>(a.w[r], i, v);
+    sto<1>(a.z, i, v);
+    sto<1>(a.last, i, v);
+  }
+  if (t.x == 12345.678f) sink[0] = t.y;
+}
+__global__ __launch_bounds__(64) void copy_u2(v4f *dst, const v4f *src) {
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const uint32_t i = wc2(u) * 16u;
+    sto<1>(dst, i, ldo<1>(src, i));
+  }
+}
+
 int main(int argc, char **argv) {
   const int64_t n = 25557032;
   const uint32_t n4 = (uint32_t)(((n + 3) / 4 + 1023) / 1024 * 1024);
@@ -565,6 +616,40 @@ int main(int argc, char **argv) {
     return 0;
   }
 
+  if (argc > 2 && std::strcmp(argv[2], "v10") == 0) {
+    const size_t stride = (buf + (2u << 20) - 1) / (2u << 20) * (2u << 20) + 4096;
+    Args a;
+    a.z = (v4f *)arena;
+    a.last = (v4f *)(arena + stride);
+    for (int r = 0; r < R; ++r) {
+      a.s[r] = (const v4f *)(arena + (2 + 2 * r) * stride);
+      a.w[r] = (v4f *)(arena + (3 + 2 * r) * stride);
+    }
+    a.n4 = n4;
+    a.alpha = 0.1f;
+    hipLaunchKernelGGL(fillk, dim3(8192), dim3(256), 0, 0, (uint32_t *)arena, nbuf * stride / 4, 12345u);
+    CK(hipDeviceSynchronize());
+    const unsigned grid = n4 / 128;
+    const double rbytes = 18.0 * n4 * 16, wbytes = 10.0 * n4 * 16;
+    // copy over 14 buffers' worth (1.43 GB) so it sees the same working-set size
+    const uint32_t cn4 = (uint32_t)(7 * (size_t)stride / 16 / 128 * 128);
+    v4f *csrc = (v4f *)arena, *cdst = (v4f *)(arena + 7 * stride + (2u << 20));
+    for (int round = 0; round < 3; ++round)
+      for (int cap : {0, 2, 3, 4, 6, 8, 12}) {
+        // dynamic LDS that admits `cap` one-wave workgroups per CU (160 KiB per CU)
+        const unsigned lds = cap ? std::min(64u * 1024u, (160u / (unsigned)(cap + 1) + 1u) * 1024u) : 0u;
+        float t;
+        t = time_ms([&] { hipLaunchKernelGGL(read18_u2, dim3(grid), dim3(64), lds, 0, a, sink); }, iters);
+        std::printf("{\"v10\":%d,\"kind\":\"read18\",\"cap\":%d,\"GBs\":%.1f}\n", round, cap, rbytes / t / 1e6);
+        t = time_ms([&] { hipLaunchKernelGGL(write10_u2, dim3(grid), dim3(64), lds, 0, a); }, iters);
+        std::printf("{\"v10\":%d,\"kind\":\"write10\",\"cap\":%d,\"GBs\":%.1f}\n", round, cap, wbytes / t / 1e6);
+        t = time_ms([&] { hipLaunchKernelGGL(mix_u2, dim3(grid), dim3(64), lds, 0, a, sink); }, iters);
+        std::printf("{\"v10\":%d,\"kind\":\"mix18r10w-nodep\",\"cap\":%d,\"GBs\":%.1f}\n", round, cap, (rbytes + wbytes) / t / 1e6);
+        t = time_ms([&] { hipLaunchKernelGGL(copy_u2, dim3(cn4 / 128), dim3(64), lds, 0, cdst, csrc); }, iters);
+        std::printf("{\"v10\":%d,\"kind\":\"copy\",\"cap\":%d,\"GBs\":%.1f}\n", round, cap, 2.0 * cn4 * 16 / t / 1e6);
+      }
+    return 0;
+  }
   if (argc > 2 && std::strcmp(argv[2], "v9") == 0) {
     const size_t stride = (buf + (2u << 20) - 1) / (2u << 20) * (2u << 20) + 4096;
     Args a;
