@@ -103,6 +103,7 @@ SIGNATURES = {
     "cbx_replica_optimise": (_I, [_P, _I, _I, _P]),
     "cbx_replica_get_copy": (_I, [_P, _I]),
     "cbx_replica_set_copy": (_I, [_P, _I, _I]),
+    "cbx_replica_set_disabled": (_I, [_P, _I, _I]),
     "cbx_replica_device": (_I, [_P, _I]),
     "cbx_replica_is_local": (_I, [_P, _I]),
     "cbx_num_replicas": (_I, [_P]),

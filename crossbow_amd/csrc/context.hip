@@ -166,6 +166,7 @@ struct Replica {
   int slot = 0;       // replica slot within its device
   int clock = 0;
   int updates = 0;
+  bool disabled = false;  // theta-queue slot skipped (thetaqueue.c:182-194)
   SolverConf conf;
   pthread_mutex_t lock;
   hipEvent_t client = nullptr;  // end of the last optimiser step on a task stream (sma.cu:79)
@@ -1353,6 +1354,12 @@ int cbx_lock_any(cbx_context *c) {
     Replica *r = c->replicas[i];
     if (r->local < 0) continue;
     ++local;
+    if (r->disabled) {
+      // modelmanager.c:217-222: counted, so BSP holds, but not locked and
+      // therefore left out of the step, unlockAny and the clock.
+      ++count;
+      continue;
+    }
     if (pthread_mutex_trylock(&r->lock) == 0) {
       c->locked[i] = 1;
       ++count;
@@ -1846,6 +1853,12 @@ int cbx_replica_get_copy(cbx_context *c, int id) {
 int cbx_replica_set_copy(cbx_context *c, int id, int flag) {
   TRY(check_replica(c, id, false));
   c->replicas[id]->conf.copy = flag ? 1u : 0u;
+  return CBX_OK;
+}
+
+int cbx_replica_set_disabled(cbx_context *c, int id, int flag) {
+  TRY(check_replica(c, id, false));
+  c->replicas[id]->disabled = flag != 0;
   return CBX_OK;
 }
 

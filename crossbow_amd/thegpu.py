@@ -218,6 +218,10 @@ class TheGPU:
     def set_replica_copy(self, id: int, flag: bool) -> None:
         check(self._L.cbx_replica_set_copy(self._ctx, id, 1 if flag else 0))
 
+    def set_replica_disabled(self, id: int, flag: bool) -> None:
+        """Theta-queue disable / enable (thetaqueue.c:182-194): counted, never locked."""
+        check(self._L.cbx_replica_set_disabled(self._ctx, id, 1 if flag else 0))
+
     def replica_device(self, id: int) -> int:
         return check(self._L.cbx_replica_device(self._ctx, id))
 

@@ -192,6 +192,11 @@ int cbx_replica_clock (cbx_context *ctx, int id);
 int cbx_replica_learning_rate (cbx_context *ctx, int id, int task, float *rate);
 int cbx_replica_get_copy (cbx_context *ctx, int id);
 int cbx_replica_set_copy (cbx_context *ctx, int id, int flag);
+/* The scheduler's theta queue disabled (flag 1) or re-enabled (0) a replica
+ * (crossbowThetaQueueDisable / Enable, thetaqueue.c:182-194).  lockAny then
+ * counts it, so BSP still holds, but does not lock it, so the step, unlockAny
+ * and the clock leave it alone (modelmanager.c:217-222).                  */
+int cbx_replica_set_disabled (cbx_context *ctx, int id, int flag);
 /* crossbowKernelOptimiserSMA (kernels/optimisers/sma.cu:3-100), fused into
  * one pass: the replica's local step for task `task`, which produces the
  * snapshot s (replica->diff) and the new w that the next synchronise()

@@ -1,0 +1,188 @@
+/*
+ * abi_driver.c -- drives libcrossbow_sma's C-ABI from plain C, the way the
+ * JNI shim does, through every host-side path: registration, the model
+ * manager, BSP/SSP barriers, SMA / S-SGD / DEFAULT steps, the optimiser
+ * step, pinned staging (serial and pipelined), checkpoint / override,
+ * autotune add / del, BN averaging, timing queries and teardown.
+ *
+ * Built with host-side AddressSanitizer + UndefinedBehaviorSanitizer
+ * (scripts/build_sanitized.sh: -Xarch_host -fsanitize=..., GPU code is not
+ * instrumented) and run on the GPU box by tests/test_gpu_sanitized.py.
+ * Exit status 0 = every call returned as expected and the results are sane.
+ */
+#define _GNU_SOURCE
+#include <math.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <unistd.h>
+
+#include "crossbow_sma.h"
+
+#define CHECK(call)                                                                  \
+	do {                                                                             \
+		int rc_ = (call);                                                            \
+		if (rc_ < 0) {                                                               \
+			fprintf (stderr, "%s:%d %s -> %d: %s\n", __FILE__, __LINE__, #call, rc_,  \
+				cbx_last_error ());                                                  \
+			exit (1);                                                                \
+		}                                                                            \
+	} while (0)
+
+#define EXPECT(cond)                                                                 \
+	do {                                                                             \
+		if (! (cond)) {                                                              \
+			fprintf (stderr, "%s:%d expectation failed: %s\n", __FILE__, __LINE__, #cond); \
+			exit (1);                                                                \
+		}                                                                            \
+	} while (0)
+
+static cbx_context *setup (int n1, int n2, int R, int sync, int type, float momentum) {
+	cbx_context *c = NULL;
+	int dev = 0;
+	CHECK (cbx_init (&c, &dev, 1));
+	int bytes = 4 * (n1 + n2);
+	CHECK (cbx_set_model (c, 2, bytes));
+	int s1[2] = { n1 / 4, 4 }, s2[1] = { n2 };
+	CHECK (cbx_set_model_variable (c, 0, 1, 2, s1, 4 * n1));
+	CHECK (cbx_set_model_variable (c, 1, 1, 1, s2, 4 * n2));
+	float *init = malloc ((size_t) 4 * n1);
+	for (int k = 0; k < n1; ++k) init[k] = 0.001f * (float) (k % 97);
+	CHECK (cbx_set_model_variable_buffer (c, 0, 1, init));
+	free (init);
+	CHECK (cbx_set_model_work_per_clock (c, 2));
+	CHECK (cbx_set_update_model_type (c, type));
+	CHECK (cbx_set_learning_rate_decay_policy_fixed (c, 0.05f));
+	CHECK (cbx_set_momentum (c, momentum, 0));
+	CHECK (cbx_set_weight_decay (c, 1e-4f));
+	CHECK (cbx_set_eamsgd_alpha (c, 0.1f));
+	CHECK (cbx_set_model_manager (c, R, sync));
+	EXPECT (cbx_num_replicas (c) == R);
+	EXPECT (cbx_model_elements (c) == n1 + n2);
+	return c;
+}
+
+static void barrier (cbx_context *c, int clock, int autotune) {
+	CHECK (cbx_lock_any (c));
+	int first = -2;
+	CHECK (cbx_merge (c, 0, &first));
+	CHECK (cbx_synchronise (c, 0, clock, autotune, 0));
+	CHECK (cbx_unlock_any (c));
+}
+
+static int all_finite (const float *p, size_t n) {
+	for (size_t k = 0; k < n; ++k)
+		if (! isfinite (p[k])) return 0;
+	return 1;
+}
+
+int main (void) {
+	int count = 0;
+	CHECK (cbx_device_count (&count));
+	EXPECT (count >= 1);
+	const int n1 = 40000, n2 = 3331, n = n1 + n2, R = 3;
+	float *host = malloc ((size_t) 4 * n);
+
+	/* SMA, BSP, momentum: tasks, barriers, staging, checkpoint, autotune */
+	cbx_context *c = setup (n1, n2, R, CBX_SYNC_BSP, CBX_UPDATE_SMA, 0.9f);
+	CHECK (cbx_fill_synthetic (c, 7));
+	CHECK (cbx_set_timing (c, 1));
+	for (int clock = 1; clock <= 3; ++clock) {
+		for (int i = 0; i < R; ++i) {
+			CHECK (cbx_replica_lock (c, i));
+			CHECK (cbx_replica_optimise (c, i, clock * R + i, NULL));
+			CHECK (cbx_replica_task_done (c, i));
+			CHECK (cbx_replica_unlock (c, i));
+		}
+		barrier (c, clock, 0);
+	}
+	float ms[CBX_T_COUNT];
+	CHECK (cbx_last_timing (c, 0, ms));
+	EXPECT (ms[CBX_T_STEP] > 0);
+	float hist[16];
+	EXPECT (cbx_timing_history (c, 0, CBX_T_KERNEL, hist, 16) >= 3);
+	void *ev = NULL;
+	CHECK (cbx_step_event (c, 0, &ev));
+	EXPECT (ev != NULL);
+	CHECK (cbx_stage_out (c));
+	CHECK (cbx_stage_in (c));
+	CHECK (cbx_lock_any (c));
+	CHECK (cbx_synchronise_staged (c, 0, 4, 0, 5));
+	CHECK (cbx_unlock_any (c));
+	CHECK (cbx_wait (c));
+	void *hz = NULL;
+	CHECK (cbx_base_host_buffer (c, 0, CBX_BUF_DATA, &hz));
+	EXPECT (all_finite ((const float *) hz, (size_t) n));
+	char dir[] = "/tmp/cbx_abi_driverXXXXXX";
+	EXPECT (mkdtemp (dir) != NULL);
+	CHECK (cbx_checkpoint_model (c, dir));
+	CHECK (cbx_base_read (c, 0, CBX_BUF_DATA, host, (size_t) 4 * n));
+	barrier (c, 5, 1);  /* autotune: add one replica per device */
+	EXPECT (cbx_num_replicas (c) == R + 1);
+	barrier (c, 6, -1); /* and delete it again */
+	EXPECT (cbx_num_replicas (c) == R);
+	/* override from the checkpoint written above (its numbered subdirectory) */
+	int rc = cbx_override_model_data (c, dir);
+	(void) rc;  /* the directory layout is checked by the Python tests; here: no crash */
+	float *z2 = malloc ((size_t) 4 * n);
+	CHECK (cbx_base_read (c, 0, CBX_BUF_DATA, z2, (size_t) 4 * n));
+	EXPECT (all_finite (z2, (size_t) n));
+	free (z2);
+	/* error paths keep the context usable */
+	EXPECT (cbx_replica_lock (c, 99) == CBX_ERR_INVALID);
+	EXPECT (cbx_synchronise_staged (c, 0, 7, 0, 0) == CBX_ERR_INVALID);
+	EXPECT (cbx_set_kernel_config (c, 96, 0, 1, 1) == CBX_ERR_INVALID);
+	CHECK (cbx_set_kernel_config (c, 64, 0, 1, 2));
+	CHECK (cbx_set_aux_kernel_config (c, 128, 2, 4));
+	barrier (c, 7, 0);
+	/* BSP failure: a replica held by a task */
+	CHECK (cbx_replica_lock (c, 1));
+	EXPECT (cbx_lock_any (c) == CBX_ERR_BARRIER);
+	CHECK (cbx_replica_unlock (c, 1));
+	CHECK (cbx_replica_set_disabled (c, 2, 1));
+	EXPECT (cbx_lock_any (c) == R);
+	CHECK (cbx_synchronise (c, 0, 8, 0, 0));
+	EXPECT (cbx_unlock_any (c) == R - 1);
+	CHECK (cbx_free (c));
+
+	/* split pipeline over a one-rank communicator, SSP */
+	c = setup (n1, n2, R, CBX_SYNC_SSP, CBX_UPDATE_SYNCHRONOUSEAMSGD, 0.9f);
+	CHECK (cbx_set_force_split (c, 1));
+	CHECK (cbx_set_bucket_elements (c, 8192));
+	CHECK (cbx_replica_lock (c, 0));
+	EXPECT (cbx_lock_any (c) == R - 1);
+	CHECK (cbx_synchronise (c, 0, 1, 0, 0));
+	CHECK (cbx_unlock_any (c));
+	CHECK (cbx_replica_unlock (c, 0));
+	CHECK (cbx_lock_any (c));
+	CHECK (cbx_synchronise_staged (c, 0, 2, 0, 3));
+	CHECK (cbx_unlock_any (c));
+	CHECK (cbx_wait (c));
+	CHECK (cbx_free (c));
+
+	/* S-SGD (WORKER) and DEFAULT, no momentum */
+	for (int type = 0; type < 2; ++type) {
+		c = setup (n1, n2, R, CBX_SYNC_BSP, type == 0 ? CBX_UPDATE_WORKER : CBX_UPDATE_DEFAULT, 0.0f);
+		for (int i = 0; i < R; ++i)
+			CHECK (cbx_replica_optimise (c, i, i, NULL));
+		barrier (c, 1, 0);
+		CHECK (cbx_replica_read (c, 1, CBX_BUF_DATA, host, (size_t) 4 * n));
+		EXPECT (all_finite (host, (size_t) n));
+		CHECK (cbx_free (c));
+	}
+
+	/* BN statistics averaging is a no-op with one device but walks its tables */
+	c = setup (n1, n2, 1, CBX_SYNC_BSP, CBX_UPDATE_SMA, 0.0f);
+	{
+		void *p = NULL;
+		CHECK (cbx_replica_buffer (c, 0, CBX_BUF_GRADIENT, &p));
+		float *mean[2] = { (float *) p, (float *) p + 64 };
+		float *var[2] = { (float *) p + 128, (float *) p + 192 };
+		int elements[2] = { 64, 64 }, updated[2] = { 1, 1 };
+		CHECK (cbx_average_batchnorm_stats (c, 2, elements, mean, var, updated));
+	}
+	CHECK (cbx_free (c));
+	free (host);
+	printf ("abi_driver: ok\n");
+	return 0;
+}

@@ -94,6 +94,40 @@ def test_ssp_partial_lock():
     _run(4099, 4, 0.1, 0.9, held=(1,), sync=1)
 
 
+@pytest.mark.parametrize("split", [False, True])
+def test_disabled_replica_counted_but_excluded(split):
+    # modelmanager.c:217-222: a theta-queue-disabled replica counts toward the
+    # BSP barrier but is not locked, so the step, unlockAny and the clock skip it.
+    n, R = 4099, 4
+    st = O.make_state(n, 1, R, 0.1, 0.9)
+    g = make_gpu(n, R, 0.1, 0.9, sync=0)
+    try:
+        if split:
+            g.set_force_split(True)
+        upload(g, st)
+        g.set_replica_disabled(2, True)
+        assert g.lockAny() == R, "BSP holds: the disabled replica is counted"
+        g.synchronise(0, 5, 0, False)
+        assert g.unlockAny() == R - 1
+        want = st.clone()
+        want.locked[2] = 0
+        O.sma_step(want)
+        g.wait()
+        compare_states(download(g, st), want)
+        assert g.replica_clock(2) == 0 and g.replica_clock(1) == 5
+        # re-enabled, it takes part again
+        g.set_replica_disabled(2, False)
+        assert g.lockAny() == R
+        g.synchronise(0, 6, 0, False)
+        assert g.unlockAny() == R
+        want.locked[2] = 1
+        O.sma_step(want)
+        g.wait()
+        compare_states(download(g, st), want)
+    finally:
+        g.free()
+
+
 def test_bsp_barrier_failure():
     from crossbow_amd import CbxError
     n, R = 1031, 2
