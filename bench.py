@@ -56,7 +56,8 @@ def parse():
     p.add_argument("--waves-per-cu", type=int, default=-1,
                    help="occupancy cap for the SMA kernels: -1 auto (library default), 0 none, else waves per CU")
     p.add_argument("--bucket-mb", type=float, default=0.0,
-                   help="G>1 pipeline bucket (MB of fp32): 0 = library default (8 buckets), <0 = one bucket")
+                   help="G>1 pipeline bucket (MB of fp32): 0 = tuned in the warm-up (dist.tune_buckets), "
+                        "<0 = one bucket")
     p.add_argument("--calib-steps", type=int, default=10,
                    help="G>1: unpipelined steps before warm-up that time kernel A, the all-reduce and kernel B apart")
     p.add_argument("--force-split", action="store_true", help="use kernel A + all-reduce + B even at G=1")
@@ -253,6 +254,10 @@ def main():
                  "apply": list(gpu.timing_history(_lib.T_APPLY)[-k:]),
                  "step": list(gpu.timing_history(_lib.T_STEP)[-k:])}
     gpu.set_bucket_elements(bucket_elems)
+    tuning = None
+    if split and args.bucket_mb == 0:
+        # warm-up autotune of the bucket count on the live communicator (same choice on every rank)
+        bucket_elems, tuning = D.tune_buckets(gpu, n, world, step)
 
     for _ in range(args.warmup):
         step()
@@ -294,6 +299,9 @@ def main():
             "bytes_per_step_per_gpu": step_bytes,
             "parallelism": f"sma-dp{G}",
             "pipeline": "fused" if not split else "accumulate+rccl-allreduce+apply, bucketed on two streams",
+            "buckets": (None if not split else min(tuning, key=lambda k: (tuning[k], k)) if tuning
+                        else -(-n // min(bucket_elems, n)) if bucket_elems else "library default (8)"),
+            "bucket_tuning_ms_per_step": tuning,
             "kernel_config": dict(block=args.block, blocks_per_cu=args.blocks_per_cu, policy=args.policy,
                                   unroll=args.unroll, waves_per_cu=args.waves_per_cu, bucket_mb=args.bucket_mb),
         },

@@ -56,6 +56,43 @@ def max_over_ranks(value: float, world: int) -> float:
     return float(t.item())
 
 
+def tune_buckets(gpu, n: int, world: int, step: Callable[[], None], candidates=(1, 2, 4, 8, 16),
+                 steps: int = 4, warmup: int = 2):
+    """Pick the bucket count of the G > 1 pipeline (kernel A / RCCL
+    all-reduce / kernel B per bucket) by timing each candidate on the live
+    communicator, the way a runtime tunes itself in its warm-up.
+
+    More buckets hide more of the all-reduce behind kernel A, but each bucket
+    costs fixed time (a cross-stream event, a shorter launch's ramp and drain:
+    ~16-20 us per bucket on one MI355X, profiles/r01/split_pipeline_trace.txt),
+    so the best count depends on how long the all-reduce is, i.e. on G and the
+    xGMI links.  Every rank times every candidate, the times are max-reduced
+    over ranks, and all ranks take the same argmin, so the RCCL call sequence
+    stays identical on every rank.  ``step()`` runs one barrier step.
+    Returns (bucket_elements, {candidate: ms_per_step}).
+    """
+    import time
+
+    results = {}
+    for nb in candidates:
+        elems = (1 << 62) if nb <= 1 else max(1, -(-n // nb))
+        gpu.set_bucket_elements(elems)
+        for _ in range(warmup):
+            step()
+        gpu.wait()
+        barrier(world)
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            step()
+        gpu.wait()
+        ms = (time.perf_counter() - t0) * 1e3 / steps
+        results[nb] = max_over_ranks(ms, world)
+    best = min(results, key=lambda k: (results[k], k))
+    elems = (1 << 62) if best <= 1 else max(1, -(-n // best))
+    gpu.set_bucket_elements(elems)
+    return elems, results
+
+
 def local_replicas(size: int, world: int, rank: int):
     """Global replica ids this rank owns (round-robin placement)."""
     return [i for i in range(size) if i % world == rank]

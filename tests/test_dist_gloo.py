@@ -196,3 +196,69 @@ def test_env_rank_defaults(monkeypatch):
     monkeypatch.setenv("WORLD_SIZE", "8")
     monkeypatch.setenv("LOCAL_RANK", "3")
     assert D.env_rank() == (3, 8, 3)
+
+
+class _FakeGpu:
+    """Stands in for TheGPU in tune_buckets: a step 'costs' a rank-dependent
+    time per bucket count (sleep), so the ranks disagree locally."""
+
+    def __init__(self, rank, n):
+        self.rank, self.n, self.elems = rank, n, 0
+
+    def set_bucket_elements(self, e):
+        self.elems = e
+
+    def wait(self):
+        pass
+
+    def step(self):
+        import time
+        nb = 1 if self.elems >= self.n else -(-self.n // self.elems)
+        # rank 0 is fastest at 8 buckets, rank 1 at 2; the max over ranks is lowest at 4
+        cost = {0: {1: 9, 2: 7, 4: 4, 8: 1, 16: 6}, 1: {1: 9, 2: 1, 4: 4, 8: 7, 16: 8}}[self.rank][nb]
+        time.sleep(cost * 2e-3)
+
+
+def _tune_main(rank, world, port, q):
+    import sys
+    sys.path.insert(0, ROOT)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    try:
+        from crossbow_amd import dist as D
+        D.init(world, rank, backend="gloo")
+        g = _FakeGpu(rank, 1000)
+        elems, res = D.tune_buckets(g, 1000, world, g.step, steps=2, warmup=1)
+        q.put((rank, (elems, g.elems, sorted(res)), None))
+        D.finalize(world)
+    except Exception:  # pragma: no cover
+        import traceback
+        q.put((rank, None, traceback.format_exc()))
+
+
+def test_bucket_tuning_agrees_across_ranks():
+    # dist.tune_buckets: every rank must end on the same bucket count (else
+    # the ranks' RCCL call sequences differ and the all-reduce hangs), chosen
+    # by the max-over-ranks step time: 4 buckets here.
+    import torch.multiprocessing as mp
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_tune_main, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = {}
+    try:
+        for _ in range(world):
+            rank, res, err = q.get(timeout=240)
+            out[rank] = (res, err)
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
+    for rank in range(world):
+        assert out[rank][1] is None, out[rank][1]
+    (e0, set0, cands), (e1, set1, _) = out[0][0], out[1][0]
+    assert e0 == e1 == set0 == set1 == 250, (out[0][0], out[1][0])
+    assert cands == [1, 2, 4, 8, 16]
