@@ -2,7 +2,7 @@
 and the signature of every function ``include/crossbow_sma.h`` declares.
 
 Torch-free on purpose, so a process can bind a library build without loading
-PyTorch's HIP runtime and RCCL (``tests/test_gpu_two_rank.py`` loads a build
+PyTorch's HIP runtime and RCCL (``tests/test_gpu_multirank.py`` loads a build
 linked against a loopback collective).  ``crossbow_amd._lib`` is the binding
 the package uses.
 """

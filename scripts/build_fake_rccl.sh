@@ -1,5 +1,5 @@
 #!/bin/bash
-# Test infrastructure for the two-rank-on-one-GPU tests (tests/test_gpu_two_rank.py):
+# Test infrastructure for the two-rank-on-one-GPU tests (tests/test_gpu_multirank.py):
 #   tests/native/libfakerccl.so             loopback stand-in for the RCCL calls the library makes
 #   tests/native/libcrossbow_sma_fakerccl.so the library's own sources linked against it
 # Both git-ignored; they travel to the GPU box with the tree.  Run here, on the CPU.

@@ -16,7 +16,7 @@
 //
 // Built by scripts/build_fake_rccl.sh as tests/native/libfakerccl.so; a
 // variant of the library linked against it (libcrossbow_sma_fakerccl.so) is
-// what tests/test_gpu_two_rank.py loads.  Never linked into the product.
+// what tests/test_gpu_multirank.py loads.  Never linked into the product.
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 

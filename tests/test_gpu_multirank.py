@@ -1,5 +1,5 @@
-"""The library's multi-rank path (cbx_init_rank, G = 2) on ONE GPU, bit for bit
-against the G = 2 oracle.
+"""The library's multi-rank path (cbx_init_rank, G = 2 and 4) on ONE GPU, bit for
+bit against the oracle with the same G.
 
 Two processes each drive the real library sources as rank 0 / rank 1 of a
 two-GPU job, both on device 0.  Real RCCL refuses two ranks on one device,
@@ -194,7 +194,7 @@ def _bn_case(L, A, rank, world, uid):
         g("cbx_set_update_model_type", 7)
         g("cbx_set_model_manager", 1, A.SYNC_BSP)
         elements = [16, 40, 7]
-        updated = [[1, 1, 1], [1, 0, 1]]
+        updated = [[1, 1, 1]] + [[1, 0, 1] if d % 2 else [0, 1, 1] for d in range(1, world)]
         mean = [[O.fill_normal(e, 50 + 10 * d + l, 0.5) for l, e in enumerate(elements)] for d in range(world)]
         var = [[O.fill_normal(e, 90 + 10 * d + l, 0.5) for l, e in enumerate(elements)] for d in range(world)]
         ref_m = [[a.copy() for a in r] for r in mean]
@@ -238,7 +238,7 @@ def _rank_main(rank, world, uids, fake_dir, q):
         A = _abi()
         L = A.bind(ctypes.CDLL(VARIANT))
         out = []
-        for case, uid in zip(CASES, uids):
+        for case, uid in zip(_cases(world), uids):
             out.append((case[0], _case(L, A, rank, world, uid, case)))
         out.append(("bn", _bn_case(L, A, rank, world, uids[-1])))
         q.put((rank, out, None))
@@ -247,10 +247,15 @@ def _rank_main(rank, world, uids, fake_dir, q):
         q.put((rank, None, traceback.format_exc()))
 
 
+def _cases(world):
+    # four ranks: the SMA cases (placement i % 4, Phase D from rank 3, buckets)
+    return CASES if world == 2 else [c for c in CASES if c[0] in ("sma", "sma-copy-ssp", "sma-5-buckets")]
+
+
 @pytest.mark.skipif(not os.path.exists(VARIANT), reason="run scripts/build_fake_rccl.sh first")
-def test_two_ranks_on_one_gpu_bitexact_vs_g2_oracle():
+@pytest.mark.parametrize("world", [2, 4])
+def test_ranks_on_one_gpu_bitexact_vs_oracle(world):
     import multiprocessing as mp
-    world = 2
     uids = [os.urandom(16) + bytes(112) for _ in range(len(CASES) + 1)]
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -273,4 +278,4 @@ def test_two_ranks_on_one_gpu_bitexact_vs_g2_oracle():
         assert err is None, f"rank {rank}:\n{err}"
         failures = [(name, bad) for name, bad in res if bad]
         assert not failures, f"rank {rank}: {failures}"
-        assert [name for name, _ in res] == [c[0] for c in CASES] + ["bn"]
+        assert [name for name, _ in res] == [c[0] for c in _cases(world)] + ["bn"]
