@@ -82,6 +82,42 @@ int main(int argc, char **argv) {
   CK(hipEventCreate(&t2));
   const unsigned grid = (n4 + 255) / 256;
   uint32_t counter = 0;
+  // mode 4: modes 1's pattern captured once into a hipGraph and replayed.
+  hipGraphExec_t gexec = nullptr;
+  {
+    hipEvent_t fork, join;
+    CK(hipEventCreateWithFlags(&fork, hipEventDisableTiming));
+    CK(hipEventCreateWithFlags(&join, hipEventDisableTiming));
+    CK(hipStreamBeginCapture(p, hipStreamCaptureModeGlobal));
+    CK(hipEventRecord(fork, p));
+    CK(hipStreamWaitEvent(c, fork, 0));
+    for (int k = 0; k < nk; ++k) {
+      hipLaunchKernelGGL(produce, dim3(grid), dim3(256), 0, p, in, out, n4, nullptr, 0u, ticket);
+      CK(hipEventRecord(ev[k], p));
+      CK(hipStreamWaitEvent(c, ev[k], 0));
+      hipLaunchKernelGGL(consume, dim3(1), dim3(64), 0, c, small, (uint32_t)k);
+    }
+    CK(hipEventRecord(join, c));
+    CK(hipStreamWaitEvent(p, join, 0));
+    hipGraph_t graph;
+    CK(hipStreamEndCapture(p, &graph));
+    CK(hipGraphInstantiate(&gexec, graph, nullptr, nullptr, 0));
+  }
+  for (int round = 0; round < 3; ++round) {
+    float tot = 0;
+    for (int r = 0; r < reps + 2; ++r) {
+      CK(hipDeviceSynchronize());
+      CK(hipEventRecord(t0, p));
+      CK(hipGraphLaunch(gexec, p));
+      CK(hipEventRecord(t1, p));
+      CK(hipEventSynchronize(t1));
+      float a;
+      CK(hipEventElapsedTime(&a, t0, t1));
+      if (r >= 2) tot += a;
+    }
+    std::printf("{\"round\":%d,\"mode\":\"graph-event\",\"kernels\":%d,\"total_us_per_kernel\":%.2f}\n", round, nk,
+                tot * 1e3 / reps / nk);
+  }
   for (int round = 0; round < 3; ++round)
     for (int mode = 0; mode < 4; ++mode) {
       float prod_ms = 0, tot_ms = 0;
