@@ -420,6 +420,73 @@ __global__ __launch_bounds__(64) void copy_u2(v4f *dst, const v4f *src) {
   }
 }
 
+// ---- v11: load order / store placement variants of the library's fused
+// kernel (64-thread blocks, U = 2 wave-contiguous, nt), under the LDS caps.
+//   LO 0: z, last, then per replica s_r, w_r (the library's order)
+//   LO 1: z, last, all s, all w
+//   LO 2: all s, all w, then z, last
+//   SO 0: all FMAs, then w stores, then last, z (the library's)
+//   SO 1: each w_r stored right after its FMA
+template <int LO, int SO>
+__global__ __launch_bounds__(64) void fused_v11(const Args a) {
+  const uint32_t e0 = blockIdx.x * 128u + (threadIdx.x & 63u);
+  const v4f al = a.alpha, nal = -a.alpha, mb = 0.9f, one = 1.0f, mone = -1.0f;
+  v4f zv[2], lv[2], sv[2][R], wv[2][R];
+  auto ldzl = [&]() {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const uint32_t i = (e0 + 64u * u) * 16u;
+      zv[u] = ldo<1>(a.z, i);
+      lv[u] = ldo<1>(a.last, i);
+    }
+  };
+  if constexpr (LO != 2) ldzl();
+  if constexpr (LO == 0) {
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const uint32_t i = (e0 + 64u * u) * 16u;
+        sv[u][r] = ldo<1>(a.s[r], i);
+        wv[u][r] = ldo<1>(a.w[r], i);
+      }
+  } else {
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+#pragma unroll
+      for (int u = 0; u < 2; ++u) sv[u][r] = ldo<1>(a.s[r], (e0 + 64u * u) * 16u);
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+#pragma unroll
+      for (int u = 0; u < 2; ++u) wv[u][r] = ldo<1>(a.w[r], (e0 + 64u * u) * 16u);
+  }
+  if constexpr (LO == 2) ldzl();
+  __builtin_amdgcn_sched_barrier(0);
+  v4f acc[2] = {0.0f, 0.0f};
+#pragma unroll
+  for (int r = 0; r < R; ++r)
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      v4f d = vfma(mone, zv[u], sv[u][r]);
+      wv[u][r] = vfma(nal, d, wv[u][r]);
+      acc[u] = vfma(al, d, acc[u]);
+      if constexpr (SO == 1) sto<1>(a.w[r], (e0 + 64u * u) * 16u, wv[u][r]);
+    }
+  if constexpr (SO == 0) {
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+#pragma unroll
+      for (int u = 0; u < 2; ++u) sto<1>(a.w[r], (e0 + 64u * u) * 16u, wv[u][r]);
+  }
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const uint32_t i = (e0 + 64u * u) * 16u;
+    v4f D = vfma(mb, lv[u], acc[u]);
+    sto<1>(a.last, i, D);
+    sto<1>(a.z, i, vfma(one, D, zv[u]));
+  }
+}
+
 int main(int argc, char **argv) {
   const int64_t n = 25557032;
   const uint32_t n4 = (uint32_t)(((n + 3) / 4 + 1023) / 1024 * 1024);
@@ -616,6 +683,36 @@ int main(int argc, char **argv) {
     return 0;
   }
 
+  if (argc > 2 && std::strcmp(argv[2], "v11") == 0) {
+    const size_t stride = (buf + (2u << 20) - 1) / (2u << 20) * (2u << 20) + 4096;
+    Args a;
+    a.z = (v4f *)arena;
+    a.last = (v4f *)(arena + stride);
+    for (int r = 0; r < R; ++r) {
+      a.s[r] = (const v4f *)(arena + (2 + 2 * r) * stride);
+      a.w[r] = (v4f *)(arena + (3 + 2 * r) * stride);
+    }
+    a.n4 = n4;
+    a.alpha = 0.1f;
+    hipLaunchKernelGGL(fillk, dim3(8192), dim3(256), 0, 0, (uint32_t *)arena, nbuf * stride / 4, 12345u);
+    CK(hipDeviceSynchronize());
+    const unsigned grid = n4 / 128;
+    for (int round = 0; round < 3; ++round)
+      for (int cap : {2, 3}) {
+        const unsigned lds = (160u / (unsigned)(cap + 1) + 1u) * 1024u;
+        auto go = [&](auto kern, int lo, int so) {
+          float t = time_ms([&] { hipLaunchKernelGGL(kern, dim3(grid), dim3(64), lds, 0, a); }, iters);
+          std::printf("{\"v11\":%d,\"cap\":%d,\"LO\":%d,\"SO\":%d,\"ms\":%.4f,\"GBs\":%.1f}\n", round, cap, lo, so, t,
+                      alg / t / 1e6);
+        };
+        go(fused_v11<0, 0>, 0, 0);
+        go(fused_v11<1, 0>, 1, 0);
+        go(fused_v11<2, 0>, 2, 0);
+        go(fused_v11<0, 1>, 0, 1);
+        go(fused_v11<1, 1>, 1, 1);
+      }
+    return 0;
+  }
   if (argc > 2 && std::strcmp(argv[2], "v10") == 0) {
     const size_t stride = (buf + (2u << 20) - 1) / (2u << 20) * (2u << 20) + 4096;
     Args a;
