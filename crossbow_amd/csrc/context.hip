@@ -244,6 +244,9 @@ struct cbx_context {
   cbx::LaunchConfig cfg;
   // Optimiser step and S-SGD kernels (one float4 stream per buffer, few reads).
   cbx::LaunchConfig aux_cfg = cbx::aux_launch_config();
+  // Write-heavy barrier kernels of DEFAULT and S-SGD (scripts/barrier_sweep.py).
+  cbx::LaunchConfig broadcast_cfg = cbx::broadcast_launch_config();
+  cbx::LaunchConfig ssgd_apply_cfg = cbx::ssgd_apply_launch_config();
   int64_t bucket_elems = 0;
   bool force_split = false;
   bool last_step_split = false;
@@ -917,7 +920,7 @@ int ssgd_step(cbx_context *c, int first) {
   for (size_t k = 0; k < c->devs.size(); ++k) {
     Device &d = c->devs[k];
     HIP_TRY(hipSetDevice(d.hip_id));
-    cbx::LaunchConfig cfg = c->aux_cfg;
+    cbx::LaunchConfig cfg = c->ssgd_apply_cfg;
     cfg.num_cus = d.num_cus;
     cbx::Timing t;
     if (!split) t.start = ring_event(c, d, EV_START);
@@ -1660,7 +1663,7 @@ static int default_step(cbx_context *c, int first) {
   a.z = reinterpret_cast<cbx::v4f *>(base_dev(c, d, CBX_BUF_DATA));
   a.n4 = c->n4;
   HIP_TRY(hipSetDevice(d.hip_id));
-  cbx::LaunchConfig cfg = c->aux_cfg;
+  cbx::LaunchConfig cfg = c->broadcast_cfg;
   cfg.num_cus = d.num_cus;
   cfg.blocks_per_cu = 0;
   HIP_TRY(cbx::launch_broadcast(a, cfg, d.stream, {ring_event(c, d, EV_START), step_stop_event(c, d, EV_A)}));
@@ -2150,6 +2153,21 @@ int cbx_set_aux_kernel_config(cbx_context *c, int block, int unroll, int waves_p
   c->aux_cfg.block = block;
   c->aux_cfg.unroll = unroll;
   c->aux_cfg.waves_per_cu = waves_per_cu;
+  return CBX_OK;
+}
+
+int cbx_set_barrier_kernel_config(cbx_context *c, int block, int unroll, int waves_per_cu) {
+  TRY(check_ctx(c));
+  if (block < 64 || block > 512 || block % 64 != 0) return fail(CBX_ERR_INVALID, "block must be 64..512, multiple of 64");
+  if (unroll != 1 && unroll != 2) return fail(CBX_ERR_INVALID, "unroll must be 1 or 2");
+  if ((int64_t)block * unroll > cbx::kPadFloat4 || cbx::kPadFloat4 % ((int64_t)block * unroll) != 0)
+    return fail(CBX_ERR_INVALID, "block*unroll must divide %lld", (long long)cbx::kPadFloat4);
+  if (waves_per_cu < -1 || waves_per_cu > 32) return fail(CBX_ERR_INVALID, "waves per CU must be -1 (auto) or 0..32");
+  for (cbx::LaunchConfig *cfg : {&c->broadcast_cfg, &c->ssgd_apply_cfg}) {
+    cfg->block = block;
+    cfg->unroll = unroll;
+    cfg->waves_per_cu = waves_per_cu;
+  }
   return CBX_OK;
 }
 

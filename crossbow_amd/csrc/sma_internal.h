@@ -73,6 +73,26 @@ inline LaunchConfig aux_launch_config() {
   return c;
 }
 
+// The write-heavy barrier kernels (scripts/barrier_sweep.py, ResNet-50, R = 8):
+// the DEFAULT broadcast (1 read + R writes) is fastest with 256-thread blocks
+// at 8 waves per CU (148 us vs 174 us at the per-task shape), the S-SGD apply
+// (3 reads + R + 3 writes) with one-wave blocks, two float4 per lane, 3 waves
+// per CU (229 us vs 252 us).
+inline LaunchConfig broadcast_launch_config() {
+  LaunchConfig c;
+  c.block = 256;
+  c.unroll = 1;
+  c.waves_per_cu = 8;
+  return c;
+}
+inline LaunchConfig ssgd_apply_launch_config() {
+  LaunchConfig c;
+  c.block = 64;
+  c.unroll = 2;
+  c.waves_per_cu = 3;
+  return c;
+}
+
 // Waves per CU for a kernel whose lanes stream `reads` + `writes` buffers:
 // 2 for the R = 8 SMA step (18 + 10), 8 for the optimiser step (3 + 4),
 // 11 for kernel B (3 + 2).

@@ -319,8 +319,11 @@ class TheGPU:
     def set_kernel_occupancy(self, waves_per_cu: int) -> None:
         check(self._L.cbx_set_kernel_occupancy(self._ctx, waves_per_cu))
 
-    def set_aux_kernel_config(self, block: int = 128, unroll: int = 1, waves_per_cu: int = -1) -> None:
+    def set_aux_kernel_config(self, block: int = 64, unroll: int = 1, waves_per_cu: int = -1) -> None:
         check(self._L.cbx_set_aux_kernel_config(self._ctx, block, unroll, waves_per_cu))
+
+    def set_barrier_kernel_config(self, block: int, unroll: int, waves_per_cu: int) -> None:
+        check(self._L.cbx_set_barrier_kernel_config(self._ctx, block, unroll, waves_per_cu))
 
     def set_bucket_elements(self, elements: int) -> None:
         check(self._L.cbx_set_bucket_elements(self._ctx, elements))

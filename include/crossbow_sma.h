@@ -283,6 +283,10 @@ int cbx_set_kernel_occupancy (cbx_context *ctx, int waves_per_cu);
  * the S-SGD task/barrier kernels): threads per block (64..512, multiple of
  * 64), float4s per lane (1 or 2), occupancy cap in waves per CU as above. */
 int cbx_set_aux_kernel_config (cbx_context *ctx, int block, int unroll, int waves_per_cu);
+/* Launch geometry of the write-heavy barrier kernels (the DEFAULT broadcast
+ * and the S-SGD apply), same arguments as above; defaults are per kernel
+ * (256 / 1 / 8 and 64 / 2 / 3, measured).                                */
+int cbx_set_barrier_kernel_config (cbx_context *ctx, int block, int unroll, int waves_per_cu);
 /* Bucketed pipeline for G > 1: kernel A / all-reduce / kernel B per bucket
  * of `bucket_elements` floats; 0 (default) = 8 buckets when G > 1, one at
  * G = 1; a value >= n = one bucket, all in order on the sync stream.  With

@@ -184,6 +184,7 @@ def test_ssgd_clock_loop_bitexact(momentum, split, aux):
         g.setModelManager(R, 1)  # SSP: the barrier may skip a busy replica
         if aux:
             g.set_aux_kernel_config(*aux)
+            g.set_barrier_kernel_config(*aux)
         if split:
             g.set_force_split(True)
         st = O.make_state(n, 1, R, 0.1, momentum)
@@ -240,6 +241,7 @@ def test_default_clock_loop_bitexact(momentum, on_torch_stream, aux):
         g.setModelManager(R, 1)
         if aux:
             g.set_aux_kernel_config(*aux)
+            g.set_barrier_kernel_config(*aux)
         st = O.make_state(n, 1, R, 0.1, momentum)
         st.locked[2] = 0
         upload(g, st)
