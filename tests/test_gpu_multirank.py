@@ -232,6 +232,60 @@ def _bn_case(L, A, rank, world, uid):
         L.cbx_free(c)
 
 
+def _autotune_case(L, A, rank, world, uid):
+    # synchronise(autotune = +1 / -1) adds / deletes one replica per device
+    # after the step (executioncontext.c:2321-2328, modelmanager.c:362-557):
+    # a new replica copies its device's first replica and joins the next step.
+    import sys
+    sys.path.insert(0, ROOT)
+    from oracle import oracle as O
+    n, R, mom = 30_011, 2, 0.9
+    c = ctypes.c_void_p()
+    ub = (ctypes.c_ubyte * 128).from_buffer_copy(uid)
+    if L.cbx_init_rank(ctypes.byref(c), 0, world, rank, ub) < 0:
+        raise RuntimeError(L.cbx_last_error().decode())
+    g = _Rank(L, A, c)
+    try:
+        shape = (ctypes.c_int * 1)(n)
+        g("cbx_set_model", 1, 4 * n)
+        g("cbx_set_model_variable", 0, 1, 1, shape, 4 * n)
+        g("cbx_set_update_model_type", 7)
+        g("cbx_set_eamsgd_alpha", ctypes.c_float(0.1))
+        g("cbx_set_momentum", ctypes.c_float(mom), 0)
+        g("cbx_set_model_manager", R, A.SYNC_BSP)
+        st = O.make_state(n, world, R, 0.1, mom)
+        g.write("cbx_base_write", rank, A.BUF_DATA, st.z[rank])
+        g.write("cbx_base_write", rank, A.BUF_LAST, st.last[rank])
+        for i in range(st.size):
+            if i % world == rank:
+                g.write("cbx_replica_write", i, A.BUF_DIFF, st.s[i])
+                g.write("cbx_replica_write", i, A.BUF_DATA, st.w[i])
+        for step, tune in enumerate((1, 0, -1, 0)):
+            g("cbx_lock_any")
+            g("cbx_synchronise", 0, step + 1, tune, 0)
+            g("cbx_unlock_any")
+            O.sma_step(st)
+            s, w = list(st.s), list(st.w)
+            if tune > 0:
+                s += [st.s[d].copy() for d in range(world)]
+                w += [st.w[d].copy() for d in range(world)]
+            elif tune < 0:
+                s, w = s[:-world], w[:-world]
+            st = O.SmaState(world, len(s), n, 0.1, mom, st.z, st.last, s, w)
+            assert g("cbx_num_replicas") == st.size
+        g("cbx_wait")
+        bad = []
+        for what, got, want in [("z", g.read("cbx_base_read", rank, A.BUF_DATA, n), st.z[rank]),
+                                ("last", g.read("cbx_base_read", rank, A.BUF_LAST, n), st.last[rank])] + \
+                [(f"w[{i}]", g.read("cbx_replica_read", i, A.BUF_DATA, n), st.w[i])
+                 for i in range(st.size) if i % world == rank]:
+            if not np.array_equal(got.view(np.uint32), want.view(np.uint32)):
+                bad.append(f"autotune {what} differs")
+        return bad
+    finally:
+        L.cbx_free(c)
+
+
 def _rank_main(rank, world, uids, fake_dir, q):
     os.environ["FAKE_RCCL_DIR"] = fake_dir
     try:
@@ -240,7 +294,8 @@ def _rank_main(rank, world, uids, fake_dir, q):
         out = []
         for case, uid in zip(_cases(world), uids):
             out.append((case[0], _case(L, A, rank, world, uid, case)))
-        out.append(("bn", _bn_case(L, A, rank, world, uids[-1])))
+        out.append(("bn", _bn_case(L, A, rank, world, uids[-2])))
+        out.append(("autotune", _autotune_case(L, A, rank, world, uids[-1])))
         q.put((rank, out, None))
     except Exception:  # pragma: no cover - reported to the parent
         import traceback
@@ -256,7 +311,7 @@ def _cases(world):
 @pytest.mark.parametrize("world", [2, 4])
 def test_ranks_on_one_gpu_bitexact_vs_oracle(world):
     import multiprocessing as mp
-    uids = [os.urandom(16) + bytes(112) for _ in range(len(CASES) + 1)]
+    uids = [os.urandom(16) + bytes(112) for _ in range(len(CASES) + 2)]
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     with tempfile.TemporaryDirectory() as fake_dir:
@@ -278,4 +333,4 @@ def test_ranks_on_one_gpu_bitexact_vs_oracle(world):
         assert err is None, f"rank {rank}:\n{err}"
         failures = [(name, bad) for name, bad in res if bad]
         assert not failures, f"rank {rank}: {failures}"
-        assert [name for name, _ in res] == [c[0] for c in _cases(world)] + ["bn"]
+        assert [name for name, _ in res] == [c[0] for c in _cases(world)] + ["bn", "autotune"]
