@@ -565,3 +565,67 @@ def test_step_event_covers_the_step(mode, timing):
         assert_bitexact(out, want.z[0], "z after the step event")
     finally:
         g.free()
+
+
+def test_concurrent_task_threads_and_barrier():
+    # The reference's threading: task threads lock a replica,
+    # run its optimiser step and release it, while the result-collector
+    # thread runs lockAny / synchronise / unlockAny.  Under SSP the barrier
+    # skips replicas a task holds.  Stress that interleaving through the
+    # C-ABI from Python threads (ctypes releases the GIL) and check the
+    # invariants: no error, every replica unlocked at the end, all values
+    # finite, clocks never ahead of the barrier.
+    import threading
+
+    from crossbow_amd import BUF_DATA, TheGPU
+    n, R, workers, iters, barriers = 65_536, 6, 3, 40, 30
+    g = TheGPU()
+    g.init([0])
+    errors = []
+    try:
+        g.setModel(1, 4 * n)
+        g.setModelVariable(0, 1, [n], 4 * n)
+        g.setUpdateModelType(7)
+        g.setEamsgdAlpha(0.1)
+        g.setMomentum(0.9, 0)
+        g.setWeightDecay(1e-4)
+        g.setLearningRateDecayPolicyFixed(0.01)
+        g.setModelManager(R, 1)  # SSP
+        g.fill_synthetic(3)
+
+        def worker(k):
+            try:
+                task = k * 1000
+                for it in range(iters):
+                    i = (k + it * workers) % R
+                    g.replica_lock(i)
+                    try:
+                        g.replica_optimise(i, task)
+                        g.replica_task_done(i)
+                    finally:
+                        g.replica_unlock(i)
+                    task += 1
+            except Exception as e:  # pragma: no cover - reported below
+                errors.append(repr(e))
+
+        threads = [threading.Thread(target=worker, args=(k,)) for k in range(workers)]
+        for t in threads:
+            t.start()
+        for clock in range(1, barriers + 1):
+            locked = g.lockAny()
+            assert 0 <= locked <= R
+            g.synchronise(0, clock, 0, False)
+            g.unlockAny()
+        for t in threads:
+            t.join(timeout=60)
+        assert not errors, errors
+        g.wait()
+        assert g.lockAny() == R, "every replica is free again"
+        g.synchronise(0, barriers + 1, 0, False)
+        g.unlockAny()
+        g.wait()
+        for i in range(R):
+            assert np.isfinite(g.replica_read(i, BUF_DATA)).all()
+            assert g.replica_clock(i) == barriers + 1
+    finally:
+        g.free()
