@@ -255,9 +255,10 @@ def main():
                  "step": list(gpu.timing_history(_lib.T_STEP)[-k:])}
     gpu.set_bucket_elements(bucket_elems)
     tuning = None
+    pipeline_mode = 0
     if split and args.bucket_mb == 0:
         # warm-up autotune of the bucket count on the live communicator (same choice on every rank)
-        bucket_elems, tuning = D.tune_buckets(gpu, n, world, step)
+        bucket_elems, pipeline_mode, tuning = D.tune_buckets(gpu, n, world, step)
 
     for _ in range(args.warmup):
         step()
@@ -299,8 +300,9 @@ def main():
             "bytes_per_step_per_gpu": step_bytes,
             "parallelism": f"sma-dp{G}",
             "pipeline": "fused" if not split else "accumulate+rccl-allreduce+apply, bucketed on two streams",
-            "buckets": (None if not split else min(tuning, key=lambda k: (tuning[k], k)) if tuning
+            "buckets": (None if not split else int(min(tuning, key=lambda k: tuning[k]).split("/")[0]) if tuning
                         else -(-n // min(bucket_elems, n)) if bucket_elems else "library default (8)"),
+            "pipeline_mode": None if not split else pipeline_mode,
             "bucket_tuning_ms_per_step": tuning,
             "kernel_config": dict(block=args.block, blocks_per_cu=args.blocks_per_cu, policy=args.policy,
                                   unroll=args.unroll, waves_per_cu=args.waves_per_cu, bucket_mb=args.bucket_mb),

@@ -25,6 +25,7 @@
 #include <errno.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
@@ -190,6 +191,17 @@ struct Device {
   std::vector<hipEvent_t> stage_k;        // per bucket: outputs computed
   std::vector<hipEvent_t> bucket_acc;  // per bucket: kernel A done (stream -> comm_stream)
   std::vector<hipEvent_t> bucket_red;  // per bucket: all-reduce done (comm_stream -> stream)
+  // Cross-step pipeline (cbx_set_pipeline_mode 1): kernels A run on a_stream,
+  // kernels B stay on `stream`; bucket_b[k] marks B(k) done, which A(k) of
+  // the next step waits for instead of the whole previous step.
+  hipStream_t a_stream = nullptr;
+  std::vector<hipEvent_t> bucket_b;
+  hipEvent_t cross_entry = nullptr;
+  float *decision = nullptr;           // 2 floats: the Phase-D decision, by step parity
+  bool cross_valid = false;            // the last step was cross-pipelined ...
+  int64_t cross_nb = 0;                // ... over this many buckets ...
+  unsigned long long cross_foreign = 0;  // ... and nothing else was enqueued since
+  unsigned cross_parity = 0;
   ncclComm_t comm = nullptr;
   cbx::BnSegment *bn_table = nullptr;  // batch-norm averaging: segment table (device)
   size_t bn_table_bytes = 0;
@@ -250,6 +262,11 @@ struct cbx_context {
   int64_t bucket_elems = 0;
   bool force_split = false;
   bool last_step_split = false;
+  int pipeline_mode = 0;  // 0 bucketed within a step, 1 across steps (G > 1 split path)
+  // Bumped by every C-ABI call that may enqueue work on a sync stream other
+  // than the barrier path itself: a cross-step pipelined step then joins the
+  // whole sync stream instead of waiting bucket by bucket.
+  std::atomic<unsigned long long> foreign_ops{0};
 };
 
 namespace {
@@ -325,14 +342,36 @@ float *replica_host(const Device &d, const Replica &r, int kind) {
   return slot_ptr(d.host, d, slot_index_replica(r.slot, kind), false);
 }
 
-int check_ctx(cbx_context *c) {
+// The *_q checks are for calls that enqueue no device work (the barrier path,
+// replica locks, queries); the others also count a possible foreign op.
+int check_ctx_q(cbx_context *c) {
   if (!c) return fail(CBX_ERR_INVALID, "null context");
   return CBX_OK;
 }
 
-int check_manager(cbx_context *c) {
-  TRY(check_ctx(c));
+int check_ctx(cbx_context *c) {
+  TRY(check_ctx_q(c));
+  c->foreign_ops.fetch_add(1, std::memory_order_relaxed);
+  return CBX_OK;
+}
+
+int check_manager_q(cbx_context *c) {
+  TRY(check_ctx_q(c));
   if (!c->manager) return fail(CBX_ERR_STATE, "model manager not created (call cbx_set_model_manager)");
+  return CBX_OK;
+}
+
+int check_manager(cbx_context *c) {
+  TRY(check_manager_q(c));
+  c->foreign_ops.fetch_add(1, std::memory_order_relaxed);
+  return CBX_OK;
+}
+
+int check_replica_q(cbx_context *c, int id, bool need_local) {
+  TRY(check_manager_q(c));
+  if (id < 0 || id >= c->size) return fail(CBX_ERR_INVALID, "replica id %d out of range [0, %d)", id, c->size);
+  if (need_local && c->replicas[id]->local < 0)
+    return fail(CBX_ERR_INVALID, "replica %d lives in another process (device %d)", id, c->replicas[id]->g);
   return CBX_OK;
 }
 
@@ -413,6 +452,11 @@ void close_device(Device &d) {
   for (hipEvent_t e : d.ring) (void)hipEventDestroy(e);
   for (hipEvent_t e : d.bucket_acc) (void)hipEventDestroy(e);
   for (hipEvent_t e : d.bucket_red) (void)hipEventDestroy(e);
+  if (d.a_stream) (void)hipStreamSynchronize(d.a_stream);
+  for (hipEvent_t e : d.bucket_b) (void)hipEventDestroy(e);
+  if (d.cross_entry) (void)hipEventDestroy(d.cross_entry);
+  if (d.decision) (void)hipFree(d.decision);
+  if (d.a_stream) (void)hipStreamDestroy(d.a_stream);
   for (hipStream_t st : {d.h2d_stream, d.d2h_stream})
     if (st) (void)hipStreamSynchronize(st);
   for (hipEvent_t e : d.stage_h2d) (void)hipEventDestroy(e);
@@ -574,6 +618,7 @@ int sma_step(cbx_context *c, int first) {
     HIP_TRY(cbx::launch_sma_fused(args[0], mom, copies_total > 0, cfg, d.stream,
                                   {ring_event(c, d, EV_START), step_stop_event(c, d, EV_A)}));
     ring_advance(c, d, 0);
+    d.cross_valid = false;
     c->last_step_split = false;
   } else {
     // G > 1: kernel A, grouped RCCL all-reduce of acc (+ control block),
@@ -592,16 +637,44 @@ int sma_step(cbx_context *c, int first) {
     if (b4 <= 0 || b4 > c->n4) b4 = c->n4;
     const int64_t nb = (c->n4 + b4 - 1) / b4;
     const bool pipelined = nb > 1;
+    // Cross-step mode (cbx_set_pipeline_mode 1): kernels A on a_stream, B on
+    // the sync stream.  A(k) waits only for B(k) of the previous step, so the
+    // next step's first buckets run while this step's last all-reduces are
+    // still on the link:
+    //   a_stream    : [wait b(0)'] A(0) [wait b(1)'] A(1) ...
+    //   comm_stream : [wait acc(0)] AR(0) [wait acc(1)] AR(1) ...
+    //   stream      : [wait red(0)] B(0) [wait red(1)] B(1) ...
+    // A step joins the whole sync stream instead when anything else was
+    // enqueued since the last cross-pipelined step (foreign_ops).
+    const bool cross = pipelined && c->pipeline_mode == 1;
+    const unsigned long long foreign = c->foreign_ops.load(std::memory_order_relaxed);
+    std::vector<char> join(c->devs.size(), 1);
     for (size_t k = 0; k < c->devs.size(); ++k) {
       Device &d = c->devs[k];
       HIP_TRY(hipSetDevice(d.hip_id));
       if (pipelined) {
         while ((int64_t)d.bucket_acc.size() < nb) {
-          hipEvent_t ea, er;
+          hipEvent_t ea, er, eb;
           HIP_TRY(hipEventCreateWithFlags(&ea, hipEventDisableTiming));
           HIP_TRY(hipEventCreateWithFlags(&er, hipEventDisableTiming));
+          HIP_TRY(hipEventCreateWithFlags(&eb, hipEventDisableTiming));
           d.bucket_acc.push_back(ea);
           d.bucket_red.push_back(er);
+          d.bucket_b.push_back(eb);
+        }
+      }
+      if (cross) {
+        if (!d.a_stream) {
+          HIP_TRY(hipStreamCreateWithFlags(&d.a_stream, hipStreamNonBlocking));
+          HIP_TRY(hipEventCreateWithFlags(&d.cross_entry, hipEventDisableTiming));
+          HIP_TRY(hipMalloc(reinterpret_cast<void **>(&d.decision), 256));
+          HIP_TRY(hipMemsetAsync(d.decision, 0, 256, d.stream));
+          d.cross_valid = false;
+        }
+        join[k] = !d.cross_valid || d.cross_nb != nb || d.cross_foreign != foreign;
+        if (join[k]) {
+          HIP_TRY(hipEventRecord(d.cross_entry, d.stream));
+          HIP_TRY(hipStreamWaitEvent(d.a_stream, d.cross_entry, 0));
         }
       }
     }
@@ -652,8 +725,10 @@ int sma_step(cbx_context *c, int first) {
         cbx::Timing t;
         if (b == 0) t.start = ring_event(c, d, EV_START);
         if (!pipelined) t.stop = ring_event(c, d, EV_A);
-        HIP_TRY(cbx::launch_sma_accumulate(offset_args(args[k], start, len), b == 0, cfg, d.stream, t));
-        if (pipelined) HIP_TRY(hipEventRecord(d.bucket_acc[b], d.stream));
+        hipStream_t st = cross ? d.a_stream : d.stream;
+        if (cross && !join[k]) HIP_TRY(hipStreamWaitEvent(st, d.bucket_b[b], 0));  // B(b) of the last step
+        HIP_TRY(cbx::launch_sma_accumulate(offset_args(args[k], start, len), b == 0, cfg, st, t));
+        if (pipelined) HIP_TRY(hipEventRecord(d.bucket_acc[b], st));
       }
       return CBX_OK;
     };
@@ -668,7 +743,16 @@ int sma_step(cbx_context *c, int first) {
         cfg.num_cus = d.num_cus;
         cbx::Timing t;
         if (b == nb - 1) t.stop = step_stop_event(c, d, EV_B);
-        HIP_TRY(cbx::launch_sma_apply(offset_args(args[k], start, len), mom, cfg, d.stream, t));
+        cbx::SmaArgs a = offset_args(args[k], start, len);
+        if (cross) {
+          // The next step's AR(0) may overwrite D's control block before this
+          // step's later buckets run: B(0) publishes the Phase-D decision to a
+          // per-parity slot that B(1..) read.
+          a.decision_mode = b == 0 ? 1 : 2;
+          a.decision = d.decision + (d.cross_parity & 1u);
+        }
+        HIP_TRY(cbx::launch_sma_apply(a, mom, cfg, d.stream, t));
+        if (cross) HIP_TRY(hipEventRecord(d.bucket_b[b], d.stream));
       }
       return CBX_OK;
     };
@@ -680,6 +764,12 @@ int sma_step(cbx_context *c, int first) {
         TRY(mark(c, d, EV_AR));
       }
       TRY(apply(0));
+    } else if (cross) {
+      for (int64_t b = 0; b < nb; ++b) {
+        TRY(accumulate(b));
+        TRY(allreduce(b, true));
+        TRY(apply(b));
+      }
     } else {
       for (int64_t b = 0; b < nb; ++b) {
         TRY(accumulate(b));
@@ -690,7 +780,15 @@ int sma_step(cbx_context *c, int first) {
       // (comm_stream is in order) back into the sync stream.
       TRY(apply(nb - 1));
     }
-    for (Device &d : c->devs) ring_advance(c, d, pipelined ? 2 : 1);
+    for (Device &d : c->devs) {
+      ring_advance(c, d, pipelined ? 2 : 1);
+      d.cross_valid = cross;
+      if (cross) {
+        d.cross_nb = nb;
+        d.cross_foreign = foreign;
+        d.cross_parity ^= 1u;
+      }
+    }
     c->last_step_split = true;
   }
 
@@ -1349,7 +1447,7 @@ int cbx_set_model_manager(cbx_context *c, int replicas, int type) {
 
 // ---- barrier path ---------------------------------------------------------
 int cbx_lock_any(cbx_context *c) {
-  TRY(check_manager(c));
+  TRY(check_manager_q(c));
   // modelmanager.c:212-231: trylock every replica this process owns.
   int count = 0, local = 0;
   for (int i = 0; i < c->size; ++i) {
@@ -1385,7 +1483,7 @@ int cbx_lock_any(cbx_context *c) {
 
 int cbx_merge(cbx_context *c, int pull, int *first_out) {
   (void)pull;
-  TRY(check_manager(c));
+  TRY(check_manager_q(c));
   if (!first_out) return fail(CBX_ERR_INVALID, "null merge result");
   // executioncontext.c:2219-2245
   int N = 0;
@@ -1409,7 +1507,7 @@ static int default_step(cbx_context *c, int first);
 // staged: 0 = device-resident step; > 0 = host-staged step over that many
 // buckets (cbx_synchronise_staged).
 static int synchronise_impl(cbx_context *c, int first, int clock, int autotune, int staged) {
-  TRY(check_manager(c));
+  TRY(check_manager_q(c));
   if (first < 0 || first > c->size) return fail(CBX_ERR_INVALID, "first replica %d out of range", first);
   // executioncontext.c:2287-2315: SYNCHRONOUSEAMSGD (3) routes to SMA because
   // ELASTIC_AVERAGE is #undef'd; SMA is 7.  The other update models are not
@@ -1417,6 +1515,10 @@ static int synchronise_impl(cbx_context *c, int first, int clock, int autotune, 
   // WORKER (1) is synchronous SGD (executioncontext.c:2277-2279), which shares
   // the base-model buffers and the all-reduce.
   const int type = c->model.type;
+  if (staged || (type != CBX_UPDATE_SMA && type != CBX_UPDATE_SYNCHRONOUSEAMSGD)) {
+    c->foreign_ops.fetch_add(1, std::memory_order_relaxed);
+    for (Device &d : c->devs) d.cross_valid = false;
+  }
   if (type == CBX_UPDATE_WORKER || type == CBX_UPDATE_DEFAULT) {
     if (staged) TRY(cbx_stage_in(c));
     TRY(type == CBX_UPDATE_WORKER ? ssgd_step(c, first) : default_step(c, first));
@@ -1449,7 +1551,7 @@ int cbx_synchronise_staged(cbx_context *c, int first, int clock, int autotune, i
 }
 
 int cbx_unlock_any(cbx_context *c) {
-  TRY(check_manager(c));
+  TRY(check_manager_q(c));
   int count = 0;
   for (int i = 0; i < c->size; ++i)
     if (c->locked[i]) {
@@ -1820,78 +1922,78 @@ int cbx_average_batchnorm_stats(cbx_context *c, int layers, const int *elements,
 
 // ---- task-side replica access ---------------------------------------------
 int cbx_replica_lock(cbx_context *c, int id) {
-  TRY(check_replica(c, id, true));
+  TRY(check_replica_q(c, id, true));
   pthread_mutex_lock(&c->replicas[id]->lock);
   return CBX_OK;
 }
 
 int cbx_replica_unlock(cbx_context *c, int id) {
-  TRY(check_replica(c, id, true));
+  TRY(check_replica_q(c, id, true));
   pthread_mutex_unlock(&c->replicas[id]->lock);
   return CBX_OK;
 }
 
 int cbx_replica_task_done(cbx_context *c, int id) {
-  TRY(check_replica(c, id, true));
+  TRY(check_replica_q(c, id, true));
   c->replicas[id]->updates++;
   return CBX_OK;
 }
 
 int cbx_replica_clock(cbx_context *c, int id) {
-  TRY(check_replica(c, id, false));
+  TRY(check_replica_q(c, id, false));
   return c->replicas[id]->clock;
 }
 
 int cbx_replica_learning_rate(cbx_context *c, int id, int task, float *rate) {
-  TRY(check_replica(c, id, false));
+  TRY(check_replica_q(c, id, false));
   if (!rate) return fail(CBX_ERR_INVALID, "null rate");
   return c->replicas[id]->conf.learning_rate(task, rate);
 }
 
 int cbx_replica_get_copy(cbx_context *c, int id) {
-  TRY(check_replica(c, id, false));
+  TRY(check_replica_q(c, id, false));
   return (int)c->replicas[id]->conf.copy;
 }
 
 int cbx_replica_set_copy(cbx_context *c, int id, int flag) {
-  TRY(check_replica(c, id, false));
+  TRY(check_replica_q(c, id, false));
   c->replicas[id]->conf.copy = flag ? 1u : 0u;
   return CBX_OK;
 }
 
 int cbx_replica_set_disabled(cbx_context *c, int id, int flag) {
-  TRY(check_replica(c, id, false));
+  TRY(check_replica_q(c, id, false));
   c->replicas[id]->disabled = flag != 0;
   return CBX_OK;
 }
 
 int cbx_replica_device(cbx_context *c, int id) {
-  TRY(check_replica(c, id, false));
+  TRY(check_replica_q(c, id, false));
   return c->replicas[id]->g;
 }
 
 int cbx_replica_is_local(cbx_context *c, int id) {
-  TRY(check_replica(c, id, false));
+  TRY(check_replica_q(c, id, false));
   return c->replicas[id]->local >= 0 ? 1 : 0;
 }
 
 int cbx_num_replicas(cbx_context *c) {
-  TRY(check_manager(c));
+  TRY(check_manager_q(c));
   return c->size;
 }
 
 int cbx_num_devices(cbx_context *c) {
-  TRY(check_ctx(c));
+  TRY(check_ctx_q(c));
   return c->G;
 }
 
 int cbx_num_local_devices(cbx_context *c) {
-  TRY(check_ctx(c));
+  TRY(check_ctx_q(c));
   return (int)c->devs.size();
 }
 
 int cbx_local_device_index(cbx_context *c, int local) {
-  TRY(check_ctx(c));
+  TRY(check_ctx_q(c));
   if (local < 0 || local >= (int)c->devs.size()) return fail(CBX_ERR_INVALID, "local device %d out of range", local);
   return c->devs[local].g;
 }
@@ -2034,7 +2136,7 @@ int cbx_base_host_buffer(cbx_context *c, int g, int kind, void **host_ptr) {
 }
 
 int cbx_wait(cbx_context *c) {
-  TRY(check_ctx(c));
+  TRY(check_ctx_q(c));
   for (Device &d : c->devs) {
     HIP_TRY(hipSetDevice(d.hip_id));
     HIP_TRY(hipStreamSynchronize(d.stream));
@@ -2043,7 +2145,7 @@ int cbx_wait(cbx_context *c) {
 }
 
 int cbx_step_event(cbx_context *c, int local, void **event) {
-  TRY(check_ctx(c));
+  TRY(check_ctx_q(c));
   if (local < 0 || local >= (int)c->devs.size() || !event) return fail(CBX_ERR_INVALID, "bad step-event query");
   *event = reinterpret_cast<void *>(c->devs[local].step_event ? c->devs[local].step_event : c->devs[local].synched);
   return CBX_OK;
@@ -2068,7 +2170,7 @@ int cbx_set_timing(cbx_context *c, int enable) {
 }
 
 int cbx_last_timing(cbx_context *c, int local, float *ms) {
-  TRY(check_ctx(c));
+  TRY(check_ctx_q(c));
   if (local < 0 || local >= (int)c->devs.size() || !ms) return fail(CBX_ERR_INVALID, "bad timing query");
   Device &d = c->devs[local];
   HIP_TRY(hipSetDevice(d.hip_id));
@@ -2095,7 +2197,7 @@ int cbx_last_timing(cbx_context *c, int local, float *ms) {
 }
 
 int cbx_timing_history(cbx_context *c, int local, int which, float *ms, int max) {
-  TRY(check_ctx(c));
+  TRY(check_ctx_q(c));
   if (local < 0 || local >= (int)c->devs.size() || !ms || max < 0) return fail(CBX_ERR_INVALID, "bad history query");
   if (which != CBX_T_KERNEL && which != CBX_T_ALLREDUCE && which != CBX_T_APPLY && which != CBX_T_STEP)
     return fail(CBX_ERR_INVALID, "history covers kernel / all-reduce / apply / step only");
@@ -2168,6 +2270,13 @@ int cbx_set_barrier_kernel_config(cbx_context *c, int block, int unroll, int wav
     cfg->unroll = unroll;
     cfg->waves_per_cu = waves_per_cu;
   }
+  return CBX_OK;
+}
+
+int cbx_set_pipeline_mode(cbx_context *c, int mode) {
+  TRY(check_ctx(c));
+  if (mode != 0 && mode != 1) return fail(CBX_ERR_INVALID, "pipeline mode must be 0 or 1");
+  c->pipeline_mode = mode;
   return CBX_OK;
 }
 

@@ -37,7 +37,12 @@ struct SmaArgs {
   float alpha;                 // conf->alpha (sma.c:33)
   float copies;                // Phase D requests on this device (kernel A)
   int nrep;                    // locked replicas on this device, id order
-  int pad_;
+  // Kernel B's Phase-D decision: 0 read ctrl_in; 1 read ctrl_in and publish
+  // it to *decision (bucket 0 of a cross-step pipelined step); 2 read
+  // *decision (its later buckets, whose ctrl_in the next step's first
+  // all-reduce may already be overwriting).
+  int decision_mode;
+  float *decision;
 };
 
 // Buffers are padded to this many float4s so every trip of every kernel is

@@ -220,7 +220,9 @@ __global__ __launch_bounds__(256) void sma_accumulate_kernel(const SmaArgs a) {
 // ---------------------------------------------------------------------------
 template <bool MOM, int P, int U>
 __global__ __launch_bounds__(256) void sma_apply_kernel(const SmaArgs a) {
-  const bool copy = a.ctrl_in[0] > 0.0f;
+  const float requests = a.decision_mode == 2 ? *a.decision : a.ctrl_in[0];
+  if (a.decision_mode == 1 && blockIdx.x == 0 && threadIdx.x == 0) *a.decision = requests;
+  const bool copy = requests > 0.0f;
   const uint32_t trip = gridDim.x * blockDim.x * U;
   const uint32_t n4 = (uint32_t)a.n4;
   const v4f mb = kBaseMomentum;

@@ -57,7 +57,7 @@ def max_over_ranks(value: float, world: int) -> float:
 
 
 def tune_buckets(gpu, n: int, world: int, step: Callable[[], None], candidates=(1, 2, 4, 8, 16),
-                 steps: int = 4, warmup: int = 2):
+                 steps: int = 4, warmup: int = 2, modes=(0, 1)):
     """Pick the bucket count of the G > 1 pipeline (kernel A / RCCL
     all-reduce / kernel B per bucket) by timing each candidate on the live
     communicator, the way a runtime tunes itself in its warm-up.
@@ -69,28 +69,34 @@ def tune_buckets(gpu, n: int, world: int, step: Callable[[], None], candidates=(
     xGMI links.  Every rank times every candidate, the times are max-reduced
     over ranks, and all ranks take the same argmin, so the RCCL call sequence
     stays identical on every rank.  ``step()`` runs one barrier step.
-    Returns (bucket_elements, {candidate: ms_per_step}).
+    With more than one bucket each count is also timed in both pipeline
+    modes (``gpu.set_pipeline_mode``: 0 within a step, 1 across steps).
+    Returns (bucket_elements, mode, {"<buckets>/<mode>": ms_per_step}).
     """
     import time
 
     results = {}
     for nb in candidates:
         elems = (1 << 62) if nb <= 1 else max(1, -(-n // nb))
-        gpu.set_bucket_elements(elems)
-        for _ in range(warmup):
-            step()
-        gpu.wait()
-        barrier(world)
-        t0 = time.perf_counter()
-        for _ in range(steps):
-            step()
-        gpu.wait()
-        ms = (time.perf_counter() - t0) * 1e3 / steps
-        results[nb] = max_over_ranks(ms, world)
+        for mode in (modes if nb > 1 else (0,)):
+            gpu.set_bucket_elements(elems)
+            gpu.set_pipeline_mode(mode)
+            for _ in range(warmup):
+                step()
+            gpu.wait()
+            barrier(world)
+            t0 = time.perf_counter()
+            for _ in range(steps):
+                step()
+            gpu.wait()
+            ms = (time.perf_counter() - t0) * 1e3 / steps
+            results[(nb, mode)] = max_over_ranks(ms, world)
     best = min(results, key=lambda k: (results[k], k))
-    elems = (1 << 62) if best <= 1 else max(1, -(-n // best))
+    nb, mode = best
+    elems = (1 << 62) if nb <= 1 else max(1, -(-n // nb))
     gpu.set_bucket_elements(elems)
-    return elems, results
+    gpu.set_pipeline_mode(mode)
+    return elems, mode, {f"{k[0]}/{k[1]}": v for k, v in results.items()}
 
 
 def local_replicas(size: int, world: int, rank: int):

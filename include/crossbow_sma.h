@@ -293,6 +293,14 @@ int cbx_set_barrier_kernel_config (cbx_context *ctx, int block, int unroll, int 
  * more than one bucket the all-reduce of bucket k runs on a second stream
  * beside kernel A of bucket k+1, and only CBX_T_STEP is timed per step.  */
 int cbx_set_bucket_elements (cbx_context *ctx, long long bucket_elements);
+/* How the bucketed pipeline overlaps (G > 1, or forced split): 0 (default)
+ * within a step only; 1 also across steps: kernels A run on their own
+ * stream and A(k) waits only for B(k) of the previous step, so the next
+ * step's first buckets run while this step's last all-reduces are on the
+ * link.  Any other C-ABI call between two steps that may enqueue device
+ * work makes the next step join the whole sync stream first.  Same results
+ * bit for bit.                                                            */
+int cbx_set_pipeline_mode (cbx_context *ctx, int mode);
 /* Force the multi-GPU pipeline (kernel A + RCCL all-reduce + kernel B) even
  * at G = 1 (a one-rank communicator), so a single-GPU host exercises it.  */
 int cbx_set_force_split (cbx_context *ctx, int force);

@@ -38,6 +38,7 @@ CASES = [
     ("sma", 50_001, 2, 0.9, 3, 0, {}, {}, 0, 7),
     ("sma-copy-ssp", 50_001, 2, 0.9, 3, 0, {1: 3}, {0: 1}, 0, 7),
     ("sma-5-buckets", 300_007, 3, 0.9, 2, 65_536, {1: 0}, {}, 0, 7),
+    ("sma-5-buckets-cross", 300_007, 2, 0.9, 5, 65_536, {2: 1}, {3: 0}, 0, 7),
     ("sma-no-momentum", 20_011, 1, 0.0, 2, 4096, {}, {}, 0, 3),
     ("sma-staged", 100_003, 2, 0.9, 2, 0, {1: 2}, {}, 3, 7),
     ("ssgd", 40_009, 2, 0.9, 2, 0, {}, {}, 0, 1),
@@ -100,6 +101,8 @@ def _case(L, A, rank, world, uid, case):
         g("cbx_set_model_manager", R, A.SYNC_SSP if held_at else A.SYNC_BSP)
         if bucket:
             g("cbx_set_bucket_elements", ctypes.c_longlong(bucket))
+        if name.endswith("-cross"):
+            g("cbx_set_pipeline_mode", 1)  # kernels A of the next step overlap this step's tail
         size = world * R
         assert g("cbx_num_replicas") == size and g("cbx_num_devices") == world
         mine = [i for i in range(size) if i % world == rank]
@@ -304,7 +307,8 @@ def _rank_main(rank, world, uids, fake_dir, q):
 
 def _cases(world):
     # four ranks: the SMA cases (placement i % 4, Phase D from rank 3, buckets)
-    return CASES if world == 2 else [c for c in CASES if c[0] in ("sma", "sma-copy-ssp", "sma-5-buckets")]
+    return CASES if world == 2 else [c for c in CASES if c[0] in ("sma", "sma-copy-ssp", "sma-5-buckets",
+                                                                  "sma-5-buckets-cross")]
 
 
 @pytest.mark.skipif(not os.path.exists(VARIANT), reason="run scripts/build_fake_rccl.sh first")

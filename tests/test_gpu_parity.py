@@ -629,3 +629,49 @@ def test_concurrent_task_threads_and_barrier():
             assert g.replica_clock(i) == barriers + 1
     finally:
         g.free()
+
+
+@pytest.mark.parametrize("momentum", [0.0, 0.9])
+@pytest.mark.parametrize("bucket", [65_536, 4096])
+def test_cross_step_pipeline(momentum, bucket):
+    # cbx_set_pipeline_mode(1): kernels A on their own stream, each waiting
+    # only for B of the same bucket in the previous step.  Eight steps with
+    # Phase D requests, SSP holds, a host write between two steps (which
+    # must make the next step join the whole sync stream) and a switch to the
+    # in-step mode and back; bit-exact with the oracle throughout.
+    from crossbow_amd import BUF_DATA
+    n, R = 300_001, 3
+    st = O.make_state(n, 1, R, 0.1, momentum)
+    g = make_gpu(n, R, 0.1, momentum, sync=1)
+    try:
+        g.set_force_split(True)
+        g.set_bucket_elements(bucket)
+        g.set_pipeline_mode(1)
+        upload(g, st)
+        want = st.clone()
+        plan = [{}, {"copy": 1}, {"hold": 2}, {}, {"write": 0}, {"mode": 0}, {"mode": 1, "copy": 2, "hold": 0}, {}, {}]
+        for step, p in enumerate(plan):
+            want.locked[:] = 1
+            if "mode" in p:
+                g.set_pipeline_mode(p["mode"])
+            if "write" in p:
+                i = p["write"]
+                new = O.fill_normal(n, 900 + step, 0.05)
+                g.replica_write(i, BUF_DATA, new)
+                want.w[i] = new.copy()
+            if "copy" in p:
+                g.set_replica_copy(p["copy"], True)
+                want.copy[p["copy"]] = 1
+            if "hold" in p:
+                g.replica_lock(p["hold"])
+                want.locked[p["hold"]] = 0
+            g.lockAny()
+            g.synchronise(0, step + 1, 0, False)
+            g.unlockAny()
+            if "hold" in p:
+                g.replica_unlock(p["hold"])
+            O.sma_step(want)
+        g.wait()
+        compare_states(download(g, st), want)
+    finally:
+        g.free()
