@@ -647,7 +647,7 @@ int sma_step(cbx_context *c, int first) {
     // A step joins the whole sync stream instead when anything else was
     // enqueued since the last cross-pipelined step (foreign_ops).
     const bool cross = pipelined && c->pipeline_mode == 1;
-    const unsigned long long foreign = c->foreign_ops.load(std::memory_order_relaxed);
+    const unsigned long long foreign = c->foreign_ops.load(std::memory_order_acquire);
     std::vector<char> join(c->devs.size(), 1);
     for (size_t k = 0; k < c->devs.size(); ++k) {
       Device &d = c->devs[k];
@@ -1804,7 +1804,20 @@ static int ssgd_worker_step(cbx_context *c, Replica &r, Device &d, int task, hip
   return CBX_OK;
 }
 
+static int replica_optimise_impl(cbx_context *c, int id, int task, void *stream);
+
+// Task threads call this while the collector thread may be enqueueing a
+// barrier.  The foreign-op counter is bumped on entry (check_replica) AND
+// after the enqueue: a cross-step pipelined step that read the counter
+// between the two then sees it move again, and the next step joins the
+// whole sync stream, which by then holds this call's wait.
 int cbx_replica_optimise(cbx_context *c, int id, int task, void *stream) {
+  const int rc = replica_optimise_impl(c, id, task, stream);
+  if (c) c->foreign_ops.fetch_add(1, std::memory_order_release);
+  return rc;
+}
+
+static int replica_optimise_impl(cbx_context *c, int id, int task, void *stream) {
   TRY(check_replica(c, id, true));
   Replica &r = *c->replicas[id];
   Device &d = c->devs[r.local];
