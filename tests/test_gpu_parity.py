@@ -567,7 +567,8 @@ def test_step_event_covers_the_step(mode, timing):
         g.free()
 
 
-def test_concurrent_task_threads_and_barrier():
+@pytest.mark.parametrize("pipeline", ["fused", "cross-step"])
+def test_concurrent_task_threads_and_barrier(pipeline):
     # The reference's threading: task threads lock a replica,
     # run its optimiser step and release it, while the result-collector
     # thread runs lockAny / synchronise / unlockAny.  Under SSP the barrier
@@ -591,6 +592,10 @@ def test_concurrent_task_threads_and_barrier():
         g.setWeightDecay(1e-4)
         g.setLearningRateDecayPolicyFixed(0.01)
         g.setModelManager(R, 1)  # SSP
+        if pipeline == "cross-step":  # kernels A across steps, racing the task threads' optimiser steps
+            g.set_force_split(True)
+            g.set_bucket_elements(16_384)
+            g.set_pipeline_mode(1)
         g.fill_synthetic(3)
 
         def worker(k):
