@@ -84,6 +84,7 @@ SIGNATURES = {
     "cbx_unlock_any": (_I, [_P]),
     "cbx_checkpoint_model": (_I, [_P, _CP]),
     "cbx_override_model_data": (_I, [_P, _CP]),
+    "cbx_register_batchnorm_stats": (_I, [_P, _I, _I, _PP, _PP]),
     "cbx_add_model": (_I, [_P]),
     "cbx_del_model": (_I, [_P]),
     "cbx_average_batchnorm_stats": (_I, [_P, _I, _IP, _PP, _PP, _IP]),

@@ -252,6 +252,13 @@ struct cbx_context {
   int64_t n4 = 0;      // padded float4 count
   bool has_last = false;
   unsigned long long version = 0;
+  // BN operators whose running statistics travel with the checkpoint
+  // (executioncontext.c:2352-2364): op id -> per-local-device buffers.
+  struct BnStats {
+    int elements = 0;
+    std::vector<float *> mean, variance;
+  };
+  std::map<int, BnStats> bn_stats;
   bool timing = false;
   cbx::LaunchConfig cfg;
   // Optimiser step and S-SGD kernels (one float4 stream per buffer, few reads).
@@ -1563,6 +1570,8 @@ int cbx_unlock_any(cbx_context *c) {
 }
 
 // ---- checkpoint -----------------------------------------------------------
+static int batchnorm_checkpoint(cbx_context *c, const std::string &dir, bool store);
+
 int cbx_checkpoint_model(cbx_context *c, const char *dir) {
   TRY(check_manager(c));
   if (!dir) return fail(CBX_ERR_INVALID, "null checkpoint directory");
@@ -1586,7 +1595,7 @@ int cbx_checkpoint_model(cbx_context *c, const char *dir) {
       if (c->has_last) TRY(store_buffer(replica_dev(d, r, CBX_BUF_LAST), bytes, rp + "-last.dat", tmp));
     }
   }
-  return CBX_OK;
+  return batchnorm_checkpoint(c, path, true);  // :2352-2364
 }
 
 int cbx_override_model_data(cbx_context *c, const char *dir) {
@@ -1608,6 +1617,65 @@ int cbx_override_model_data(cbx_context *c, const char *dir) {
       if (c->has_last) TRY(load_buffer(replica_dev(d, r, CBX_BUF_LAST), bytes, rp + "-last.dat", tmp));
     }
   }
+  return batchnorm_checkpoint(c, dir, false);  // :2375-2386
+}
+
+// cudnnbatchnormparams.c:102-143: one BN operator's running mean / variance,
+// one pair of files per device that holds it.  `store` selects the direction.
+static int batchnorm_stats_files(cbx_context *c, const std::string &dir, int op, int elements,
+                                 float *const *mean, float *const *variance, bool store) {
+  if (op < 0 || elements <= 0 || !mean || !variance)
+    return fail(CBX_ERR_INVALID, "bad batch-norm checkpoint arguments (op %d, %d elements)", op, elements);
+  std::vector<char> tmp;
+  const size_t bytes = (size_t)elements * 4;
+  for (size_t k = 0; k < c->devs.size(); ++k) {
+    Device &d = c->devs[k];
+    if (!mean[k] && !variance[k]) continue;  // :110-111
+    if (!mean[k] || !variance[k])
+      return fail(CBX_ERR_INVALID, "device %d holds only one of operator %d's mean / variance", d.g, op);
+    HIP_TRY(hipSetDevice(d.hip_id));
+    HIP_TRY(hipDeviceSynchronize());
+    const std::string avg = fmt("%s/gpu-%02d-bn-avg-%03d.dat", dir.c_str(), d.g, op);
+    const std::string var = fmt("%s/gpu-%02d-bn-var-%03d.dat", dir.c_str(), d.g, op);
+    if (store) {
+      TRY(store_buffer(mean[k], bytes, avg, tmp));
+      TRY(store_buffer(variance[k], bytes, var, tmp));
+    } else {
+      TRY(load_buffer(mean[k], bytes, avg, tmp));
+      TRY(load_buffer(variance[k], bytes, var, tmp));
+    }
+  }
+  return CBX_OK;
+}
+
+static int batchnorm_checkpoint(cbx_context *c, const std::string &dir, bool store) {
+  for (auto &e : c->bn_stats)
+    TRY(batchnorm_stats_files(c, dir, e.first, e.second.elements, e.second.mean.data(), e.second.variance.data(),
+                              store));
+  return CBX_OK;
+}
+
+// crossbowCudnnBatchNormParamsSetEstimatedMeanAndVariable (executioncontext.c:
+// 1280-1290) hands each device's buffers to the operator's BN params; here the
+// dataflow side hands them to the context, once per BN operator.
+int cbx_register_batchnorm_stats(cbx_context *c, int op, int elements, float *const *mean, float *const *variance) {
+  TRY(check_ctx(c));
+  if (op < 0) return fail(CBX_ERR_INVALID, "bad batch-norm operator id %d", op);
+  if (elements == 0) {
+    c->bn_stats.erase(op);
+    return CBX_OK;
+  }
+  if (elements < 0 || !mean || !variance)
+    return fail(CBX_ERR_INVALID, "bad batch-norm statistics (op %d, %d elements)", op, elements);
+  cbx_context::BnStats b;
+  b.elements = elements;
+  for (size_t k = 0; k < c->devs.size(); ++k) {
+    if (!mean[k] != !variance[k])
+      return fail(CBX_ERR_INVALID, "device %d holds only one of operator %d's mean / variance", c->devs[k].g, op);
+    b.mean.push_back(mean[k]);
+    b.variance.push_back(variance[k]);
+  }
+  c->bn_stats[op] = std::move(b);
   return CBX_OK;
 }
 

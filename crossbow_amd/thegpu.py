@@ -171,7 +171,22 @@ class TheGPU:
     def delModel(self) -> int:
         return check(self._L.cbx_del_model(self._ctx))
 
-    # ---- batch-norm running statistics (cudnnbatchnormparams.c:157-222) ------
+    # ---- batch-norm running statistics (cudnnbatchnormparams.c:102-222) ------
+    def register_batchnorm_stats(self, op: int, elements: int, mean_ptrs: Sequence[int],
+                                 var_ptrs: Sequence[int]) -> None:
+        """Make BN operator ``op``'s running mean / variance part of the checkpoint.
+
+        ``mean_ptrs[k]`` / ``var_ptrs[k]``: device pointers on local device k (both 0: that
+        device holds no copy).  ``checkpointModel`` / ``overrideModelData`` then store / load
+        ``gpu-%02d-bn-{avg,var}-%03d.dat`` beside the model files; ``elements == 0`` removes it.
+        """
+        ndev = check(self._L.cbx_num_local_devices(self._ctx))
+        if len(mean_ptrs) != ndev or len(var_ptrs) != ndev:
+            raise ValueError(f"one mean / variance pointer per local device ({ndev}) expected")
+        mp = (ctypes.c_void_p * ndev)(*mean_ptrs)
+        vp = (ctypes.c_void_p * ndev)(*var_ptrs)
+        check(self._L.cbx_register_batchnorm_stats(self._ctx, op, elements, mp, vp))
+
     def average_batchnorm_stats(self, elements: Sequence[int], mean_ptrs: Sequence[int],
                                 var_ptrs: Sequence[int], updated: Sequence[int]) -> None:
         """Average every BN layer's running mean/variance across devices.

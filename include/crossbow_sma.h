@@ -156,6 +156,21 @@ int cbx_unlock_any (cbx_context *ctx);
 int cbx_checkpoint_model (cbx_context *ctx, const char *dir);
 /* TheGPU.overrideModelData(String) GPU.c:1165-1176 -> executioncontext.c:2369-2388 */
 int cbx_override_model_data (cbx_context *ctx, const char *dir);
+/* Batch-norm running statistics in the checkpoint.  After the model files,
+ * executioncontext.c:2352-2364 / 2375-2386 walk the dataflow's BATCHNORM
+ * operators and call crossbowCudnnBatchNormParams{Store,Load}Estimated-
+ * MeanAndVariable (cudnn/cudnnbatchnormparams.c:102-143) with the
+ * operator's id.  The dataflow stays with the caller, so it registers each
+ * BN operator's buffers here once (where executioncontext.c:1280-1290 sets
+ * them per device); cbx_checkpoint_model / cbx_override_model_data then
+ * store / load gpu-%02d-bn-avg-%03d.dat and gpu-%02d-bn-var-%03d.dat
+ * (global device id, op id; raw fp32, `elements` floats) in the same
+ * directory as the model files.  mean/variance[k]: device pointers on
+ * LOCAL device k; a device whose pair is both NULL holds no copy and is
+ * skipped (:110-111).  Registering an op again replaces it; elements == 0
+ * removes it.                                                             */
+int cbx_register_batchnorm_stats (cbx_context *ctx, int op, int elements,
+		float *const *mean, float *const *variance);
 /* TheGPU.addModel() / delModel()   GPU.c:1178-1199 (autotune; also called
  * by cbx_synchronise for autotune > 0 / < 0, executioncontext.c:2321-2328).
  * add: one new replica per device, ids size .. size+G-1 (id size+g on device

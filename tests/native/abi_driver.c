@@ -2,7 +2,8 @@
  * abi_driver.c -- drives libcrossbow_sma's C-ABI from plain C, the way the
  * JNI shim does, through every host-side path: registration, the model
  * manager, BSP/SSP barriers, SMA / S-SGD / DEFAULT steps, the optimiser
- * step, pinned staging (serial and pipelined), checkpoint / override,
+ * step, pinned staging (serial and pipelined), checkpoint / override (with
+ * batch-norm statistics),
  * autotune add / del, BN averaging, timing queries and teardown.
  *
  * Built with host-side AddressSanitizer + UndefinedBehaviorSanitizer
@@ -115,6 +116,14 @@ int main (void) {
 	EXPECT (all_finite ((const float *) hz, (size_t) n));
 	char dir[] = "/tmp/cbx_abi_driverXXXXXX";
 	EXPECT (mkdtemp (dir) != NULL);
+	{	/* one BN operator's statistics travel with the checkpoint */
+		void *bn = NULL;
+		CHECK (cbx_replica_buffer (c, 0, CBX_BUF_GRADIENT, &bn));
+		float *bm[1] = { (float *) bn }, *bv[1] = { (float *) bn + 256 };
+		CHECK (cbx_register_batchnorm_stats (c, 4, 256, bm, bv));
+		float *half[1] = { NULL };
+		EXPECT (cbx_register_batchnorm_stats (c, 5, 256, bm, half) == CBX_ERR_INVALID);
+	}
 	CHECK (cbx_checkpoint_model (c, dir));
 	CHECK (cbx_base_read (c, 0, CBX_BUF_DATA, host, (size_t) 4 * n));
 	barrier (c, 5, 1);  /* autotune: add one replica per device */

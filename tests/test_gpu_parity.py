@@ -290,6 +290,55 @@ def test_checkpoint_roundtrip_file_format():
         g.free()
 
 
+def test_checkpoint_batchnorm_stats():
+    # executioncontext.c:2352-2386 -> cudnnbatchnormparams.c:102-143: each BN
+    # operator's running mean / variance beside the model files, per device, by op id.
+    import torch
+    n, R = 4099, 2
+    st = O.make_state(n, 1, R, 0.1, 0.0)
+    g = make_gpu(n, R, 0.1, 0.0)
+    try:
+        upload(g, st)
+        ops = {3: 64, 17: 1001}
+        mean = {op: torch.from_numpy(O.fill_normal(e, 900 + op, 0.5)).cuda() for op, e in ops.items()}
+        var = {op: torch.from_numpy(O.fill_normal(e, 800 + op, 0.5)).cuda() for op, e in ops.items()}
+        want = {op: (mean[op].cpu().numpy(), var[op].cpu().numpy()) for op in ops}
+        for op, e in ops.items():
+            g.register_batchnorm_stats(op, e, [mean[op].data_ptr()], [var[op].data_ptr()])
+        g.register_batchnorm_stats(5, 8, [0], [0])  # no copy on this device: no files
+        with pytest.raises(ValueError):
+            g.register_batchnorm_stats(6, 8, [], [])
+        with tempfile.TemporaryDirectory() as d:
+            g.checkpointModel(d)
+            ck = os.path.join(d, "000001")
+            names = sorted(x for x in os.listdir(ck) if "-bn-" in x)
+            assert names == ["gpu-00-bn-avg-003.dat", "gpu-00-bn-avg-017.dat",
+                             "gpu-00-bn-var-003.dat", "gpu-00-bn-var-017.dat"]
+            for op in ops:
+                assert_bitexact(np.fromfile(os.path.join(ck, f"gpu-00-bn-avg-{op:03d}.dat"), "<f4"),
+                                want[op][0], f"op {op} mean file")
+                assert_bitexact(np.fromfile(os.path.join(ck, f"gpu-00-bn-var-{op:03d}.dat"), "<f4"),
+                                want[op][1], f"op {op} variance file")
+                mean[op].zero_()
+                var[op].fill_(-1.0)
+            torch.cuda.synchronize()
+            g.overrideModelData(ck)
+            for op in ops:
+                assert_bitexact(mean[op].cpu().numpy(), want[op][0], f"op {op} mean restored")
+                assert_bitexact(var[op].cpu().numpy(), want[op][1], f"op {op} variance restored")
+            # Unregistered: the next checkpoint has no BN files for it.
+            g.register_batchnorm_stats(17, 0, [0], [0])
+            g.checkpointModel(d)
+            assert sorted(x for x in os.listdir(os.path.join(d, "000002")) if "-bn-" in x) == \
+                ["gpu-00-bn-avg-003.dat", "gpu-00-bn-var-003.dat"]
+            # A missing file is an I/O error, as crossbowDataBufferLoad's err() (databuffer.c:242-244).
+            os.remove(os.path.join(ck, "gpu-00-bn-var-003.dat"))
+            with pytest.raises(Exception, match="bn-var-003"):
+                g.overrideModelData(ck)
+    finally:
+        g.free()
+
+
 def test_staged_roundtrip():
     # Pinned-host staging: stage_in -> step -> stage_out equals the oracle.
     from crossbow_amd import BUF_DATA, BUF_DIFF, BUF_LAST
