@@ -12,7 +12,7 @@ TMP=$(mktemp -d)
 trap 'rm -rf "$TMP"' EXIT
 /opt/rocm/lib/llvm/bin/clang -c -O1 -g -std=c11 -fno-omit-frame-pointer -fsanitize=address,undefined \
   -I include -o "$TMP/abi_driver.o" tests/native/abi_driver.c
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -O1 -g -std=c++17 -ffp-contract=off -fno-omit-frame-pointer \
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -O1 -Xarch_host -gline-tables-only -std=c++17 -ffp-contract=off -fno-omit-frame-pointer \
   -Xarch_host -fsanitize=address -Xarch_host -fsanitize=undefined \
   -I include -o "$OUT.tmp" \
   crossbow_amd/csrc/context.hip crossbow_amd/csrc/sma_kernels.hip -x none "$TMP/abi_driver.o" \
