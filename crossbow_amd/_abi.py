@@ -96,6 +96,10 @@ SIGNATURES = {
     "cbx_replica_optimise": (_I, [_P, _I, _I, _P]),
     "cbx_replica_get_copy": (_I, [_P, _I]),
     "cbx_replica_set_copy": (_I, [_P, _I, _I]),
+    "cbx_acquire_access": (_I, [_P, _IP]),
+    "cbx_upgrade_access": (_I, [_P, _I, _IP]),
+    "cbx_get_next_or_wait": (_I, [_P, _I]),
+    "cbx_replica_release": (_I, [_P, _I]),
     "cbx_replica_set_disabled": (_I, [_P, _I, _I]),
     "cbx_replica_device": (_I, [_P, _I]),
     "cbx_replica_is_local": (_I, [_P, _I]),

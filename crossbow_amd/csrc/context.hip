@@ -18,6 +18,7 @@
 #include <rccl/rccl.h>
 
 #include <pthread.h>
+#include <sched.h>
 #include <sys/stat.h>
 #include <sys/types.h>
 #include <fcntl.h>
@@ -31,6 +32,7 @@
 #include <cstdio>
 #include <cstring>
 #include <map>
+#include <memory>
 #include <string>
 #include <utility>
 #include <vector>
@@ -160,6 +162,14 @@ struct ModelDef {
   std::vector<float> host;  // initial values (PIN host buffer of theModel->data)
 };
 
+// The model manager's theta queue (thetaqueue.c, modelmanager.c:121-132): one
+// cache-line slot per replica id.  FREE; BUSY = reserved by a task from
+// acquireAccess until its release; SKIP = disabled.
+enum ThetaState { kThetaFree = 0, kThetaBusy = 1, kThetaSkip = 2 };  // thetaqueue.c:6-8
+struct alignas(64) ThetaSlot {
+  std::atomic<int> state{kThetaFree};
+};
+
 struct Replica {
   int id = 0;
   int g = 0;          // global device index (id % G)
@@ -167,7 +177,6 @@ struct Replica {
   int slot = 0;       // replica slot within its device
   int clock = 0;
   int updates = 0;
-  bool disabled = false;  // theta-queue slot skipped (thetaqueue.c:182-194)
   SolverConf conf;
   pthread_mutex_t lock;
   hipEvent_t client = nullptr;  // end of the last optimiser step on a task stream (sma.cu:79)
@@ -248,6 +257,8 @@ struct cbx_context {
   int sync_type = CBX_SYNC_BSP;
   std::vector<Replica *> replicas;  // global id -> replica (all ids; remote ones have local = -1)
   std::vector<int> locked;
+  std::unique_ptr<ThetaSlot[]> theta;  // kMaxReplicas * G slots, index = replica id
+  std::atomic<unsigned> theta_iter{0};  // round-robin cursor (thetaqueue.c:95-104)
   int64_t n = 0;       // model elements
   int64_t n4 = 0;      // padded float4 count
   bool has_last = false;
@@ -1411,6 +1422,11 @@ int cbx_set_model_manager(cbx_context *c, int replicas, int type) {
   // Replicas round-robin over devices: replica j*G + g on device g.
   c->replicas.assign(c->size, nullptr);
   c->locked.assign(c->size, 0);
+  // Capacity for every replica addModel can create, so that the task side's
+  // lookups never see these arrays move (add / del only resize them).
+  c->replicas.reserve((size_t)cbx::kMaxReplicas * c->G);
+  c->locked.reserve((size_t)cbx::kMaxReplicas * c->G);
+  c->theta.reset(new ThetaSlot[(size_t)cbx::kMaxReplicas * c->G]);
   for (int i = 0; i < c->size; ++i) {
     Replica *r = new Replica();
     r->id = i;
@@ -1462,7 +1478,7 @@ int cbx_lock_any(cbx_context *c) {
     Replica *r = c->replicas[i];
     if (r->local < 0) continue;
     ++local;
-    if (r->disabled) {
+    if (c->theta[i].state.load(std::memory_order_acquire) == kThetaSkip) {
       // modelmanager.c:217-222: counted, so BSP holds, but not locked and
       // therefore left out of the step, unlockAny and the clock.
       ++count;
@@ -1540,7 +1556,7 @@ static int synchronise_impl(cbx_context *c, int first, int clock, int autotune, 
   // modelmanager.c:259-265: clock of every locked replica.
   for (int i = 0; i < c->size; ++i)
     if (c->locked[i]) {
-      c->replicas[i]->clock = clock;
+      __atomic_store_n(&c->replicas[i]->clock, clock, __ATOMIC_RELEASE);  // read by cbx_get_next_or_wait
       c->replicas[i]->updates = 0;
     }
   return CBX_OK;
@@ -1721,6 +1737,7 @@ int cbx_add_model(cbx_context *c) {
     r->updates = src.updates;
     pthread_mutex_init(&r->lock, nullptr);
     c->replicas[id] = r;
+    c->theta[id].state.store(kThetaFree, std::memory_order_release);  // crossbowThetaQueueExpand (:442)
     if (r->local >= 0) {
       Device &d = c->devs[r->local];
       HIP_TRY(hipSetDevice(d.hip_id));
@@ -1763,6 +1780,9 @@ int cbx_del_model(cbx_context *c) {
       d.replicas.erase(std::remove(d.replicas.begin(), d.replicas.end(), id), d.replicas.end());
     }
     if (c->locked[id]) pthread_mutex_unlock(&r->lock);
+    // crossbowThetaQueueShrink (:537): the slot leaves the rotation.  A task
+    // still holding its reservation gets -1 from cbx_upgrade_access.
+    c->theta[id].state.store(kThetaSkip, std::memory_order_release);
     pthread_mutex_destroy(&r->lock);
     delete r;
   }
@@ -2042,9 +2062,95 @@ int cbx_replica_set_copy(cbx_context *c, int id, int flag) {
   return CBX_OK;
 }
 
+// crossbowThetaQueueDisable / Enable (thetaqueue.c:168-206).
 int cbx_replica_set_disabled(cbx_context *c, int id, int flag) {
   TRY(check_replica_q(c, id, false));
-  c->replicas[id]->disabled = flag != 0;
+  std::atomic<int> &st = c->theta[id].state;
+  if (flag) {
+    int expect = kThetaFree;
+    if (st.compare_exchange_strong(expect, kThetaSkip, std::memory_order_acq_rel)) return 0;
+    return expect == kThetaSkip ? 0 : 1;  // :199-201: reserved by a task, still enabled
+  }
+  int expect = kThetaSkip;
+  if (st.compare_exchange_strong(expect, kThetaFree, std::memory_order_acq_rel) || expect == kThetaFree) return CBX_OK;
+  return fail(CBX_ERR_STATE, "replica %d is reserved by a task; enable it before acquiring it", id);  // :182-184
+}
+
+// ---- the theta queue: task-side reservation (modelmanager.c:147-204) ---------
+static inline void spin_pause(unsigned &spins) {
+  if (++spins < 4096)
+    __builtin_ia32_pause();
+  else
+    sched_yield();
+}
+
+// crossbowThetaQueueGetNextSafely + Reserve (thetaqueue.c:106-128): the next
+// enabled slot of this process in round-robin order, then spin until it is
+// free and reserve it.  The reference spins forever when every slot is
+// disabled; here that is CBX_ERR_STATE.
+static int theta_reserve_next(cbx_context *c) {
+  for (;;) {
+    const int size = c->size;
+    int id = -1;
+    for (int tries = 0; tries < size && id < 0; ++tries) {
+      const int next = (int)(c->theta_iter.fetch_add(1, std::memory_order_relaxed) % (unsigned)size);
+      if (c->replicas[next]->local >= 0 && c->theta[next].state.load(std::memory_order_acquire) != kThetaSkip)
+        id = next;
+    }
+    if (id < 0) return fail(CBX_ERR_STATE, "every model replica of this process is disabled");
+    std::atomic<int> &st = c->theta[id].state;
+    unsigned spins = 0;
+    for (;;) {
+      int expect = kThetaFree;
+      if (st.compare_exchange_weak(expect, kThetaBusy, std::memory_order_acq_rel)) return id;
+      if (expect == kThetaSkip) break;  // disabled meanwhile: take the next one
+      spin_pause(spins);
+    }
+  }
+}
+
+int cbx_acquire_access(cbx_context *c, int *clock) {
+  TRY(check_manager_q(c));
+  if (!clock) return fail(CBX_ERR_INVALID, "null clock");
+  // modelmanager.c:180-190
+  const int id = theta_reserve_next(c);
+  if (id < 0) return id;
+  *clock = __atomic_load_n(&c->replicas[id]->clock, __ATOMIC_ACQUIRE);
+  return id;
+}
+
+int cbx_upgrade_access(cbx_context *c, int id, int *clock) {
+  TRY(check_manager_q(c));
+  if (!clock) return fail(CBX_ERR_INVALID, "null clock");
+  // modelmanager.c:192-198; 0 (Java null: the task processor re-acquires,
+  // TaskProcessor.java:112-114) once the replica has been deleted.
+  if (id < 0 || id >= c->size || c->theta[id].state.load(std::memory_order_acquire) != kThetaBusy) return 0;
+  *clock = __atomic_load_n(&c->replicas[id]->clock, __ATOMIC_ACQUIRE);
+  return 1;
+}
+
+int cbx_get_next_or_wait(cbx_context *c, int bound) {
+  TRY(check_manager_q(c));
+  // modelmanager.c:147-167: reserve, wait for the replica's clock to reach
+  // `bound` (the barrier advances it), lock.
+  const int id = theta_reserve_next(c);
+  if (id < 0) return id;
+  Replica &r = *c->replicas[id];
+  unsigned spins = 0;
+  while (bound > __atomic_load_n(&r.clock, __ATOMIC_ACQUIRE)) spin_pause(spins);
+  pthread_mutex_lock(&r.lock);
+  return id;
+}
+
+int cbx_replica_release(cbx_context *c, int id) {
+  TRY(check_replica_q(c, id, true));
+  // modelmanager.c:200-204: unlock, then free the theta slot.  The reference
+  // spins until the slot is BUSY; a slot nobody reserved is an error here.
+  std::atomic<int> &st = c->theta[id].state;
+  if (st.load(std::memory_order_acquire) != kThetaBusy)
+    return fail(CBX_ERR_STATE, "replica %d was not reserved (cbx_acquire_access)", id);
+  pthread_mutex_unlock(&c->replicas[id]->lock);
+  st.store(kThetaFree, std::memory_order_release);
   return CBX_OK;
 }
 

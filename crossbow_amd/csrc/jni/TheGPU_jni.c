@@ -219,3 +219,52 @@ NATIVE(jint, delModel) (JNIEnv *env, jobject obj) {
 	(void) env; (void) obj;
 	return fatal_or (cbx_del_model (theGPU));
 }
+
+/* The theta queue (GPU.c:888-932 -> modelmanager.c:180-198).  Replica ids
+ * cross JNI as java.lang.Integer, as in the reference (modelmanager.c:187). */
+static jobject box (JNIEnv *env, int id) {
+	jclass cls = (*env)->FindClass (env, "java/lang/Integer");
+	jmethodID valueOf = (*env)->GetStaticMethodID (env, cls, "valueOf", "(I)Ljava/lang/Integer;");
+	return (*env)->CallStaticObjectMethod (env, cls, valueOf, (jint) id);
+}
+
+static int unbox (JNIEnv *env, jobject obj) {
+	jclass cls = (*env)->FindClass (env, "java/lang/Integer");
+	jmethodID intValue = (*env)->GetMethodID (env, cls, "intValue", "()I");
+	return (int) (*env)->CallIntMethod (env, obj, intValue);
+}
+
+static int *clock_arg (JNIEnv *env, jintArray clock, jint **argv) {
+	if ((*env)->GetArrayLength (env, clock) != 1) { /* GPU.c:897 */
+		fprintf (stderr, "error: clock must be an int[1]\n");
+		exit (1);
+	}
+	*argv = (*env)->GetIntArrayElements (env, clock, 0);
+	return (int *) *argv;
+}
+
+NATIVE(jobject, acquireAccess) (JNIEnv *env, jobject obj, jintArray clock) {
+	(void) obj;
+	jint *argv;
+	int *c = clock_arg (env, clock, &argv);
+	int id = (int) fatal_or (cbx_acquire_access (theGPU, c));
+	(*env)->ReleaseIntArrayElements (env, clock, argv, 0);
+	return box (env, id);
+}
+
+NATIVE(jobject, upgradeAccess) (JNIEnv *env, jobject obj, jobject replicaId, jintArray clock) {
+	(void) obj;
+	if ((*env)->IsSameObject (env, replicaId, NULL))
+		return NULL;
+	jint *argv;
+	int *c = clock_arg (env, clock, &argv);
+	int held = (int) fatal_or (cbx_upgrade_access (theGPU, unbox (env, replicaId), c));
+	(*env)->ReleaseIntArrayElements (env, clock, argv, 0);
+	return held ? replicaId : NULL;
+}
+
+NATIVE(jint, release) (JNIEnv *env, jobject obj, jobject replicaId) {
+	(void) env; (void) obj; (void) replicaId;
+	fprintf (stderr, "error: Cannot release a GPU model replica id object from the GPU\n"); /* GPU.c:930 */
+	exit (1);
+}

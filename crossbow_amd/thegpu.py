@@ -233,9 +233,42 @@ class TheGPU:
     def set_replica_copy(self, id: int, flag: bool) -> None:
         check(self._L.cbx_replica_set_copy(self._ctx, id, 1 if flag else 0))
 
-    def set_replica_disabled(self, id: int, flag: bool) -> None:
-        """Theta-queue disable / enable (thetaqueue.c:182-194): counted, never locked."""
-        check(self._L.cbx_replica_set_disabled(self._ctx, id, 1 if flag else 0))
+    def set_replica_disabled(self, id: int, flag: bool) -> bool:
+        """Theta-queue disable / enable (thetaqueue.c:182-206): counted, never locked.
+
+        Returns False when a disable found the slot reserved by a task (it stays enabled).
+        """
+        return check(self._L.cbx_replica_set_disabled(self._ctx, id, 1 if flag else 0)) == 0
+
+    # ---- the theta queue (TheGPU.java:297-299, modelmanager.c:147-204) ----------
+    def acquireAccess(self, clock: list) -> Optional[int]:
+        """Reserve the next replica (round robin, waits while it is busy); clock[0] := its clock."""
+        c = ctypes.c_int(0)
+        rid = check(self._L.cbx_acquire_access(self._ctx, ctypes.byref(c)))
+        clock[0] = c.value
+        return rid
+
+    def upgradeAccess(self, replica_id: Optional[int], clock: list) -> Optional[int]:
+        """Refresh clock[0] of a reserved replica; None once it is gone (delModel)."""
+        if replica_id is None:
+            return None
+        c = ctypes.c_int(0)
+        if not check(self._L.cbx_upgrade_access(self._ctx, replica_id, ctypes.byref(c))):
+            return None
+        clock[0] = c.value
+        return replica_id
+
+    def release(self, replica_id: int) -> int:
+        # GPU.c:923-932: a GPU replica is released by the callback handler, not from Java.
+        raise CbxError(_lib.CBX_ERR_STATE, "Cannot release a GPU model replica id object from the GPU")
+
+    def replica_release(self, id: int) -> None:
+        """The callback handler's release (modelmanager.c:200-204): unlock + free the slot."""
+        check(self._L.cbx_replica_release(self._ctx, id))
+
+    def get_next_or_wait(self, bound: int) -> int:
+        """modelmanager.c:147-167: reserve the next replica, wait for clock >= bound, lock it."""
+        return check(self._L.cbx_get_next_or_wait(self._ctx, bound))
 
     def replica_device(self, id: int) -> int:
         return check(self._L.cbx_replica_device(self._ctx, id))

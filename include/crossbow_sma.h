@@ -207,10 +207,35 @@ int cbx_replica_clock (cbx_context *ctx, int id);
 int cbx_replica_learning_rate (cbx_context *ctx, int id, int task, float *rate);
 int cbx_replica_get_copy (cbx_context *ctx, int id);
 int cbx_replica_set_copy (cbx_context *ctx, int id, int flag);
-/* The scheduler's theta queue disabled (flag 1) or re-enabled (0) a replica
- * (crossbowThetaQueueDisable / Enable, thetaqueue.c:182-194).  lockAny then
- * counts it, so BSP still holds, but does not lock it, so the step, unlockAny
- * and the clock leave it alone (modelmanager.c:217-222).                  */
+/* ---- the theta queue: which replica a task runs on -------------------- */
+/* The model manager's theta queue (thetaqueue.c, modelmanager.c:121-132)
+ * has one slot per replica id: free, reserved by a task, or disabled.
+ * TheGPU.acquireAccess([I)  GPU.c:888-903 -> modelmanager.c:180-190:
+ * reserve the next enabled replica of this process in round-robin order,
+ * waiting (spinning) until it is free; returns its id and sets *clock to
+ * its clock.  CBX_ERR_STATE if every replica here is disabled (the
+ * reference spins forever).                                              */
+int cbx_acquire_access (cbx_context *ctx, int *clock);
+/* TheGPU.upgradeAccess(Integer,[I)  GPU.c:905-921 -> modelmanager.c:192-198:
+ * refresh *clock of a reserved replica and return 1, or return 0 (Java
+ * null: the task processor re-acquires) once that replica is gone.       */
+int cbx_upgrade_access (cbx_context *ctx, int id, int *clock);
+/* crossbowModelManagerGetNextOrWait (modelmanager.c:147-167), the execute
+ * paths that pick the replica natively (executioncontext.c:2018, 2130):
+ * reserve the next replica, wait until its clock >= bound, lock it.
+ * Returns its id.  Blocks until a barrier advances the clock.            */
+int cbx_get_next_or_wait (cbx_context *ctx, int bound);
+/* crossbowModelManagerRelease (modelmanager.c:200-204), from the callback
+ * handler after a task (callbackhandler.c:155): unlock the replica and free
+ * its theta slot.  CBX_ERR_STATE if the slot is not reserved.             */
+int cbx_replica_release (cbx_context *ctx, int id);
+/* Disable (flag 1) or re-enable (0) a replica's theta slot
+ * (crossbowThetaQueueDisable / Enable, thetaqueue.c:182-206; delModel
+ * disables the slots of the replicas it removes).  lockAny then counts it,
+ * so BSP still holds, but does not lock it, so the step, unlockAny and the
+ * clock leave it alone (modelmanager.c:217-222).  Disabling returns 0, or 1
+ * when a task holds the reservation (the slot stays enabled, :199-201);
+ * enabling a reserved slot is CBX_ERR_STATE (:182-184).                   */
 int cbx_replica_set_disabled (cbx_context *ctx, int id, int flag);
 /* crossbowKernelOptimiserSMA (kernels/optimisers/sma.cu:3-100), fused into
  * one pass: the replica's local step for task `task`, which produces the

@@ -16,8 +16,11 @@ typedef struct _jobject *jobject;
 typedef jobject jintArray;
 typedef jobject jfloatArray;
 typedef jobject jstring;
+typedef jobject jclass;
+typedef struct _jmethodID *jmethodID;
 #define JNI_FALSE 0
 #define JNI_TRUE 1
+#define JNI_COMMIT 1
 #define JNI_ABORT 2
 #define JNIEXPORT __attribute__((visibility("default")))
 #define JNICALL
@@ -33,5 +36,10 @@ struct JNINativeInterface_ {
 	const char *(*GetStringUTFChars) (JNIEnv *, jstring, jboolean *);
 	void (*ReleaseStringUTFChars) (JNIEnv *, jstring, const char *);
 	jboolean (*IsSameObject) (JNIEnv *, jobject, jobject);
+	jclass (*FindClass) (JNIEnv *, const char *);
+	jmethodID (*GetStaticMethodID) (JNIEnv *, jclass, const char *, const char *);
+	jmethodID (*GetMethodID) (JNIEnv *, jclass, const char *, const char *);
+	jobject (*CallStaticObjectMethod) (JNIEnv *, jclass, jmethodID, ...);
+	jint (*CallIntMethod) (JNIEnv *, jobject, jmethodID, ...);
 };
 #endif

@@ -144,6 +144,22 @@ int main (void) {
 	CHECK (cbx_set_kernel_config (c, 64, 0, 1, 2));
 	CHECK (cbx_set_aux_kernel_config (c, 128, 2, 4));
 	barrier (c, 7, 0);
+	/* the theta queue: reserve, run, release (modelmanager.c:147-204) */
+	{
+		int clk = -1;
+		int a = cbx_acquire_access (c, &clk), b = cbx_acquire_access (c, &clk);
+		EXPECT (a >= 0 && b >= 0 && a != b && clk >= 0);
+		EXPECT (cbx_upgrade_access (c, a, &clk) == 1);
+		EXPECT (cbx_replica_set_disabled (c, a, 1) == 1);  /* reserved: stays enabled */
+		CHECK (cbx_replica_lock (c, a));
+		CHECK (cbx_replica_release (c, a));
+		CHECK (cbx_replica_lock (c, b));
+		CHECK (cbx_replica_release (c, b));
+		EXPECT (cbx_replica_release (c, b) == CBX_ERR_STATE);
+		int d = cbx_get_next_or_wait (c, 0);
+		EXPECT (d >= 0);
+		CHECK (cbx_replica_release (c, d));
+	}
 	/* BSP failure: a replica held by a task */
 	CHECK (cbx_replica_lock (c, 1));
 	EXPECT (cbx_lock_any (c) == CBX_ERR_BARRIER);

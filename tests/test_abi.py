@@ -77,7 +77,7 @@ JNI_NATIVES = [
     "setLearningRateDecayPolicyStep", "setLearningRateDecayPolicyMultiStep", "setLearningRateDecayPolicyExp",
     "setBaseModelMomentum", "setMomentum", "setWeightDecay", "setEamsgdAlpha", "setEamsgdTau",
     "setModelManager", "lockAny", "merge", "synchronise", "unlockAny", "checkpointModel",
-    "overrideModelData", "addModel", "delModel",
+    "overrideModelData", "addModel", "delModel", "acquireAccess", "upgradeAccess", "release",
 ]
 
 

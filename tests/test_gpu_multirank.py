@@ -106,6 +106,13 @@ def _case(L, A, rank, world, uid, case):
         size = world * R
         assert g("cbx_num_replicas") == size and g("cbx_num_devices") == world
         mine = [i for i in range(size) if i % world == rank]
+        # The theta queue hands out this rank's replicas only, round robin (modelmanager.c:180-190).
+        clk = ctypes.c_int(-1)
+        got = [g("cbx_acquire_access", ctypes.byref(clk)) for _ in mine]
+        assert got == mine and clk.value == 0, got
+        for i in got:
+            g("cbx_replica_lock", i)
+            g("cbx_replica_release", i)
         st = O.make_state(n, world, R, 0.1, mom)
         if staged:
             g.host("cbx_base_host_buffer", rank, A.BUF_DATA, n)[:] = st.z[rank]
