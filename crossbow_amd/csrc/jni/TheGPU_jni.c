@@ -17,6 +17,16 @@
 
 static cbx_context *theGPU = NULL;
 
+/* The dataflow natives that stay in the reference's GPU.c (execute, the
+ * callback handler, ...) are linked into the same libGPU.so and reach the
+ * model manager through this context (cbx_replica_lock / _release /
+ * _buffer / _optimise, ...).  Declare it there as
+ *     extern cbx_context *crossbow_sma_context (void);                    */
+cbx_context *crossbow_sma_context (void);
+cbx_context *crossbow_sma_context (void) {
+	return theGPU;
+}
+
 static jint fatal_or (int rc) {
 	if (rc < 0) {
 		fprintf (stderr, "error: %s\n", cbx_last_error ());
