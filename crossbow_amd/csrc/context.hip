@@ -1237,7 +1237,7 @@ int cbx_set_model(cbx_context *c, int variables, int bytes) {
   c->model.ops = variables;
   c->model.bytes = bytes;
   c->model.count_per_op.assign(variables, 0);
-  c->model.host.assign((size_t)(bytes + 3) / 4, 0.0f);
+  c->model.host.assign(((size_t)bytes + 3) / 4, 0.0f);
   return CBX_OK;
 }
 

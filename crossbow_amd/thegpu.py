@@ -24,6 +24,13 @@ def _ptr(a: np.ndarray) -> ctypes.c_void_p:
     return ctypes.c_void_p(a.ctypes.data)
 
 
+
+def _java_int(what: str, v: int) -> None:
+    # The natives take Java ints (TheGPU.java:268-271; model.h:35 `int bytes`):
+    # a model is at most 2^31 - 1 bytes.  ctypes would wrap a larger value silently.
+    if not -2**31 <= v < 2**31:
+        raise CbxError(_lib.CBX_ERR_INVALID, f"{what} {v} does not fit a Java int (models are < 2 GiB)")
+
 class TheGPU:
     """One execution context (the reference's process-global ``theGPU``)."""
 
@@ -75,9 +82,11 @@ class TheGPU:
 
     # ---- model registration (Model.GPURegister, Model.java:338-371) -------
     def setModel(self, variables: int, size: int) -> int:
+        _java_int("setModel size", size)
         return check(self._L.cbx_set_model(self._ctx, variables, size))
 
     def setModelVariable(self, id: int, order: int, shape: Sequence[int], capacity: int) -> int:
+        _java_int("setModelVariable capacity", capacity)
         arr = (ctypes.c_int * max(1, len(shape)))(*shape)
         return check(self._L.cbx_set_model_variable(self._ctx, id, order, len(shape), arr, capacity))
 
