@@ -1252,7 +1252,13 @@ int cbx_set_model_variable(cbx_context *c, int id, int order, int ndims, const i
   if (order != m.count_per_op[id] + 1)
     return fail(CBX_ERR_INVALID, "invalid model variable order (ndx=%d, ord=%d)", id, m.count_per_op[id] + 1);
   int64_t elements = 1;
-  for (int k = 0; k < ndims; ++k) elements *= shape[k];
+  for (int k = 0; k < ndims; ++k) {
+    if (shape[k] < 0) return fail(CBX_ERR_INVALID, "negative dimension %d of variable (%d, %d)", shape[k], id, order);
+    elements *= shape[k];
+  }
+  if (elements * 4 > capacity)
+    return fail(CBX_ERR_INVALID, "variable (%d, %d) of %lld floats exceeds its capacity of %d bytes", id, order,
+                (long long)elements, capacity);
   if (m.offset + capacity > m.bytes)
     return fail(CBX_ERR_INVALID, "variable overflows the model (%lld + %d > %lld)", (long long)m.offset, capacity,
                 (long long)m.bytes);
