@@ -69,6 +69,17 @@ def test_null_context_is_an_error_not_a_crash():
     assert lib.cbx_free(None) == _lib.CBX_OK
 
 
+def test_model_sizes_must_fit_a_java_int():
+    # TheGPU.setModel(II) / setModelVariable take Java ints (model.h:35 `int bytes`);
+    # the wrapper refuses a size ctypes would silently wrap, before any library call.
+    from crossbow_amd import CbxError, TheGPU
+    g = TheGPU()
+    with pytest.raises(CbxError, match="Java int"):
+        g.setModel(1, 2**31)
+    with pytest.raises(CbxError, match="Java int"):
+        g.setModelVariable(0, 1, [2**29], 2**31)
+
+
 # The model-path natives of TheGPU.java (:268-354) the shim must export.
 JNI_NATIVES = [
     "init", "free", "setModel", "setModelVariable", "setModelVariableBuffer",
