@@ -729,3 +729,57 @@ def test_cross_step_pipeline(momentum, bucket):
         compare_states(download(g, st), want)
     finally:
         g.free()
+
+
+def test_cross_step_pipeline_randomised_long_run():
+    # 60 steps in pipeline mode 1 with a random mix of Phase-D requests, SSP
+    # holds, host writes between steps, bucket-size changes (a new bucket
+    # count forces a full join) and mode switches, checked bit for bit
+    # against the oracle every 20 steps and at the end.
+    import random
+
+    from crossbow_amd import BUF_DATA
+    rng = random.Random(4242)
+    n, R = 200_003, 4
+    st = O.make_state(n, 1, R, 0.1, 0.9)
+    g = make_gpu(n, R, 0.1, 0.9, sync=1)
+    try:
+        g.set_force_split(True)
+        g.set_bucket_elements(16_384)
+        g.set_pipeline_mode(1)
+        upload(g, st)
+        want = st.clone()
+        for step in range(60):
+            want.locked[:] = 1
+            u = rng.random()
+            held = None
+            if u < 0.08:
+                i = rng.randrange(R)
+                g.set_replica_copy(i, True)
+                want.copy[i] = 1
+            elif u < 0.16:
+                held = rng.randrange(R)
+                g.replica_lock(held)
+                want.locked[held] = 0
+            elif u < 0.21:
+                i = rng.randrange(R)
+                new = O.fill_normal(n, 7000 + step, 0.05)
+                g.replica_write(i, BUF_DATA, new)
+                want.w[i] = new.copy()
+            elif u < 0.26:
+                g.set_bucket_elements(rng.choice([4096, 16_384, 65_536, 1 << 40]))
+            elif u < 0.30:
+                g.set_pipeline_mode(rng.choice([0, 1]))
+            g.lockAny()
+            g.synchronise(0, step + 1, 0, False)
+            g.unlockAny()
+            if held is not None:
+                g.replica_unlock(held)
+            O.sma_step(want)
+            if step % 20 == 19:
+                g.wait()
+                compare_states(download(g, st), want)
+        g.wait()
+        compare_states(download(g, st), want)
+    finally:
+        g.free()
