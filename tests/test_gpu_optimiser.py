@@ -278,3 +278,67 @@ def test_default_clock_loop_bitexact(momentum, on_torch_stream, aux):
         assert not np.array_equal(st.w[2], st.z[0]), "the held replica is not copied"
     finally:
         g.free()
+
+
+@pytest.mark.parametrize("pipeline", ["fused", "cross-step"])
+def test_threaded_clock_loop_bitexact(pipeline):
+    # The clock loop with the reference's threading: one task thread per
+    # replica, each on its own task (torch) stream, locking its replica,
+    # running its optimiser steps and releasing it; the result-collector
+    # thread runs the barrier once every task of the clock is done.  The
+    # optimiser kernels of different replicas interleave on the sync stream
+    # in whatever order the threads enqueue them, but touch disjoint
+    # replicas, so the result is deterministic: bit-exact vs the oracle.
+    import threading
+
+    import torch
+
+    from crossbow_amd import BUF_GRADIENT
+    from tests.helpers import compare_states, download, upload
+    n, R, clocks, wpc, alpha, momentum = 65_537, 4, 4, 3, 0.1, 0.9
+    g = _gpu(n, R, momentum, 1e-4, alpha=alpha)
+    try:
+        if pipeline == "cross-step":
+            g.set_force_split(True)
+            g.set_bucket_elements(8192)
+            g.set_pipeline_mode(1)
+        st = O.make_state(n, 1, R, alpha, momentum)
+        upload(g, st)
+        lasts = [np.zeros(n, np.float32) for _ in range(R)]
+        grads = {(c, i, k): O.fill_normal(n, 20_000 + 100 * c + 10 * i + k, 0.01)
+                 for c in range(clocks) for i in range(R) for k in range(wpc)}
+        streams = [torch.cuda.Stream() for _ in range(R)]
+        errors = []
+
+        def worker(i, clock):
+            try:
+                with torch.cuda.stream(streams[i]):
+                    for k in range(wpc):
+                        g.replica_lock(i)
+                        g.replica_write(i, BUF_GRADIENT, grads[(clock, i, k)])
+                        g.replica_optimise(i, (clock * R + i) * wpc + k, streams[i].cuda_stream)
+                        g.replica_task_done(i)
+                        g.replica_unlock(i)
+            except Exception as e:  # pragma: no cover - reported below
+                errors.append(repr(e))
+
+        for clock in range(clocks):
+            threads = [threading.Thread(target=worker, args=(i, clock)) for i in range(R)]
+            for t in threads:
+                t.start()
+            for t in threads:
+                t.join(timeout=60)
+            assert not errors, errors
+            for i in range(R):
+                for k in range(wpc):
+                    O.sma_optimise(np.float32(-0.05), momentum, 1e-4, st.w[i], grads[(clock, i, k)], lasts[i],
+                                   st.s[i])
+            assert g.lockAny() == R
+            g.synchronise(0, clock + 1, 0, False)
+            g.unlockAny()
+            O.sma_step(st)
+        g.wait()
+        torch.cuda.synchronize()
+        compare_states(download(g, st), st)
+    finally:
+        g.free()
