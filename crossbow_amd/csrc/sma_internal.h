@@ -128,6 +128,23 @@ inline unsigned lds_for_occupancy(const LaunchConfig &cfg, int reads, int writes
   return per;
 }
 
+// A launch too small to fill the chip 16 waves per CU over (LeNet's 4 MB
+// buffers, small G > 1 buckets) is latency-bound: with one element group per
+// lane every wave loads, then every wave stores, in lockstep across the chip.
+// In auto mode such a launch of one-wave blocks runs one float4 per lane in a
+// grid-stride loop over 8 blocks per CU instead, so waves fall out of step and
+// one iteration's stores overlap the next one's loads (scripts/lenet_sweep.py,
+// profiles/r01/lenet_sweep.jsonl: C2 22.6 -> 20.5 us).
+inline LaunchConfig small_launch_shape(const LaunchConfig &cfg, int64_t n4) {
+  if (cfg.waves_per_cu >= 0 || cfg.blocks_per_cu != 0 || cfg.block != 64) return cfg;
+  const int64_t waves = (n4 + 64ll * cfg.unroll - 1) / (64ll * cfg.unroll);
+  if (waves >= 16ll * cfg.num_cus) return cfg;
+  LaunchConfig c = cfg;
+  c.unroll = 1;
+  c.blocks_per_cu = 8;
+  return c;
+}
+
 // Every SMA launcher takes an optional (start, stop) event pair that the
 // dispatch itself timestamps (hipExtLaunchKernelGGL): timing a launch adds no
 // marker packets to the stream.  Pass nullptr for untimed launches.

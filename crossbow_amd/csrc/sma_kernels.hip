@@ -501,7 +501,8 @@ inline dim3 grid_for(int64_t n4, const LaunchConfig &cfg) {
 }
 
 template <int R, bool MOM, bool COPY, int P>
-hipError_t fused_u(const SmaArgs &a, const LaunchConfig &cfg, hipStream_t s, Timing t) {
+hipError_t fused_u(const SmaArgs &a, const LaunchConfig &cfg0, hipStream_t s, Timing t) {
+  const LaunchConfig cfg = small_launch_shape(cfg0, a.n4);
   const dim3 g = grid_for(a.n4, cfg);
   const unsigned lds = lds_for_occupancy(cfg, (COPY ? 1 : 2) * a.nrep + 1 + (MOM ? 1 : 0), a.nrep + 1 + (MOM ? 1 : 0), g.x);
   if (cfg.unroll == 4)
@@ -530,7 +531,8 @@ hipError_t fused_r(const SmaArgs &a, const LaunchConfig &cfg, hipStream_t s, Tim
 }
 
 template <int R, int P>
-hipError_t acc_u(const SmaArgs &a, const LaunchConfig &cfg, hipStream_t s, Timing t) {
+hipError_t acc_u(const SmaArgs &a, const LaunchConfig &cfg0, hipStream_t s, Timing t) {
+  const LaunchConfig cfg = small_launch_shape(cfg0, a.n4);
   const dim3 g = grid_for(a.n4, cfg);
   const unsigned lds = lds_for_occupancy(cfg, 2 * a.nrep + 1, a.nrep + 1, g.x);
   if (cfg.unroll == 4)
@@ -559,7 +561,8 @@ hipError_t acc_r(const SmaArgs &a, const LaunchConfig &cfg, hipStream_t s, Timin
 }
 
 template <bool MOM, int P>
-hipError_t apply_u(const SmaArgs &a, const LaunchConfig &cfg, hipStream_t s, Timing t) {
+hipError_t apply_u(const SmaArgs &a, const LaunchConfig &cfg0, hipStream_t s, Timing t) {
+  const LaunchConfig cfg = small_launch_shape(cfg0, a.n4);
   const dim3 g = grid_for(a.n4, cfg);
   const unsigned lds = lds_for_occupancy(cfg, MOM ? 3 : 2, MOM ? 2 : 1, g.x);
   if (cfg.unroll == 4)
