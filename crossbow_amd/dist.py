@@ -57,7 +57,7 @@ def max_over_ranks(value: float, world: int) -> float:
 
 
 def tune_buckets(gpu, n: int, world: int, step: Callable[[], None], candidates=(1, 2, 4, 8, 16),
-                 steps: int = 4, warmup: int = 2, modes=(0, 1)):
+                 steps: int = 10, warmup: int = 2, modes=(0, 1), passes: int = 2):
     """Pick the bucket count of the G > 1 pipeline (kernel A / RCCL
     all-reduce / kernel B per bucket) by timing each candidate on the live
     communicator, the way a runtime tunes itself in its warm-up.
@@ -71,26 +71,29 @@ def tune_buckets(gpu, n: int, world: int, step: Callable[[], None], candidates=(
     stays identical on every rank.  ``step()`` runs one barrier step.
     With more than one bucket each count is also timed in both pipeline
     modes (``gpu.set_pipeline_mode``: 0 within a step, 1 across steps).
-    Returns (bucket_elements, mode, {"<buckets>/<mode>": ms_per_step}).
+    The candidates are timed in ``passes`` interleaved passes and each keeps
+    its best pass, so one noisy sample (a few percent on one GPU) does not
+    decide.  Returns (bucket_elements, mode, {"<buckets>/<mode>": ms_per_step}).
     """
     import time
 
     results = {}
-    for nb in candidates:
-        elems = (1 << 62) if nb <= 1 else max(1, -(-n // nb))
-        for mode in (modes if nb > 1 else (0,)):
-            gpu.set_bucket_elements(elems)
-            gpu.set_pipeline_mode(mode)
-            for _ in range(warmup):
-                step()
-            gpu.wait()
-            barrier(world)
-            t0 = time.perf_counter()
-            for _ in range(steps):
-                step()
-            gpu.wait()
-            ms = (time.perf_counter() - t0) * 1e3 / steps
-            results[(nb, mode)] = max_over_ranks(ms, world)
+    for _ in range(max(1, passes)):
+        for nb in candidates:
+            elems = (1 << 62) if nb <= 1 else max(1, -(-n // nb))
+            for mode in (modes if nb > 1 else (0,)):
+                gpu.set_bucket_elements(elems)
+                gpu.set_pipeline_mode(mode)
+                for _ in range(warmup):
+                    step()
+                gpu.wait()
+                barrier(world)
+                t0 = time.perf_counter()
+                for _ in range(steps):
+                    step()
+                gpu.wait()
+                ms = max_over_ranks((time.perf_counter() - t0) * 1e3 / steps, world)
+                results[(nb, mode)] = min(ms, results.get((nb, mode), ms))
     best = min(results, key=lambda k: (results[k], k))
     nb, mode = best
     elems = (1 << 62) if nb <= 1 else max(1, -(-n // nb))
