@@ -242,10 +242,12 @@ def _bn_case(L, A, rank, world, uid):
         L.cbx_free(c)
 
 
-def _autotune_case(L, A, rank, world, uid):
+def _autotune_case(L, A, rank, world, uid, ckdir):
     # synchronise(autotune = +1 / -1) adds / deletes one replica per device
     # after the step (executioncontext.c:2321-2328, modelmanager.c:362-557):
     # a new replica copies its device's first replica and joins the next step.
+    # Then every rank checkpoints into one shared directory (each writes its
+    # own device's files, with one BN operator's statistics) and reads it back.
     import sys
     sys.path.insert(0, ROOT)
     from oracle import oracle as O
@@ -291,6 +293,34 @@ def _autotune_case(L, A, rank, world, uid):
                  for i in range(st.size) if i % world == rank]:
             if not np.array_equal(got.view(np.uint32), want.view(np.uint32)):
                 bad.append(f"autotune {what} differs")
+        # checkpoint (executioncontext.c:2340-2364) into the shared directory
+        os.makedirs(ckdir, exist_ok=True)
+        p = ctypes.c_void_p()
+        g("cbx_base_buffer", rank, A.BUF_GRADIENT, ctypes.byref(p))  # scratch for BN statistics
+        bn = O.fill_normal(2 * 33, 300 + rank, 0.5)
+        hip = ctypes.CDLL("libamdhip64.so")
+        hip.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+        assert hip.hipMemcpy(p.value, bn.ctypes.data, bn.nbytes, 1) == 0
+        pm = (ctypes.c_void_p * 1)(p.value)
+        pv = (ctypes.c_void_p * 1)(p.value + 4 * 33)
+        g("cbx_register_batchnorm_stats", 7, 33, ctypes.cast(pm, ctypes.POINTER(ctypes.c_void_p)),
+          ctypes.cast(pv, ctypes.POINTER(ctypes.c_void_p)))
+        ckb = ckdir.encode()
+        g("cbx_checkpoint_model", ckb)
+        ver = os.path.join(ckdir, "000001")
+        files = {f"gpu-{rank:02d}-theModel-data.dat": st.z[rank], f"gpu-{rank:02d}-theModel-last.dat": st.last[rank],
+                 f"gpu-{rank:02d}-bn-avg-007.dat": bn[:33], f"gpu-{rank:02d}-bn-var-007.dat": bn[33:]}
+        files.update({f"gpu-{rank:02d}-replica-{i:03d}-data.dat": st.w[i] for i in range(st.size) if i % world == rank})
+        for name, want in files.items():
+            path = os.path.join(ver, name)
+            if not os.path.exists(path):
+                bad.append(f"checkpoint: {name} missing")
+            elif not np.array_equal(np.fromfile(path, "<f4").view(np.uint32), want.view(np.uint32)):
+                bad.append(f"checkpoint: {name} differs")
+        g.write("cbx_base_write", rank, A.BUF_DATA, np.zeros(n, np.float32))
+        g("cbx_override_model_data", ver.encode())
+        if not np.array_equal(g.read("cbx_base_read", rank, A.BUF_DATA, n).view(np.uint32), st.z[rank].view(np.uint32)):
+            bad.append("override: z not restored")
         return bad
     finally:
         L.cbx_free(c)
@@ -305,7 +335,7 @@ def _rank_main(rank, world, uids, fake_dir, q):
         for case, uid in zip(_cases(world), uids):
             out.append((case[0], _case(L, A, rank, world, uid, case)))
         out.append(("bn", _bn_case(L, A, rank, world, uids[-2])))
-        out.append(("autotune", _autotune_case(L, A, rank, world, uids[-1])))
+        out.append(("autotune", _autotune_case(L, A, rank, world, uids[-1], os.path.join(fake_dir, "ckpt"))))
         q.put((rank, out, None))
     except Exception:  # pragma: no cover - reported to the parent
         import traceback
