@@ -55,7 +55,7 @@ def build_lib(force: bool = False, verbose: bool = False) -> str:
            # fp32 results must equal the reference's cuBLAS op order bit for bit: every
            # fma is written explicitly, nothing may be contracted behind our back.
            "-ffp-contract=off",
-           "-I", os.path.join(ROOT, "include"), "-o", tmp] + _sources() + ["-lrccl", "-lpthread"]
+           "-I", os.path.join(ROOT, "include"), "-o", tmp] + _sources() + ["-lrccl", "-lrocprofiler-sdk-roctx", "-lpthread"]
     if verbose:
         print(" ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)

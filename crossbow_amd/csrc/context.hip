@@ -16,6 +16,7 @@
 //   * errors return codes; the JNI shim turns them back into exit(1).
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
+#include <rocprofiler-sdk-roctx/roctx.h>
 
 #include <pthread.h>
 #include <sched.h>
@@ -67,6 +68,17 @@ int fail(int code, const char *fmt, ...) {
     if (r_ != ncclSuccess)                                                                         \
       return fail(CBX_ERR_RCCL, "%s:%d %s: %s", __FILE__, __LINE__, #call, ncclGetErrorString(r_)); \
   } while (0)
+
+// ROCTx range over one C-ABI call (tracing): rocprofv3
+// --marker-trace shows each barrier step, staging pass, checkpoint and task
+// step as a host range beside its kernels.  Without a tool attached a push /
+// pop is a call through an empty dispatch table.
+struct TraceRange {
+  explicit TraceRange(const char *name) { roctxRangePushA(name); }
+  ~TraceRange() { roctxRangePop(); }
+  TraceRange(const TraceRange &) = delete;
+  TraceRange &operator=(const TraceRange &) = delete;
+};
 
 #define TRY(expr)            \
   do {                       \
@@ -1536,6 +1548,7 @@ static int default_step(cbx_context *c, int first);
 // staged: 0 = device-resident step; > 0 = host-staged step over that many
 // buckets (cbx_synchronise_staged).
 static int synchronise_impl(cbx_context *c, int first, int clock, int autotune, int staged) {
+  TraceRange trace(staged ? "cbx_synchronise_staged" : "cbx_synchronise");
   TRY(check_manager_q(c));
   if (first < 0 || first > c->size) return fail(CBX_ERR_INVALID, "first replica %d out of range", first);
   // executioncontext.c:2287-2315: SYNCHRONOUSEAMSGD (3) routes to SMA because
@@ -1595,6 +1608,7 @@ int cbx_unlock_any(cbx_context *c) {
 static int batchnorm_checkpoint(cbx_context *c, const std::string &dir, bool store);
 
 int cbx_checkpoint_model(cbx_context *c, const char *dir) {
+  TraceRange trace("cbx_checkpoint_model");
   TRY(check_manager(c));
   if (!dir) return fail(CBX_ERR_INVALID, "null checkpoint directory");
   // executioncontext.c:2340-2350: dir/%06llu, a new version per call.
@@ -1621,6 +1635,7 @@ int cbx_checkpoint_model(cbx_context *c, const char *dir) {
 }
 
 int cbx_override_model_data(cbx_context *c, const char *dir) {
+  TraceRange trace("cbx_override_model_data");
   TRY(check_manager(c));
   if (!dir) return CBX_OK;  // GPU.c:1169: a null directory is a no-op
   TRY(cbx_wait(c));
@@ -1906,6 +1921,7 @@ static int replica_optimise_impl(cbx_context *c, int id, int task, void *stream)
 // between the two then sees it move again, and the next step joins the
 // whole sync stream, which by then holds this call's wait.
 int cbx_replica_optimise(cbx_context *c, int id, int task, void *stream) {
+  TraceRange trace("cbx_replica_optimise");
   const int rc = replica_optimise_impl(c, id, task, stream);
   if (c) c->foreign_ops.fetch_add(1, std::memory_order_release);
   return rc;
@@ -1970,6 +1986,7 @@ static int grow(void **p, size_t *have, size_t need) {
 
 int cbx_average_batchnorm_stats(cbx_context *c, int layers, const int *elements, float *const *mean,
                                 float *const *variance, const int *updated) {
+  TraceRange trace("cbx_average_batchnorm_stats");
   TRY(check_ctx(c));
   if (layers < 0 || (layers > 0 && (!elements || !mean || !variance || !updated)))
     return fail(CBX_ERR_INVALID, "bad batch-norm statistics arguments");
@@ -2272,6 +2289,7 @@ int cbx_base_read(cbx_context *c, int g, int kind, void *dst, size_t bytes) {
 
 // ---- staging --------------------------------------------------------------
 int cbx_stage_in(cbx_context *c) {
+  TraceRange trace("cbx_stage_in");
   TRY(check_manager(c));
   TRY(alloc_host_mirror(c));
   const size_t bytes = (size_t)c->n * 4;
@@ -2292,6 +2310,7 @@ int cbx_stage_in(cbx_context *c) {
 }
 
 int cbx_stage_out(cbx_context *c) {
+  TraceRange trace("cbx_stage_out");
   TRY(check_manager(c));
   TRY(alloc_host_mirror(c));
   const size_t bytes = (size_t)c->n * 4;

@@ -16,6 +16,6 @@ trap 'rm -rf "$TMP"' EXIT
   -Xarch_host -fsanitize=address -Xarch_host -fsanitize=undefined \
   -I include -o "$OUT.tmp" \
   crossbow_amd/csrc/context.hip crossbow_amd/csrc/sma_kernels.hip -x none "$TMP/abi_driver.o" \
-  -lrccl -lpthread
+  -lrccl -lrocprofiler-sdk-roctx -lpthread
 mv "$OUT.tmp" "$OUT"
 echo "built $OUT"
