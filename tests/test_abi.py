@@ -115,3 +115,57 @@ def test_jni_shim_compiles_against_the_c_abi():
                         "-I", os.path.join(ROOT, "tests", "jni_stub"), "-I", os.path.join(ROOT, "include"),
                         JNI_SRC], capture_output=True, text=True)
     assert r.returncode == 0, r.stderr
+
+
+CPP_POLICY = r"""
+#include <cstdio>
+#include <stdexcept>
+#include "ModelManager.hpp"
+#define EXPECT(c) do { if (!(c)) { std::printf("failed: %s\n", #c); return 1; } } while (0)
+int main() {
+  crossbow::SystemConf c;
+  c.wpc = 3; c.checkpointInterval = 7;             // ModelManager.java:73-80: 7 tasks -> 9 -> 3 clocks
+  EXPECT(crossbow::ModelManager(nullptr, c).checkpointStep() == 3);
+  c.autotuneModels = true; c.autotuneInterval = 2; c.autotuneThreshold = 0.1;
+  crossbow::ModelManager m(nullptr, c);
+  bool threw = false;                              // :243-244: no monitor
+  try { m.autotune(); m.autotune(); } catch (const std::logic_error &) { threw = true; }
+  EXPECT(threw);
+  crossbow::ModelManager a(nullptr, c);
+  const double tp[] = {10.0, 12.0, 12.5};
+  int k = 0;
+  a.setPerformanceMonitor([&] { return tp[k++]; });
+  int got[8];
+  for (int i = 0; i < 8; ++i) got[i] = a.autotune();  // :257-274
+  const int want[8] = {0, 1, 0, 1, 0, -1, 0, 0};   // first reading, +20 %, +4.2 % (< 10 %)
+  for (int i = 0; i < 8; ++i) EXPECT(got[i] == want[i]);
+  EXPECT(k == 3 && !a.autotuning());
+  crossbow::SystemConf off;                        // SystemConf.java:228: autotuning off
+  EXPECT(crossbow::ModelManager(nullptr, off).autotune() == 0);
+  std::printf("ok\n");
+  return 0;
+}
+"""
+
+
+def test_cpp_model_manager_policy(tmp_path):
+    # crossbow_amd/host/ModelManager.hpp (the Java ModelManager restated in C++):
+    # compiled against crossbow_sma.h and run here for its host-side policy
+    # (checkpoint step, autotune decisions, null monitor); the GPU test
+    # (tests/test_gpu_host.py) runs its barrier and checkpoint calls.
+    import shutil
+    import subprocess
+    gxx = shutil.which("g++")
+    if gxx is None:
+        pytest.skip("no g++")
+    src = tmp_path / "policy.cpp"
+    src.write_text(CPP_POLICY)
+    exe = tmp_path / "policy"
+    lib_dir = os.path.join(ROOT, "crossbow_amd")
+    r = subprocess.run([gxx, "-std=c++17", "-Wall", "-Wextra", "-Werror",
+                        "-I", os.path.join(ROOT, "crossbow_amd", "host"), "-I", os.path.join(ROOT, "include"),
+                        "-o", str(exe), str(src), "-L", lib_dir, "-lcrossbow_sma", f"-Wl,-rpath,{lib_dir}"],
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0 and "ok" in r.stdout, r.stdout + r.stderr
