@@ -289,6 +289,8 @@ struct cbx_context {
   // Write-heavy barrier kernels of DEFAULT and S-SGD (scripts/barrier_sweep.py).
   cbx::LaunchConfig broadcast_cfg = cbx::broadcast_launch_config();
   cbx::LaunchConfig ssgd_apply_cfg = cbx::ssgd_apply_launch_config();
+  // Kernel B of the split SMA path (scripts/apply_sweep.py).
+  cbx::LaunchConfig apply_cfg = cbx::sma_apply_launch_config();
   int64_t bucket_elems = 0;
   bool force_split = false;
   bool last_step_split = false;
@@ -769,7 +771,7 @@ int sma_step(cbx_context *c, int first) {
         Device &d = c->devs[k];
         HIP_TRY(hipSetDevice(d.hip_id));
         if (pipelined) HIP_TRY(hipStreamWaitEvent(d.stream, d.bucket_red[b], 0));
-        cbx::LaunchConfig cfg = c->cfg;
+        cbx::LaunchConfig cfg = c->apply_cfg;
         cfg.num_cus = d.num_cus;
         cbx::Timing t;
         if (b == nb - 1) t.stop = step_stop_event(c, d, EV_B);
@@ -949,7 +951,7 @@ int sma_step_staged(cbx_context *c, int first, int buckets) {
       for (size_t k = 0; k < c->devs.size(); ++k) {
         Device &d = c->devs[k];
         HIP_TRY(hipSetDevice(d.hip_id));
-        cbx::LaunchConfig cfg = c->cfg;
+        cbx::LaunchConfig cfg = c->apply_cfg;
         cfg.num_cus = d.num_cus;
         HIP_TRY(cbx::launch_sma_apply(offset_args(args[k], s4, l4), mom, cfg, d.stream));
       }
@@ -2446,6 +2448,7 @@ int cbx_set_kernel_config(cbx_context *c, int block, int blocks_per_cu, int poli
   c->cfg.block = block;
   c->cfg.blocks_per_cu = blocks_per_cu;
   c->cfg.policy = policy;
+  c->apply_cfg.policy = policy;  // load/store policy is shared; kernel B keeps its own geometry
   c->cfg.unroll = unroll;
   return CBX_OK;
 }
@@ -2482,6 +2485,19 @@ int cbx_set_barrier_kernel_config(cbx_context *c, int block, int unroll, int wav
     cfg->unroll = unroll;
     cfg->waves_per_cu = waves_per_cu;
   }
+  return CBX_OK;
+}
+
+int cbx_set_apply_kernel_config(cbx_context *c, int block, int unroll, int waves_per_cu) {
+  TRY(check_ctx(c));
+  if (block < 64 || block > 256 || block % 64 != 0) return fail(CBX_ERR_INVALID, "block must be 64..256, multiple of 64");
+  if (unroll != 1 && unroll != 2 && unroll != 4) return fail(CBX_ERR_INVALID, "unroll must be 1, 2 or 4");
+  if ((int64_t)block * unroll > cbx::kPadFloat4 || cbx::kPadFloat4 % ((int64_t)block * unroll) != 0)
+    return fail(CBX_ERR_INVALID, "block*unroll must divide %lld", (long long)cbx::kPadFloat4);
+  if (waves_per_cu < -1 || waves_per_cu > 32) return fail(CBX_ERR_INVALID, "waves per CU must be -1 (auto) or 0..32");
+  c->apply_cfg.block = block;
+  c->apply_cfg.unroll = unroll;
+  c->apply_cfg.waves_per_cu = waves_per_cu;
   return CBX_OK;
 }
 

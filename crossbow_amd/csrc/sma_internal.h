@@ -90,6 +90,15 @@ inline LaunchConfig broadcast_launch_config() {
   c.waves_per_cu = 8;
   return c;
 }
+// Kernel B of the G > 1 split path (sma_apply_kernel: 3 reads + 2 writes);
+// cbx_set_apply_kernel_config overrides it.
+inline LaunchConfig sma_apply_launch_config() {
+  LaunchConfig c;
+  c.block = 64;
+  c.unroll = 2;
+  c.waves_per_cu = -1;
+  return c;
+}
 inline LaunchConfig ssgd_apply_launch_config() {
   LaunchConfig c;
   c.block = 64;

@@ -382,6 +382,10 @@ class TheGPU:
     def set_barrier_kernel_config(self, block: int, unroll: int, waves_per_cu: int) -> None:
         check(self._L.cbx_set_barrier_kernel_config(self._ctx, block, unroll, waves_per_cu))
 
+    def set_apply_kernel_config(self, block: int, unroll: int, waves_per_cu: int) -> None:
+        """Launch geometry of kernel B (Phase C) of the split SMA path."""
+        check(self._L.cbx_set_apply_kernel_config(self._ctx, block, unroll, waves_per_cu))
+
     def set_pipeline_mode(self, mode: int) -> None:
         """0: buckets overlap within a step; 1: also across steps."""
         check(self._L.cbx_set_pipeline_mode(self._ctx, mode))

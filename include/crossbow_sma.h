@@ -327,6 +327,10 @@ int cbx_set_aux_kernel_config (cbx_context *ctx, int block, int unroll, int wave
  * and the S-SGD apply), same arguments as above; defaults are per kernel
  * (256 / 1 / 8 and 64 / 2 / 3, measured).                                */
 int cbx_set_barrier_kernel_config (cbx_context *ctx, int block, int unroll, int waves_per_cu);
+/* Launch geometry of kernel B of the G > 1 split SMA path (Phase C,
+ * sma.c:135-183: 3 reads + 2 writes per element): block 64..256, unroll 1,
+ * 2 or 4, occupancy cap as above.  Default 64 / 2 / auto.                 */
+int cbx_set_apply_kernel_config (cbx_context *ctx, int block, int unroll, int waves_per_cu);
 /* Bucketed pipeline for G > 1: kernel A / all-reduce / kernel B per bucket
  * of `bucket_elements` floats; 0 (default) = 8 buckets when G > 1, one at
  * G = 1; a value >= n = one bucket, all in order on the sync stream.  With

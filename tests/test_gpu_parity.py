@@ -19,7 +19,7 @@ pytestmark = pytest.mark.gpu
 
 
 def _run(n, R, alpha, momentum, copy_ids=(), first=0, held=(), sync=0, config=None, split=False,
-         bucket=0, steps=1):
+         bucket=0, steps=1, apply=None):
     st = O.make_state(n, 1, R, alpha, momentum)
     g = make_gpu(n, R, alpha, momentum, sync=sync)
     try:
@@ -30,6 +30,8 @@ def _run(n, R, alpha, momentum, copy_ids=(), first=0, held=(), sync=0, config=No
             g.set_kernel_occupancy(occ)
         if split:
             g.set_force_split(True)
+        if apply:
+            g.set_apply_kernel_config(*apply)
         if bucket:
             g.set_bucket_elements(bucket)
         upload(g, st)
@@ -162,6 +164,14 @@ def test_launch_configs_identical(config):
 def test_split_pipeline_one_rank(momentum):
     # Kernel A + RCCL all-reduce (one-rank communicator) + kernel B.
     _run(4099, 4, 0.1, momentum, split=True)
+
+
+@pytest.mark.parametrize("apply", [(64, 1, -1), (64, 1, 2), (64, 4, 0), (128, 2, 4), (256, 1, 8), (256, 2, -1)])
+def test_split_apply_launch_shapes_identical(apply):
+    # Kernel B's own launch geometry (cbx_set_apply_kernel_config): ragged n,
+    # one bucket and 5 buckets, Phase D on the second step.
+    _run(300_001, 3, 0.1, 0.9, split=True, apply=apply, copy_ids=(1,), steps=2)
+    _run(300_001, 3, 0.1, 0.9, split=True, apply=apply, bucket=65_536, steps=2)
 
 
 def test_split_pipeline_buckets_and_copy():
