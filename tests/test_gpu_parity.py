@@ -77,6 +77,30 @@ def test_fused_generic_replica_count(R):
     _run(1031, R, 0.1, 0.9)
 
 
+@pytest.mark.parametrize("n", [1, 3, 4, 5, 63, 64, 65, 255, 257, 4096 * 16 + 1])
+@pytest.mark.parametrize("split", [False, True])
+def test_tiny_and_ragged_sizes(n, split):
+    # Sub-float4 and wave-boundary sizes: the float4 tail lives in the arena's
+    # padding, which the step must never let leak into the n real elements.
+    _run(n, 3, 0.1, 0.9, split=split, copy_ids=(0,) if n % 2 else (), steps=2)
+
+
+@pytest.mark.parametrize("R", [9, 17, 64])
+def test_chunked_replicas_split_path(R):
+    # > 8 replicas per GPU in kernel A (chunks of 8) and the maximum, 64, fused.
+    _run(2053, R, 0.1, 0.9, split=True, steps=2)
+    if R == 64:
+        _run(2053, R, 0.1, 0.9, steps=2)
+
+
+@pytest.mark.parametrize("alpha", [0.0, 1.0, 1e-30])
+def test_alpha_extremes(alpha):
+    # alpha 0: replicas and acc unchanged, z moves by momentum only;
+    # alpha 1: replicas jump by their whole elastic difference; denormal-range alpha.
+    _run(4099, 4, alpha, 0.9)
+    _run(4099, 4, alpha, 0.9, split=True)
+
+
 def test_lenet_size_alpha_half():
     # C2: LeNet, 4 replicas on 1 GPU, alpha = 0.5 (SolverConf default).
     _run(1_111_946, 4, 0.5, 0.0)
