@@ -295,6 +295,9 @@ struct cbx_context {
   bool force_split = false;
   bool last_step_split = false;
   int pipeline_mode = 0;  // 0 bucketed within a step, 1 across steps (G > 1 split path)
+  // Bucket events as kernel stop events (default); CBX_SEPARATE_EVENT_RECORDS=1
+  // at context creation restores separate hipEventRecord markers, for A/B runs.
+  bool dispatch_events = !(getenv("CBX_SEPARATE_EVENT_RECORDS") && getenv("CBX_SEPARATE_EVENT_RECORDS")[0] == '1');
   // Bumped by every C-ABI call that may enqueue work on a sync stream other
   // than the barrier path itself: a cross-step pipelined step then joins the
   // whole sync stream instead of waiting bucket by bucket.
@@ -679,6 +682,11 @@ int sma_step(cbx_context *c, int first) {
     // A step joins the whole sync stream instead when anything else was
     // enqueued since the last cross-pipelined step (foreign_ops).
     const bool cross = pipelined && c->pipeline_mode == 1;
+    // Per-bucket events ride on the kernels' own dispatch packets (stop
+    // event) instead of a separate hipEventRecord marker, which left a
+    // ~10 us gap on the sync stream per bucket: -2 to -8 % per step
+    // (scripts/dispatch_event_ab.py, profiles/r01/dispatch_event_ab.json).
+    const bool dispatch_events = c->dispatch_events;
     const unsigned long long foreign = c->foreign_ops.load(std::memory_order_acquire);
     std::vector<char> join(c->devs.size(), 1);
     for (size_t k = 0; k < c->devs.size(); ++k) {
@@ -687,9 +695,10 @@ int sma_step(cbx_context *c, int first) {
       if (pipelined) {
         while ((int64_t)d.bucket_acc.size() < nb) {
           hipEvent_t ea, er, eb;
-          HIP_TRY(hipEventCreateWithFlags(&ea, hipEventDisableTiming));
+          // ea / eb are also handed to kernel dispatches as their stop events.
+          HIP_TRY(hipEventCreate(&ea));
           HIP_TRY(hipEventCreateWithFlags(&er, hipEventDisableTiming));
-          HIP_TRY(hipEventCreateWithFlags(&eb, hipEventDisableTiming));
+          HIP_TRY(hipEventCreate(&eb));
           d.bucket_acc.push_back(ea);
           d.bucket_red.push_back(er);
           d.bucket_b.push_back(eb);
@@ -759,8 +768,10 @@ int sma_step(cbx_context *c, int first) {
         if (!pipelined) t.stop = ring_event(c, d, EV_A);
         hipStream_t st = cross ? d.a_stream : d.stream;
         if (cross && !join[k]) HIP_TRY(hipStreamWaitEvent(st, d.bucket_b[b], 0));  // B(b) of the last step
+        const bool in_dispatch = pipelined && dispatch_events;
+        if (in_dispatch) t.stop = d.bucket_acc[b];
         HIP_TRY(cbx::launch_sma_accumulate(offset_args(args[k], start, len), b == 0, cfg, st, t));
-        if (pipelined) HIP_TRY(hipEventRecord(d.bucket_acc[b], st));
+        if (pipelined && !in_dispatch) HIP_TRY(hipEventRecord(d.bucket_acc[b], st));
       }
       return CBX_OK;
     };
@@ -783,8 +794,10 @@ int sma_step(cbx_context *c, int first) {
           a.decision_mode = b == 0 ? 1 : 2;
           a.decision = d.decision + (d.cross_parity & 1u);
         }
+        const bool in_dispatch = cross && dispatch_events && !t.stop;
+        if (in_dispatch) t.stop = d.bucket_b[b];
         HIP_TRY(cbx::launch_sma_apply(a, mom, cfg, d.stream, t));
-        if (cross) HIP_TRY(hipEventRecord(d.bucket_b[b], d.stream));
+        if (cross && !in_dispatch) HIP_TRY(hipEventRecord(d.bucket_b[b], d.stream));
       }
       return CBX_OK;
     };

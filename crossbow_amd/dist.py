@@ -64,7 +64,8 @@ def tune_buckets(gpu, n: int, world: int, step: Callable[[], None], candidates=(
 
     More buckets hide more of the all-reduce behind kernel A, but each bucket
     costs fixed time (a cross-stream event, a shorter launch's ramp and drain:
-    ~16-20 us per bucket on one MI355X, profiles/r01/split_pipeline_trace.txt),
+    ~7 us per bucket on one MI355X with the bucket events on the kernel dispatches,
+    profiles/r01/bench_force_split_tuned.json),
     so the best count depends on how long the all-reduce is, i.e. on G and the
     xGMI links.  Every rank times every candidate, the times are max-reduced
     over ranks, and all ranks take the same argmin, so the RCCL call sequence
