@@ -294,7 +294,7 @@ struct cbx_context {
   int64_t bucket_elems = 0;
   bool force_split = false;
   bool last_step_split = false;
-  int pipeline_mode = 0;  // 0 bucketed within a step, 1 across steps (G > 1 split path)
+  int pipeline_mode = 0;  // 0 bucketed within a step, 1 across steps, 2 as 1 with B on comm_stream (G > 1 split path)
   // Bucket events as kernel stop events (default); CBX_SEPARATE_EVENT_RECORDS=1
   // at context creation restores separate hipEventRecord markers, for A/B runs.
   bool dispatch_events = !(getenv("CBX_SEPARATE_EVENT_RECORDS") && getenv("CBX_SEPARATE_EVENT_RECORDS")[0] == '1');
@@ -681,7 +681,14 @@ int sma_step(cbx_context *c, int first) {
     //   stream      : [wait red(0)] B(0) [wait red(1)] B(1) ...
     // A step joins the whole sync stream instead when anything else was
     // enqueued since the last cross-pipelined step (foreign_ops).
-    const bool cross = pipelined && c->pipeline_mode == 1;
+    const bool cross = pipelined && c->pipeline_mode >= 1;
+    // Mode 2: as mode 1, but kernel B(k) runs on comm_stream right behind
+    // AR(k), so no event separates them and the sync stream joins once per
+    // step (after the last B) instead of waiting once per bucket:
+    //   a_stream    : [wait b(0)'] A(0) [wait b(1)'] A(1) ...
+    //   comm_stream : [wait acc(0)] AR(0) B(0) [wait acc(1)] AR(1) B(1) ...
+    //   stream      :                                  ... [wait B(nb-1)]
+    const bool b_on_comm = cross && c->pipeline_mode == 2;
     // Per-bucket events ride on the kernels' own dispatch packets (stop
     // event) instead of a separate hipEventRecord marker, which left a
     // ~10 us gap on the sync stream per bucket: -2 to -8 % per step
@@ -746,7 +753,7 @@ int sma_step(cbx_context *c, int first) {
         NCCL_TRY(ncclAllReduce(src, dst, count, ncclFloat, ncclSum, d.comm, on_comm ? d.comm_stream : d.stream));
       }
       NCCL_TRY(ncclGroupEnd());
-      if (on_comm) {
+      if (on_comm && !b_on_comm) {
         for (size_t k = 0; k < c->devs.size(); ++k) {
           Device &d = c->devs[k];
           HIP_TRY(hipSetDevice(d.hip_id));
@@ -781,7 +788,8 @@ int sma_step(cbx_context *c, int first) {
       for (size_t k = 0; k < c->devs.size(); ++k) {
         Device &d = c->devs[k];
         HIP_TRY(hipSetDevice(d.hip_id));
-        if (pipelined) HIP_TRY(hipStreamWaitEvent(d.stream, d.bucket_red[b], 0));
+        hipStream_t st = b_on_comm ? d.comm_stream : d.stream;
+        if (pipelined && !b_on_comm) HIP_TRY(hipStreamWaitEvent(d.stream, d.bucket_red[b], 0));
         cbx::LaunchConfig cfg = c->apply_cfg;
         cfg.num_cus = d.num_cus;
         cbx::Timing t;
@@ -796,8 +804,10 @@ int sma_step(cbx_context *c, int first) {
         }
         const bool in_dispatch = cross && dispatch_events && !t.stop;
         if (in_dispatch) t.stop = d.bucket_b[b];
-        HIP_TRY(cbx::launch_sma_apply(a, mom, cfg, d.stream, t));
-        if (cross && !in_dispatch) HIP_TRY(hipEventRecord(d.bucket_b[b], d.stream));
+        HIP_TRY(cbx::launch_sma_apply(a, mom, cfg, st, t));
+        if (cross && !in_dispatch) HIP_TRY(hipEventRecord(d.bucket_b[b], st));
+        // The step's last kernel ran on comm_stream: join it into the sync stream.
+        if (b_on_comm && b == nb - 1) HIP_TRY(hipStreamWaitEvent(d.stream, t.stop, 0));
       }
       return CBX_OK;
     };
@@ -2516,7 +2526,7 @@ int cbx_set_apply_kernel_config(cbx_context *c, int block, int unroll, int waves
 
 int cbx_set_pipeline_mode(cbx_context *c, int mode) {
   TRY(check_ctx(c));
-  if (mode != 0 && mode != 1) return fail(CBX_ERR_INVALID, "pipeline mode must be 0 or 1");
+  if (mode < 0 || mode > 2) return fail(CBX_ERR_INVALID, "pipeline mode must be 0, 1 or 2");
   c->pipeline_mode = mode;
   return CBX_OK;
 }

@@ -57,7 +57,7 @@ def max_over_ranks(value: float, world: int) -> float:
 
 
 def tune_buckets(gpu, n: int, world: int, step: Callable[[], None], candidates=(1, 2, 4, 8, 16),
-                 steps: int = 10, warmup: int = 2, modes=(0, 1), passes: int = 2):
+                 steps: int = 10, warmup: int = 2, modes=(0, 1, 2), passes: int = 2):
     """Pick the bucket count of the G > 1 pipeline (kernel A / RCCL
     all-reduce / kernel B per bucket) by timing each candidate on the live
     communicator, the way a runtime tunes itself in its warm-up.
@@ -71,7 +71,8 @@ def tune_buckets(gpu, n: int, world: int, step: Callable[[], None], candidates=(
     over ranks, and all ranks take the same argmin, so the RCCL call sequence
     stays identical on every rank.  ``step()`` runs one barrier step.
     With more than one bucket each count is also timed in both pipeline
-    modes (``gpu.set_pipeline_mode``: 0 within a step, 1 across steps).
+    modes (``gpu.set_pipeline_mode``: 0 within a step, 1 across steps, 2 across
+    steps with kernel B on the all-reduce's stream).
     The candidates are timed in ``passes`` interleaved passes and each keeps
     its best pass, so one noisy sample (a few percent on one GPU) does not
     decide.  Returns (bucket_elements, mode, {"<buckets>/<mode>": ms_per_step}).

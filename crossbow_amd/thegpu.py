@@ -387,7 +387,7 @@ class TheGPU:
         check(self._L.cbx_set_apply_kernel_config(self._ctx, block, unroll, waves_per_cu))
 
     def set_pipeline_mode(self, mode: int) -> None:
-        """0: buckets overlap within a step; 1: also across steps."""
+        """0: buckets overlap within a step; 1: also across steps; 2: as 1, kernel B on the all-reduce stream."""
         check(self._L.cbx_set_pipeline_mode(self._ctx, mode))
 
     def set_bucket_elements(self, elements: int) -> None:

@@ -342,8 +342,10 @@ int cbx_set_bucket_elements (cbx_context *ctx, long long bucket_elements);
  * stream and A(k) waits only for B(k) of the previous step, so the next
  * step's first buckets run while this step's last all-reduces are on the
  * link.  Any other C-ABI call between two steps that may enqueue device
- * work makes the next step join the whole sync stream first.  Same results
- * bit for bit.                                                            */
+ * work makes the next step join the whole sync stream first.  2 as 1, but
+ * kernel B(k) runs on the all-reduce's stream right behind AR(k) (no event
+ * between them; the sync stream joins once, after the last B).  Same
+ * results bit for bit in every mode.                                      */
 int cbx_set_pipeline_mode (cbx_context *ctx, int mode);
 /* Force the multi-GPU pipeline (kernel A + RCCL all-reduce + kernel B) even
  * at G = 1 (a one-rank communicator), so a single-GPU host exercises it.  */

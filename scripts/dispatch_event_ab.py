@@ -50,7 +50,7 @@ def main():
     res = {}
     for _ in range(rounds):
         for nb in (4, 8, 16):
-            for mode in (0, 1):
+            for mode in (0, 1, 2):
                 for de, g in gpus.items():
                     g.set_bucket_elements(-(-n // nb))
                     g.set_pipeline_mode(mode)

@@ -183,9 +183,11 @@ int main (void) {
 	CHECK (cbx_synchronise_staged (c, 0, 2, 0, 3));
 	CHECK (cbx_unlock_any (c));
 	CHECK (cbx_set_pipeline_mode (c, 1));  /* across steps */
-	EXPECT (cbx_set_pipeline_mode (c, 2) == CBX_ERR_INVALID);
-	for (int clock = 3; clock < 7; ++clock) {
+	EXPECT (cbx_set_pipeline_mode (c, 3) == CBX_ERR_INVALID);
+	EXPECT (cbx_set_pipeline_mode (c, -1) == CBX_ERR_INVALID);
+	for (int clock = 3; clock < 9; ++clock) {
 		if (clock == 5) CHECK (cbx_replica_set_copy (c, 1, 1));
+		if (clock == 6) CHECK (cbx_set_pipeline_mode (c, 2));  /* B behind its all-reduce */
 		CHECK (cbx_lock_any (c));
 		CHECK (cbx_synchronise (c, 0, clock, 0, 0));
 		CHECK (cbx_unlock_any (c));

@@ -39,6 +39,7 @@ CASES = [
     ("sma-copy-ssp", 50_001, 2, 0.9, 3, 0, {1: 3}, {0: 1}, 0, 7),
     ("sma-5-buckets", 300_007, 3, 0.9, 2, 65_536, {1: 0}, {}, 0, 7),
     ("sma-5-buckets-cross", 300_007, 2, 0.9, 5, 65_536, {2: 1}, {3: 0}, 0, 7),
+    ("sma-5-buckets-cross-bcomm", 300_007, 2, 0.9, 5, 65_536, {2: 1}, {3: 0}, 0, 7),
     ("sma-no-momentum", 20_011, 1, 0.0, 2, 4096, {}, {}, 0, 3),
     ("sma-staged", 100_003, 2, 0.9, 2, 0, {1: 2}, {}, 3, 7),
     ("ssgd", 40_009, 2, 0.9, 2, 0, {}, {}, 0, 1),
@@ -103,6 +104,8 @@ def _case(L, A, rank, world, uid, case):
             g("cbx_set_bucket_elements", ctypes.c_longlong(bucket))
         if name.endswith("-cross"):
             g("cbx_set_pipeline_mode", 1)  # kernels A of the next step overlap this step's tail
+        elif name.endswith("-cross-bcomm"):
+            g("cbx_set_pipeline_mode", 2)  # and kernels B run behind their all-reduce on its stream
         size = world * R
         assert g("cbx_num_replicas") == size and g("cbx_num_devices") == world
         mine = [i for i in range(size) if i % world == rank]
