@@ -256,9 +256,10 @@ def main():
     gpu.set_bucket_elements(bucket_elems)
     tuning = None
     pipeline_mode = 0
+    wait_stride = 1
     if split and args.bucket_mb == 0:
         # warm-up autotune of the bucket count on the live communicator (same choice on every rank)
-        bucket_elems, pipeline_mode, tuning = D.tune_buckets(gpu, n, world, step)
+        bucket_elems, pipeline_mode, wait_stride, tuning = D.tune_buckets(gpu, n, world, step)
 
     for _ in range(args.warmup):
         step()
@@ -303,6 +304,7 @@ def main():
             "buckets": (None if not split else int(min(tuning, key=lambda k: tuning[k]).split("/")[0]) if tuning
                         else -(-n // min(bucket_elems, n)) if bucket_elems else "library default (8)"),
             "pipeline_mode": None if not split else pipeline_mode,
+            "cross_wait_stride": None if not split else wait_stride,
             "bucket_tuning_ms_per_step": tuning,
             "kernel_config": dict(block=args.block, blocks_per_cu=args.blocks_per_cu, policy=args.policy,
                                   unroll=args.unroll, waves_per_cu=args.waves_per_cu, bucket_mb=args.bucket_mb),

@@ -297,6 +297,7 @@ struct cbx_context {
   int pipeline_mode = 0;  // 0 bucketed within a step, 1 across steps, 2 as 1 with B on comm_stream (G > 1 split path)
   // Bucket events as kernel stop events (default); CBX_SEPARATE_EVENT_RECORDS=1
   // at context creation restores separate hipEventRecord markers, for A/B runs.
+  int cross_wait_stride = 1;  // modes 1/2: buckets per cross-step wait
   bool dispatch_events = !(getenv("CBX_SEPARATE_EVENT_RECORDS") && getenv("CBX_SEPARATE_EVENT_RECORDS")[0] == '1');
   // Bumped by every C-ABI call that may enqueue work on a sync stream other
   // than the barrier path itself: a cross-step pipelined step then joins the
@@ -694,6 +695,11 @@ int sma_step(cbx_context *c, int first) {
     // ~10 us gap on the sync stream per bucket: -2 to -8 % per step
     // (scripts/dispatch_event_ab.py, profiles/r01/dispatch_event_ab.json).
     const bool dispatch_events = c->dispatch_events;
+    // Modes 1/2: A(k) waits for B(k + stride - 1) of the last step once per
+    // `stride` buckets (it implies B(k..): same stream).  Each satisfied
+    // cross-queue wait still costs the waiting queue ~10 us; fewer waits
+    // trade that for less cross-step overlap (cbx_set_cross_wait_stride).
+    const int64_t wait_stride = std::max(1, c->cross_wait_stride);
     const unsigned long long foreign = c->foreign_ops.load(std::memory_order_acquire);
     std::vector<char> join(c->devs.size(), 1);
     for (size_t k = 0; k < c->devs.size(); ++k) {
@@ -774,7 +780,8 @@ int sma_step(cbx_context *c, int first) {
         if (b == 0) t.start = ring_event(c, d, EV_START);
         if (!pipelined) t.stop = ring_event(c, d, EV_A);
         hipStream_t st = cross ? d.a_stream : d.stream;
-        if (cross && !join[k]) HIP_TRY(hipStreamWaitEvent(st, d.bucket_b[b], 0));  // B(b) of the last step
+        if (cross && !join[k] && b % wait_stride == 0)  // B(b .. b+stride-1) of the last step
+          HIP_TRY(hipStreamWaitEvent(st, d.bucket_b[std::min<int64_t>(b + wait_stride - 1, nb - 1)], 0));
         const bool in_dispatch = pipelined && dispatch_events;
         if (in_dispatch) t.stop = d.bucket_acc[b];
         HIP_TRY(cbx::launch_sma_accumulate(offset_args(args[k], start, len), b == 0, cfg, st, t));
@@ -2528,6 +2535,13 @@ int cbx_set_pipeline_mode(cbx_context *c, int mode) {
   TRY(check_ctx(c));
   if (mode < 0 || mode > 2) return fail(CBX_ERR_INVALID, "pipeline mode must be 0, 1 or 2");
   c->pipeline_mode = mode;
+  return CBX_OK;
+}
+
+int cbx_set_cross_wait_stride(cbx_context *c, int stride) {
+  TRY(check_ctx(c));
+  if (stride < 1 || stride > 4096) return fail(CBX_ERR_INVALID, "cross-step wait stride must be 1..4096");
+  c->cross_wait_stride = stride;
   return CBX_OK;
 }
 

@@ -57,35 +57,43 @@ def max_over_ranks(value: float, world: int) -> float:
 
 
 def tune_buckets(gpu, n: int, world: int, step: Callable[[], None], candidates=(1, 2, 4, 8, 16),
-                 steps: int = 10, warmup: int = 2, modes=(0, 1, 2), passes: int = 2):
+                 steps: int = 10, warmup: int = 2, modes=(0, 1, 2), strides=(1, 2, 4), passes: int = 2):
     """Pick the bucket count of the G > 1 pipeline (kernel A / RCCL
     all-reduce / kernel B per bucket) by timing each candidate on the live
     communicator, the way a runtime tunes itself in its warm-up.
 
     More buckets hide more of the all-reduce behind kernel A, but each bucket
-    costs fixed time (a cross-stream event, a shorter launch's ramp and drain:
-    ~7 us per bucket on one MI355X with the bucket events on the kernel dispatches,
-    profiles/r01/bench_force_split_tuned.json),
-    so the best count depends on how long the all-reduce is, i.e. on G and the
-    xGMI links.  Every rank times every candidate, the times are max-reduced
-    over ranks, and all ranks take the same argmin, so the RCCL call sequence
-    stays identical on every rank.  ``step()`` runs one barrier step.
-    With more than one bucket each count is also timed in both pipeline
-    modes (``gpu.set_pipeline_mode``: 0 within a step, 1 across steps, 2 across
-    steps with kernel B on the all-reduce's stream).
+    costs fixed time (cross-queue waits, a shorter launch's ramp and drain:
+    ~7 us per bucket on one MI355X with the bucket events on the kernel
+    dispatches, profiles/r01/bench_force_split_tuned.json), so the best count
+    depends on how long the all-reduce is, i.e. on G and the xGMI links.
+    Every rank times every candidate, the times are max-reduced over ranks,
+    and all ranks take the same argmin, so the RCCL call sequence stays
+    identical on every rank.  ``step()`` runs one barrier step.
+    With more than one bucket each count is also timed in every pipeline
+    mode (``gpu.set_pipeline_mode``: 0 within a step, 1 across steps, 2 across
+    steps with kernel B on the all-reduce's stream), and modes 1/2 with each
+    cross-step wait stride below the bucket count (``gpu.set_cross_wait_stride``).
     The candidates are timed in ``passes`` interleaved passes and each keeps
     its best pass, so one noisy sample (a few percent on one GPU) does not
-    decide.  Returns (bucket_elements, mode, {"<buckets>/<mode>": ms_per_step}).
+    decide.  Returns (bucket_elements, mode, stride, {key: ms_per_step}) with
+    keys "<buckets>/<mode>" for stride 1 and "<buckets>/<mode>/s<stride>".
     """
     import time
+
+    def combos(nb):
+        if nb <= 1:
+            return [(0, 1)]
+        return [(m, s) for m in modes for s in ((1,) if m == 0 else strides) if s == 1 or s < nb]
 
     results = {}
     for _ in range(max(1, passes)):
         for nb in candidates:
             elems = (1 << 62) if nb <= 1 else max(1, -(-n // nb))
-            for mode in (modes if nb > 1 else (0,)):
+            for mode, stride in combos(nb):
                 gpu.set_bucket_elements(elems)
                 gpu.set_pipeline_mode(mode)
+                gpu.set_cross_wait_stride(stride)
                 for _ in range(warmup):
                     step()
                 gpu.wait()
@@ -95,13 +103,19 @@ def tune_buckets(gpu, n: int, world: int, step: Callable[[], None], candidates=(
                     step()
                 gpu.wait()
                 ms = max_over_ranks((time.perf_counter() - t0) * 1e3 / steps, world)
-                results[(nb, mode)] = min(ms, results.get((nb, mode), ms))
+                key = (nb, mode, stride)
+                results[key] = min(ms, results.get(key, ms))
     best = min(results, key=lambda k: (results[k], k))
-    nb, mode = best
+    nb, mode, stride = best
     elems = (1 << 62) if nb <= 1 else max(1, -(-n // nb))
     gpu.set_bucket_elements(elems)
     gpu.set_pipeline_mode(mode)
-    return elems, mode, {f"{k[0]}/{k[1]}": v for k, v in results.items()}
+    gpu.set_cross_wait_stride(stride)
+    return elems, mode, stride, {tuning_key(*k): v for k, v in results.items()}
+
+
+def tuning_key(nb: int, mode: int, stride: int = 1) -> str:
+    return f"{nb}/{mode}" if stride == 1 else f"{nb}/{mode}/s{stride}"
 
 
 def local_replicas(size: int, world: int, rank: int):

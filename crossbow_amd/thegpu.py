@@ -390,6 +390,10 @@ class TheGPU:
         """0: buckets overlap within a step; 1: also across steps; 2: as 1, kernel B on the all-reduce stream."""
         check(self._L.cbx_set_pipeline_mode(self._ctx, mode))
 
+    def set_cross_wait_stride(self, stride: int) -> None:
+        """Modes 1/2: buckets per cross-step wait of kernel A on last step's kernel B."""
+        check(self._L.cbx_set_cross_wait_stride(self._ctx, stride))
+
     def set_bucket_elements(self, elements: int) -> None:
         check(self._L.cbx_set_bucket_elements(self._ctx, elements))
 

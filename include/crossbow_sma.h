@@ -347,6 +347,11 @@ int cbx_set_bucket_elements (cbx_context *ctx, long long bucket_elements);
  * between them; the sync stream joins once, after the last B).  Same
  * results bit for bit in every mode.                                      */
 int cbx_set_pipeline_mode (cbx_context *ctx, int mode);
+/* Modes 1 and 2: kernel A(k) waits for kernel B of the previous step once
+ * per `stride` buckets, on B(k + stride - 1), which implies the earlier
+ * ones.  1 (default) waits per bucket; larger strides pay fewer
+ * cross-queue waits for less overlap between steps.  1..4096.            */
+int cbx_set_cross_wait_stride (cbx_context *ctx, int stride);
 /* Force the multi-GPU pipeline (kernel A + RCCL all-reduce + kernel B) even
  * at G = 1 (a one-rank communicator), so a single-GPU host exercises it.  */
 int cbx_set_force_split (cbx_context *ctx, int force);

@@ -185,9 +185,11 @@ int main (void) {
 	CHECK (cbx_set_pipeline_mode (c, 1));  /* across steps */
 	EXPECT (cbx_set_pipeline_mode (c, 3) == CBX_ERR_INVALID);
 	EXPECT (cbx_set_pipeline_mode (c, -1) == CBX_ERR_INVALID);
+	EXPECT (cbx_set_cross_wait_stride (c, 0) == CBX_ERR_INVALID);
 	for (int clock = 3; clock < 9; ++clock) {
 		if (clock == 5) CHECK (cbx_replica_set_copy (c, 1, 1));
 		if (clock == 6) CHECK (cbx_set_pipeline_mode (c, 2));  /* B behind its all-reduce */
+		if (clock == 7) CHECK (cbx_set_cross_wait_stride (c, 3));
 		CHECK (cbx_lock_any (c));
 		CHECK (cbx_synchronise (c, 0, clock, 0, 0));
 		CHECK (cbx_unlock_any (c));

@@ -106,6 +106,7 @@ def _case(L, A, rank, world, uid, case):
             g("cbx_set_pipeline_mode", 1)  # kernels A of the next step overlap this step's tail
         elif name.endswith("-cross-bcomm"):
             g("cbx_set_pipeline_mode", 2)  # and kernels B run behind their all-reduce on its stream
+            g("cbx_set_cross_wait_stride", 2)  # one cross-step wait per two buckets
         size = world * R
         assert g("cbx_num_replicas") == size and g("cbx_num_devices") == world
         mine = [i for i in range(size) if i % world == rank]
