@@ -347,13 +347,18 @@ def _rank_main(rank, world, uids, fake_dir, q):
 
 
 def _cases(world):
-    # four ranks: the SMA cases (placement i % 4, Phase D from rank 3, buckets)
-    return CASES if world == 2 else [c for c in CASES if c[0] in ("sma", "sma-copy-ssp", "sma-5-buckets",
-                                                                  "sma-5-buckets-cross")]
+    # four ranks: the SMA cases (placement i % 4, Phase D from rank 3, buckets, both cross-step modes);
+    # eight ranks (the driver's full-node G): the plain step and the mode-2 pipeline
+    if world == 2:
+        return CASES
+    if world == 4:
+        return [c for c in CASES if c[0] in ("sma", "sma-copy-ssp", "sma-5-buckets", "sma-5-buckets-cross",
+                                             "sma-5-buckets-cross-bcomm")]
+    return [c for c in CASES if c[0] in ("sma-copy-ssp", "sma-5-buckets-cross-bcomm")]
 
 
 @pytest.mark.skipif(not os.path.exists(VARIANT), reason="run scripts/build_fake_rccl.sh first")
-@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("world", [2, 4, 8])
 def test_ranks_on_one_gpu_bitexact_vs_oracle(world):
     import multiprocessing as mp
     uids = [os.urandom(16) + bytes(112) for _ in range(len(CASES) + 2)]
