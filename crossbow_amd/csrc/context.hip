@@ -1064,29 +1064,72 @@ int ssgd_step(cbx_context *c, int first) {
     a.ratio = ratio;
     a.momentum = mom ? c->model.conf.momentum : 0.0f;
   }
+  // Buckets as in the SMA split pipeline (cbx_set_bucket_elements; 8 by
+  // default at G > 1).  With more than one, the all-reduce of bucket k+1
+  // runs on comm_stream beside the apply kernel of bucket k:
+  //   stream      : [entry] [wait red(0)] K(0) [wait red(1)] K(1) ...
+  //   comm_stream : [wait entry] AR(0) AR(1) ...
+  int64_t b4 = c->n4, nb = 1;
+  if (split) {
+    const int64_t pad = cbx::kPadFloat4;
+    if (c->bucket_elems > 0) b4 = ((c->bucket_elems / 4 + pad - 1) / pad) * pad;
+    else if (c->G > 1) b4 = ((c->n4 / kDefaultBuckets + pad - 1) / pad) * pad;
+    if (b4 <= 0 || b4 > c->n4) b4 = c->n4;
+    nb = (c->n4 + b4 - 1) / b4;
+  }
+  const bool pipelined = nb > 1;
   if (split) {
     for (Device &d : c->devs) {
       HIP_TRY(hipSetDevice(d.hip_id));
       TRY(mark(c, d, EV_START));
+      if (!pipelined) continue;
+      while ((int64_t)d.bucket_red.size() < nb) {
+        hipEvent_t ea, er, eb;
+        HIP_TRY(hipEventCreate(&ea));
+        HIP_TRY(hipEventCreateWithFlags(&er, hipEventDisableTiming));
+        HIP_TRY(hipEventCreate(&eb));
+        d.bucket_acc.push_back(ea);
+        d.bucket_red.push_back(er);
+        d.bucket_b.push_back(eb);
+      }
+      // everything the task steps accumulated into acc, in sync-stream order
+      HIP_TRY(hipEventRecord(d.bucket_acc[0], d.stream));
+      HIP_TRY(hipStreamWaitEvent(d.comm_stream, d.bucket_acc[0], 0));
     }
-    NCCL_TRY(ncclGroupStart());
-    for (Device &d : c->devs) {
-      HIP_TRY(hipSetDevice(d.hip_id));
-      NCCL_TRY(ncclAllReduce(base_dev(c, d, CBX_BUF_GRADIENT), base_dev(c, d, CBX_BUF_DIFF), (size_t)c->n4 * 4,
-                             ncclFloat, ncclSum, d.comm, d.stream));
-    }
-    NCCL_TRY(ncclGroupEnd());
   }
-  for (size_t k = 0; k < c->devs.size(); ++k) {
-    Device &d = c->devs[k];
-    HIP_TRY(hipSetDevice(d.hip_id));
-    cbx::LaunchConfig cfg = c->ssgd_apply_cfg;
-    cfg.num_cus = d.num_cus;
-    cbx::Timing t;
-    if (!split) t.start = ring_event(c, d, EV_START);
-    t.stop = step_stop_event(c, d, split ? EV_B : EV_A);
-    HIP_TRY(cbx::launch_ssgd_apply(args[k], cfg, d.stream, t));
-    ring_advance(c, d, split ? 2 : 0);
+  for (int64_t b = 0; b < nb; ++b) {
+    const int64_t start = b * b4, len = std::min(b4, c->n4 - start);
+    if (split) {
+      NCCL_TRY(ncclGroupStart());
+      for (Device &d : c->devs) {
+        HIP_TRY(hipSetDevice(d.hip_id));
+        NCCL_TRY(ncclAllReduce(base_dev(c, d, CBX_BUF_GRADIENT) + start * 4, base_dev(c, d, CBX_BUF_DIFF) + start * 4,
+                               (size_t)len * 4, ncclFloat, ncclSum, d.comm, pipelined ? d.comm_stream : d.stream));
+      }
+      NCCL_TRY(ncclGroupEnd());
+    }
+    for (size_t k = 0; k < c->devs.size(); ++k) {
+      Device &d = c->devs[k];
+      HIP_TRY(hipSetDevice(d.hip_id));
+      if (pipelined) {
+        HIP_TRY(hipEventRecord(d.bucket_red[b], d.comm_stream));
+        HIP_TRY(hipStreamWaitEvent(d.stream, d.bucket_red[b], 0));
+      }
+      cbx::LaunchConfig cfg = c->ssgd_apply_cfg;
+      cfg.num_cus = d.num_cus;
+      cbx::Timing t;
+      if (!split) t.start = ring_event(c, d, EV_START);
+      if (b == nb - 1) t.stop = step_stop_event(c, d, split ? EV_B : EV_A);
+      cbx::SsgdArgs a = args[k];
+      for (int r = 0; r < a.nrep; ++r) a.w[r] += start;
+      a.z += start;
+      if (a.last) a.last += start;
+      a.acc += start;
+      a.D += start;
+      a.n4 = len;
+      HIP_TRY(cbx::launch_ssgd_apply(a, cfg, d.stream, t));
+      if (b == nb - 1) ring_advance(c, d, split ? 2 : 0);
+    }
   }
   c->last_step_split = split;
   return finish_step(c);

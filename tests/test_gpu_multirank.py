@@ -43,6 +43,7 @@ CASES = [
     ("sma-no-momentum", 20_011, 1, 0.0, 2, 4096, {}, {}, 0, 3),
     ("sma-staged", 100_003, 2, 0.9, 2, 0, {1: 2}, {}, 3, 7),
     ("ssgd", 40_009, 2, 0.9, 2, 0, {}, {}, 0, 1),
+    ("ssgd-buckets", 40_009, 2, 0.9, 2, 4096, {}, {}, 0, 1),
 ]
 
 
@@ -354,7 +355,7 @@ def _cases(world):
     if world == 4:
         return [c for c in CASES if c[0] in ("sma", "sma-copy-ssp", "sma-5-buckets", "sma-5-buckets-cross",
                                              "sma-5-buckets-cross-bcomm")]
-    return [c for c in CASES if c[0] in ("sma-copy-ssp", "sma-5-buckets-cross-bcomm")]
+    return [c for c in CASES if c[0] in ("sma-copy-ssp", "sma-5-buckets-cross-bcomm", "ssgd-buckets")]
 
 
 @pytest.mark.skipif(not os.path.exists(VARIANT), reason="run scripts/build_fake_rccl.sh first")

@@ -162,7 +162,7 @@ def test_nesterov_is_unsupported():
 
 
 @pytest.mark.parametrize("momentum", [0.0, 0.9])
-@pytest.mark.parametrize("split", [False, True])
+@pytest.mark.parametrize("split", [False, True, 4096, 16_384])
 @pytest.mark.parametrize("aux", AUX_CONFIGS)
 def test_ssgd_clock_loop_bitexact(momentum, split, aux):
     # Synchronous SGD (update model WORKER): task steps add
@@ -187,6 +187,8 @@ def test_ssgd_clock_loop_bitexact(momentum, split, aux):
             g.set_barrier_kernel_config(*aux)
         if split:
             g.set_force_split(True)
+            if split is not True:  # bucketed barrier: all-reduce of bucket k+1 beside the apply of bucket k
+                g.set_bucket_elements(split)
         st = O.make_state(n, 1, R, 0.1, momentum)
         st.locked[2] = 0  # hold replica 2 (SSP): not copied at the barrier
         upload(g, st)
