@@ -295,9 +295,9 @@ struct cbx_context {
   bool force_split = false;
   bool last_step_split = false;
   int pipeline_mode = 0;  // 0 bucketed within a step, 1 across steps, 2 as 1 with B on comm_stream (G > 1 split path)
+  int cross_wait_stride = 1;  // modes 1/2: buckets per cross-step wait
   // Bucket events as kernel stop events (default); CBX_SEPARATE_EVENT_RECORDS=1
   // at context creation restores separate hipEventRecord markers, for A/B runs.
-  int cross_wait_stride = 1;  // modes 1/2: buckets per cross-step wait
   bool dispatch_events = !(getenv("CBX_SEPARATE_EVENT_RECORDS") && getenv("CBX_SEPARATE_EVENT_RECORDS")[0] == '1');
   // Bumped by every C-ABI call that may enqueue work on a sync stream other
   // than the barrier path itself: a cross-step pipelined step then joins the
