@@ -130,6 +130,7 @@ SIGNATURES = {
     "cbx_set_apply_kernel_config": (_I, [_P, _I, _I, _I]),
     "cbx_set_pipeline_mode": (_I, [_P, _I]),
     "cbx_set_cross_wait_stride": (_I, [_P, _I]),
+    "cbx_set_allreduce_group": (_I, [_P, _I]),
     "cbx_set_bucket_elements": (_I, [_P, _c.c_longlong]),
     "cbx_set_force_split": (_I, [_P, _I]),
     "cbx_fill_synthetic": (_I, [_P, _c.c_ulonglong]),

@@ -296,6 +296,7 @@ struct cbx_context {
   bool last_step_split = false;
   int pipeline_mode = 0;  // 0 bucketed within a step, 1 across steps, 2 as 1 with B on comm_stream (G > 1 split path)
   int cross_wait_stride = 1;  // modes 1/2: buckets per cross-step wait
+  int allreduce_group = 1;     // pipelined split path: buckets per comm-stream wait
   // Bucket events as kernel stop events (default); CBX_SEPARATE_EVENT_RECORDS=1
   // at context creation restores separate hipEventRecord markers, for A/B runs.
   bool dispatch_events = !(getenv("CBX_SEPARATE_EVENT_RECORDS") && getenv("CBX_SEPARATE_EVENT_RECORDS")[0] == '1');
@@ -732,16 +733,19 @@ int sma_step(cbx_context *c, int first) {
         }
       }
     }
-    auto allreduce = [&](int64_t b, bool on_comm) -> int {
+    // `wait_acc`: the comm stream first waits for kernel A of that bucket
+    // (-1: no wait; an earlier all-reduce of the same group already waited
+    // on a later bucket, which implies this one: A runs in order).
+    auto allreduce = [&](int64_t b, bool on_comm, int64_t wait_acc) -> int {
       const int64_t start = b * b4;
       const int64_t len = std::min(b4, c->n4 - start);
       // common.c:14-54: grouped all-reduce, fp32 sum.  Bucket 0 also carries
       // the control block that sits right in front of the data.
-      if (on_comm) {
+      if (on_comm && wait_acc >= 0) {
         for (size_t k = 0; k < c->devs.size(); ++k) {
           Device &d = c->devs[k];
           HIP_TRY(hipSetDevice(d.hip_id));
-          HIP_TRY(hipStreamWaitEvent(d.comm_stream, d.bucket_acc[b], 0));
+          HIP_TRY(hipStreamWaitEvent(d.comm_stream, d.bucket_acc[wait_acc], 0));
         }
       }
       NCCL_TRY(ncclGroupStart());
@@ -820,27 +824,33 @@ int sma_step(cbx_context *c, int first) {
     };
     if (!pipelined) {
       TRY(accumulate(0));
-      TRY(allreduce(0, false));
+      TRY(allreduce(0, false, -1));
       for (Device &d : c->devs) {
         HIP_TRY(hipSetDevice(d.hip_id));
         TRY(mark(c, d, EV_AR));
       }
       TRY(apply(0));
-    } else if (cross) {
-      for (int64_t b = 0; b < nb; ++b) {
-        TRY(accumulate(b));
-        TRY(allreduce(b, true));
-        TRY(apply(b));
-      }
     } else {
+      // All-reduces go out in groups of `ar_group` buckets behind a single
+      // comm-stream wait on the group's last kernel A (cbx_set_allreduce_group).
+      // Every event is recorded before the wait on it is enqueued: a group's
+      // all-reduces follow its last A, and B(j) follows AR(j).  Mode 0 applies
+      // the previous group while this one is on the link; modes 1/2 apply a
+      // group right behind its all-reduces.  ar_group 1 is the per-bucket order
+      // A(b) AR(b) B(b-1) (mode 0) / A(b) AR(b) B(b) (modes 1/2).
+      const int64_t ar_group = std::max(1, c->allreduce_group);
+      int64_t applied = 0;
       for (int64_t b = 0; b < nb; ++b) {
         TRY(accumulate(b));
-        TRY(allreduce(b, true));
-        if (b > 0) TRY(apply(b - 1));
+        if ((b + 1) % ar_group != 0 && b != nb - 1) continue;
+        const int64_t g0 = b - b % ar_group;
+        for (int64_t j = g0; j <= b; ++j) TRY(allreduce(j, true, j == g0 ? b : -1));
+        const int64_t upto = cross ? b + 1 : g0;
+        for (; applied < upto; ++applied) TRY(apply(applied));
       }
       // The wait inside apply(nb-1) also joins every earlier all-reduce
       // (comm_stream is in order) back into the sync stream.
-      TRY(apply(nb - 1));
+      for (; applied < nb; ++applied) TRY(apply(applied));
     }
     for (Device &d : c->devs) {
       ring_advance(c, d, pipelined ? 2 : 1);
@@ -2585,6 +2595,13 @@ int cbx_set_cross_wait_stride(cbx_context *c, int stride) {
   TRY(check_ctx(c));
   if (stride < 1 || stride > 4096) return fail(CBX_ERR_INVALID, "cross-step wait stride must be 1..4096");
   c->cross_wait_stride = stride;
+  return CBX_OK;
+}
+
+int cbx_set_allreduce_group(cbx_context *c, int group) {
+  TRY(check_ctx(c));
+  if (group < 1 || group > 4096) return fail(CBX_ERR_INVALID, "all-reduce group must be 1..4096");
+  c->allreduce_group = group;
   return CBX_OK;
 }
 

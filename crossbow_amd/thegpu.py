@@ -394,6 +394,10 @@ class TheGPU:
         """Modes 1/2: buckets per cross-step wait of kernel A on last step's kernel B."""
         check(self._L.cbx_set_cross_wait_stride(self._ctx, stride))
 
+    def set_allreduce_group(self, group: int) -> None:
+        """Split path: buckets all-reduced behind one wait on the group's last kernel A."""
+        check(self._L.cbx_set_allreduce_group(self._ctx, group))
+
     def set_bucket_elements(self, elements: int) -> None:
         check(self._L.cbx_set_bucket_elements(self._ctx, elements))
 

@@ -352,6 +352,15 @@ int cbx_set_pipeline_mode (cbx_context *ctx, int mode);
  * ones.  1 (default) waits per bucket; larger strides pay fewer
  * cross-queue waits for less overlap between steps.  1..4096.            */
 int cbx_set_cross_wait_stride (cbx_context *ctx, int stride);
+/* Split path with buckets (every pipeline mode): all-reduce `group`
+ * buckets behind one wait of the all-reduce stream on kernel A of the
+ * group's last bucket, instead of one wait per bucket.  1 (default) is the
+ * per-bucket order.  Larger groups pay fewer cross-queue waits (~10 us of
+ * queue latency each) and start each group's all-reduces later.  Same
+ * results bit for bit.  1..4096.  No reference counterpart: the bucket
+ * pipeline itself is this library's (common.c:14-54 all-reduces one flat
+ * buffer).                                                                */
+int cbx_set_allreduce_group (cbx_context *ctx, int group);
 /* Force the multi-GPU pipeline (kernel A + RCCL all-reduce + kernel B) even
  * at G = 1 (a one-rank communicator), so a single-GPU host exercises it.  */
 int cbx_set_force_split (cbx_context *ctx, int force);

@@ -108,6 +108,9 @@ def _case(L, A, rank, world, uid, case):
         elif name.endswith("-cross-bcomm"):
             g("cbx_set_pipeline_mode", 2)  # and kernels B run behind their all-reduce on its stream
             g("cbx_set_cross_wait_stride", 2)  # one cross-step wait per two buckets
+            g("cbx_set_allreduce_group", 3)  # all-reduces 0-2 behind one wait, then 3-4
+        elif name == "sma-5-buckets":
+            g("cbx_set_allreduce_group", 2)  # mode 0: all-reduces in pairs, B of the previous pair beside them
         size = world * R
         assert g("cbx_num_replicas") == size and g("cbx_num_devices") == world
         mine = [i for i in range(size) if i % world == rank]

@@ -721,8 +721,8 @@ def test_concurrent_task_threads_and_barrier(pipeline):
 
 @pytest.mark.parametrize("momentum", [0.0, 0.9])
 @pytest.mark.parametrize("bucket", [65_536, 4096])
-@pytest.mark.parametrize("xmode,stride", [(1, 1), (2, 1), (1, 3), (2, 2)])
-def test_cross_step_pipeline(momentum, bucket, xmode, stride):
+@pytest.mark.parametrize("xmode,stride,group", [(1, 1, 1), (2, 1, 1), (1, 3, 1), (2, 2, 1), (1, 1, 2), (2, 3, 4)])
+def test_cross_step_pipeline(momentum, bucket, xmode, stride, group):
     # cbx_set_pipeline_mode(1): kernels A on their own stream, each waiting
     # only for B of the same bucket in the previous step.  Eight steps with
     # Phase D requests, SSP holds, a host write between two steps (which
@@ -737,6 +737,7 @@ def test_cross_step_pipeline(momentum, bucket, xmode, stride):
         g.set_bucket_elements(bucket)
         g.set_pipeline_mode(xmode)
         g.set_cross_wait_stride(stride)
+        g.set_allreduce_group(group)  # all-reduces per comm-stream wait; mode 0 steps use it too
         upload(g, st)
         want = st.clone()
         plan = [{}, {"copy": 1}, {"hold": 2}, {}, {"write": 0}, {"mode": 0}, {"mode": xmode, "copy": 2, "hold": 0},
@@ -808,6 +809,7 @@ def test_cross_step_pipeline_randomised_long_run():
             elif u < 0.30:
                 g.set_pipeline_mode(rng.choice([0, 1, 2]))
                 g.set_cross_wait_stride(rng.choice([1, 2, 3, 8]))
+                g.set_allreduce_group(rng.choice([1, 1, 2, 5]))
             g.lockAny()
             g.synchronise(0, step + 1, 0, False)
             g.unlockAny()
