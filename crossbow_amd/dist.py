@@ -57,7 +57,8 @@ def max_over_ranks(value: float, world: int) -> float:
 
 
 def tune_buckets(gpu, n: int, world: int, step: Callable[[], None], candidates=(1, 2, 4, 8, 16),
-                 steps: int = 10, warmup: int = 2, modes=(0, 1, 2), strides=(1, 2, 4), passes: int = 2):
+                 steps: int = 10, warmup: int = 2, modes=(0, 1, 2), strides=(1, 2, 4), passes: int = 2,
+                 group_candidates=(2, 4)):
     """Pick the bucket count of the G > 1 pipeline (kernel A / RCCL
     all-reduce / kernel B per bucket) by timing each candidate on the live
     communicator, the way a runtime tunes itself in its warm-up.
@@ -111,7 +112,31 @@ def tune_buckets(gpu, n: int, world: int, step: Callable[[], None], candidates=(
     gpu.set_bucket_elements(elems)
     gpu.set_pipeline_mode(mode)
     gpu.set_cross_wait_stride(stride)
-    return elems, mode, stride, {tuning_key(*k): v for k, v in results.items()}
+    out = {tuning_key(*k): v for k, v in results.items()}
+    # Then the all-reduce grouping of the winner (gpu.set_allreduce_group):
+    # fewer comm-stream waits, later all-reduce starts.  On one GPU groups of
+    # 2-4 cut 8-16-bucket mode-0 steps by 4-9 % (profiles/r01/allreduce_group_ab.json);
+    # over xGMI the later start may cost more than the waits save, so it is timed.
+    groups = [grp for grp in group_candidates if 1 < grp < nb]
+    if groups:
+        timed = {1: results[best]}
+        for _ in range(max(1, passes)):
+            for grp in groups:
+                gpu.set_allreduce_group(grp)
+                for _ in range(warmup):
+                    step()
+                gpu.wait()
+                barrier(world)
+                t0 = time.perf_counter()
+                for _ in range(steps):
+                    step()
+                gpu.wait()
+                ms = max_over_ranks((time.perf_counter() - t0) * 1e3 / steps, world)
+                timed[grp] = min(ms, timed.get(grp, ms))
+        for grp in groups:
+            out[tuning_key(nb, mode, stride) + f"/g{grp}"] = timed[grp]
+        gpu.set_allreduce_group(min(timed, key=lambda g: (timed[g], g)))
+    return elems, mode, stride, out
 
 
 def tuning_key(nb: int, mode: int, stride: int = 1) -> str:
