@@ -199,6 +199,10 @@ enum TimingEv { EV_START = 0, EV_A, EV_AR, EV_B, EV_H2D0, EV_H2D1, EV_D2H0, EV_D
 struct Device {
   int hip_id = 0;
   int g = 0;  // global device index
+  // The device number in checkpoint file names, `model->dev` in the
+  // reference (modelmanager.c:285,324,337): the selected HIP device id, or
+  // the rank in the one-process-per-GPU form.
+  int file_id = 0;
   hipStream_t stream = nullptr;       // model synchronisation stream (kernels)
   hipStream_t comm_stream = nullptr;  // RCCL all-reduce of the bucketed pipeline (G > 1)
   // Pipelined host-staged step (cbx_synchronise_staged): pinned H2D and D2H
@@ -265,9 +269,15 @@ struct cbx_context {
   ModelDef model;
   bool manager = false;
   int R = 0;           // replicas per device
-  int size = 0;        // R * G
+  // R * G.  Task threads read it (the theta queue) while the barrier thread
+  // may add or delete replicas (autotune), hence atomic.
+  std::atomic<int> size{0};
   int sync_type = CBX_SYNC_BSP;
   std::vector<Replica *> replicas;  // global id -> replica (all ids; remote ones have local = -1)
+  // Replicas removed by cbx_del_model.  A task thread may still be spinning
+  // on one's clock or blocked on its lock (cbx_get_next_or_wait), so the
+  // objects live until cbx_free instead of being deleted at once.
+  std::vector<Replica *> retired;
   std::vector<int> locked;
   std::unique_ptr<ThetaSlot[]> theta;  // kMaxReplicas * G slots, index = replica id
   std::atomic<unsigned> theta_iter{0};  // round-robin cursor (thetaqueue.c:95-104)
@@ -406,7 +416,7 @@ int check_manager(cbx_context *c) {
 
 int check_replica_q(cbx_context *c, int id, bool need_local) {
   TRY(check_manager_q(c));
-  if (id < 0 || id >= c->size) return fail(CBX_ERR_INVALID, "replica id %d out of range [0, %d)", id, c->size);
+  if (id < 0 || id >= c->size) return fail(CBX_ERR_INVALID, "replica id %d out of range [0, %d)", id, c->size.load());
   if (need_local && c->replicas[id]->local < 0)
     return fail(CBX_ERR_INVALID, "replica %d lives in another process (device %d)", id, c->replicas[id]->g);
   return CBX_OK;
@@ -414,7 +424,7 @@ int check_replica_q(cbx_context *c, int id, bool need_local) {
 
 int check_replica(cbx_context *c, int id, bool need_local) {
   TRY(check_manager(c));
-  if (id < 0 || id >= c->size) return fail(CBX_ERR_INVALID, "replica id %d out of range [0, %d)", id, c->size);
+  if (id < 0 || id >= c->size) return fail(CBX_ERR_INVALID, "replica id %d out of range [0, %d)", id, c->size.load());
   if (need_local && c->replicas[id]->local < 0)
     return fail(CBX_ERR_INVALID, "replica %d lives in another process (device %d)", id, c->replicas[id]->g);
   return CBX_OK;
@@ -459,6 +469,7 @@ int open_device(Device &d, int hip_id, int g) {
                 p.gcnArchName);
   d.hip_id = hip_id;
   d.g = g;
+  d.file_id = g;
   d.num_cus = p.multiProcessorCount;
   HIP_TRY(hipSetDevice(hip_id));
   // executioncontext.c:324: one non-blocking model-synchronisation stream.
@@ -1250,6 +1261,14 @@ int cbx_init(cbx_context **out, const int *devices, int ndevices) {
       return fail(rc, "%s", msg.c_str());
     }
   }
+  // Checkpoint files carry the selected device id, as the reference's do.  A
+  // selection that repeats a device (only the loopback test harness can run
+  // one; RCCL refuses it) keeps the position, so the names stay distinct.
+  bool repeated = false;
+  for (int a = 0; a < ndevices; ++a)
+    for (int b = 0; b < a; ++b) repeated = repeated || devices[a] == devices[b];
+  if (!repeated)
+    for (Device &d : c->devs) d.file_id = d.hip_id;
   if (ndevices > 1) {
     // executioncontext.c:185-201: ncclCommInitAll over the selected devices;
     // communicators are indexed by rank (selected-device order).
@@ -1314,12 +1333,13 @@ int cbx_free(cbx_context *c) {
     }
   }
   for (Device &d : c->devs) close_device(d);
-  for (Replica *r : c->replicas) {
-    if (!r) continue;
-    if (r->client) (void)hipEventDestroy(r->client);
-    pthread_mutex_destroy(&r->lock);
-    delete r;
-  }
+  for (std::vector<Replica *> *list : {&c->replicas, &c->retired})
+    for (Replica *r : *list) {
+      if (!r) continue;
+      if (r->client) (void)hipEventDestroy(r->client);
+      pthread_mutex_destroy(&r->lock);
+      delete r;
+    }
   delete c;
   return CBX_OK;
 }
@@ -1706,12 +1726,12 @@ int cbx_checkpoint_model(cbx_context *c, const char *dir) {
   for (Device &d : c->devs) {
     HIP_TRY(hipSetDevice(d.hip_id));
     // modelmanager.c:306-343, model.c:396-405
-    std::string prefix = fmt("%s/gpu-%02d-theModel", path.c_str(), d.g);
+    std::string prefix = fmt("%s/gpu-%02d-theModel", path.c_str(), d.file_id);
     TRY(store_buffer(base_dev(c, d, CBX_BUF_DATA), bytes, prefix + "-data.dat", tmp));
     if (c->has_last) TRY(store_buffer(base_dev(c, d, CBX_BUF_LAST), bytes, prefix + "-last.dat", tmp));
     for (int id : d.replicas) {
       Replica &r = *c->replicas[id];
-      std::string rp = fmt("%s/gpu-%02d-replica-%03d", path.c_str(), d.g, id);
+      std::string rp = fmt("%s/gpu-%02d-replica-%03d", path.c_str(), d.file_id, id);
       TRY(store_buffer(replica_dev(d, r, CBX_BUF_DATA), bytes, rp + "-data.dat", tmp));
       if (c->has_last) TRY(store_buffer(replica_dev(d, r, CBX_BUF_LAST), bytes, rp + "-last.dat", tmp));
     }
@@ -1729,12 +1749,12 @@ int cbx_override_model_data(cbx_context *c, const char *dir) {
   for (Device &d : c->devs) {
     HIP_TRY(hipSetDevice(d.hip_id));
     // modelmanager.c:267-304
-    std::string prefix = fmt("%s/gpu-%02d-theModel", dir, d.g);
+    std::string prefix = fmt("%s/gpu-%02d-theModel", dir, d.file_id);
     TRY(load_buffer(base_dev(c, d, CBX_BUF_DATA), bytes, prefix + "-data.dat", tmp));
     if (c->has_last) TRY(load_buffer(base_dev(c, d, CBX_BUF_LAST), bytes, prefix + "-last.dat", tmp));
     for (int id : d.replicas) {
       Replica &r = *c->replicas[id];
-      std::string rp = fmt("%s/gpu-%02d-replica-%03d", dir, d.g, id);
+      std::string rp = fmt("%s/gpu-%02d-replica-%03d", dir, d.file_id, id);
       TRY(load_buffer(replica_dev(d, r, CBX_BUF_DATA), bytes, rp + "-data.dat", tmp));
       if (c->has_last) TRY(load_buffer(replica_dev(d, r, CBX_BUF_LAST), bytes, rp + "-last.dat", tmp));
     }
@@ -1757,8 +1777,8 @@ static int batchnorm_stats_files(cbx_context *c, const std::string &dir, int op,
       return fail(CBX_ERR_INVALID, "device %d holds only one of operator %d's mean / variance", d.g, op);
     HIP_TRY(hipSetDevice(d.hip_id));
     HIP_TRY(hipDeviceSynchronize());
-    const std::string avg = fmt("%s/gpu-%02d-bn-avg-%03d.dat", dir.c_str(), d.g, op);
-    const std::string var = fmt("%s/gpu-%02d-bn-var-%03d.dat", dir.c_str(), d.g, op);
+    const std::string avg = fmt("%s/gpu-%02d-bn-avg-%03d.dat", dir.c_str(), d.file_id, op);
+    const std::string var = fmt("%s/gpu-%02d-bn-var-%03d.dat", dir.c_str(), d.file_id, op);
     if (store) {
       TRY(store_buffer(mean[k], bytes, avg, tmp));
       TRY(store_buffer(variance[k], bytes, var, tmp));
@@ -1883,18 +1903,21 @@ int cbx_del_model(cbx_context *c) {
         }
       }
       if (r->client) (void)hipEventDestroy(r->client);
+      r->client = nullptr;
       d.replicas.erase(std::remove(d.replicas.begin(), d.replicas.end(), id), d.replicas.end());
     }
-    if (c->locked[id]) pthread_mutex_unlock(&r->lock);
     // crossbowThetaQueueShrink (:537): the slot leaves the rotation.  A task
     // still holding its reservation gets -1 from cbx_upgrade_access.
     c->theta[id].state.store(kThetaSkip, std::memory_order_release);
-    pthread_mutex_destroy(&r->lock);
-    delete r;
+    if (c->locked[id]) pthread_mutex_unlock(&r->lock);
+    c->retired.push_back(r);  // freed by cbx_free: a task may still hold a reference
   }
+  // Shrink the count first: a task that reads it afterwards no longer picks
+  // the removed ids.  The arrays keep their capacity (reserved at creation),
+  // so they never move under a reader.
+  c->size = size_;
   c->replicas.resize(size_);
   c->locked.resize(size_);
-  c->size = size_;
   c->R -= 1;
   return CBX_OK;
 }

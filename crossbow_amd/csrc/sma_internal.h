@@ -224,7 +224,8 @@ struct BnSegment {
   uint32_t layer;  // count slot: scratch[layer] sums the counted devices
   float scale;     // 1 if this device's statistics count, else 0
 };
-// scratch[seg.off + i] = seg.scale * seg.ptr[i]; scratch[seg.layer] = seg.scale.
+// scratch[seg.off + i] = seg.ptr[i] if seg.scale != 0 else +0 (the buffer is
+// then not read); scratch[seg.layer] = seg.scale.
 hipError_t launch_bn_pack(const BnSegment *segs, int nseg, uint32_t maxlen, float *scratch, hipStream_t stream);
 // seg.ptr[i] = r * scratch[seg.off + i], r = 1/count (count > 1) else 1.
 hipError_t launch_bn_unpack(const BnSegment *segs, int nseg, uint32_t maxlen, const float *scratch,

@@ -444,7 +444,11 @@ __global__ __launch_bounds__(512) void ssgd_apply_kernel(const SsgdArgs a) {
 __global__ __launch_bounds__(256) void bn_pack_kernel(const BnSegment *segs, float *scratch) {
   const BnSegment sg = segs[blockIdx.y];
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < sg.len) scratch[sg.off + i] = sg.scale * sg.ptr[i];
+  // A device that does not count contributes an exact +0 without its
+  // statistics being read: the reference never touches a non-updated
+  // device's buffers (cudnnbatchnormparams.c:177-184), so a NaN or Inf left
+  // in them must not reach the average (0 * Inf would be NaN).
+  if (i < sg.len) scratch[sg.off + i] = sg.scale != 0.0f ? sg.ptr[i] : 0.0f;
   // A device's count for the layer, written once (by its mean segment's first thread).
   if (i == 0 && (blockIdx.y & 1u) == 0) scratch[sg.layer] = sg.scale;
 }

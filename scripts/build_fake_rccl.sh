@@ -15,3 +15,15 @@ mv "$N/libfakerccl.so.tmp" "$N/libfakerccl.so"
   -L "$N" -lfakerccl -Wl,-rpath,'$ORIGIN' -lrocprofiler-sdk-roctx -lpthread
 mv "$N/libcrossbow_sma_fakerccl.so.tmp" "$N/libcrossbow_sma_fakerccl.so"
 echo "built $N/libfakerccl.so $N/libcrossbow_sma_fakerccl.so"
+# The JNI shim and its driver over the loopback build: tests/test_gpu_jni.py
+# runs `jni_driver_fakerccl G`, one process over G copies of device 0.
+gcc -O2 -fPIC -shared -Wall -Wextra -std=c11 -I tests/jni_stub -I include \
+  -o "$N/libGPU_stubjni_fakerccl.so.tmp" crossbow_amd/csrc/jni/TheGPU_jni.c \
+  -L "$N" -l:libcrossbow_sma_fakerccl.so -Wl,-rpath,'$ORIGIN'
+mv "$N/libGPU_stubjni_fakerccl.so.tmp" "$N/libGPU_stubjni_fakerccl.so"
+gcc -O2 -Wall -Wextra -std=c11 -I tests/jni_stub -I include -I oracle \
+  -o "$N/jni_driver_fakerccl.tmp" "$N/jni_driver.c" oracle/sma_oracle.c \
+  -L "$N" -l:libGPU_stubjni_fakerccl.so -l:libcrossbow_sma_fakerccl.so \
+  -Wl,-rpath,'$ORIGIN' -lm -ldl -lpthread
+mv "$N/jni_driver_fakerccl.tmp" "$N/jni_driver_fakerccl"
+echo "built $N/libGPU_stubjni_fakerccl.so $N/jni_driver_fakerccl"

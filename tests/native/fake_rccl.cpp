@@ -1,22 +1,39 @@
 // fake_rccl.cpp -- TEST INFRASTRUCTURE: a loopback stand-in for the subset of
-// RCCL that libcrossbow_sma calls, so that several processes sharing ONE GPU
-// can run the library's multi-rank path (cbx_init_rank, G > 1) against the
-// oracle.  Real RCCL refuses two ranks on one device ("Duplicate GPU
-// detected"), and the GPU box has one GPU.
+// RCCL that libcrossbow_sma calls, so that the library's multi-GPU paths run
+// against the oracle on a box with ONE GPU.  Real RCCL refuses two ranks or
+// two communicators on one device ("Duplicate GPU detected").  Two forms:
 //
-// ncclAllReduce(float, sum) synchronises the stream it is given (so every
-// kernel the library ordered before it has finished), copies the send
-// buffer to a file under $FAKE_RCCL_DIR (default /tmp), waits for every
-// rank's file of the same sequence number, sums them IN RANK ORDER starting
-// from +0 (the oracle's order, oracle/sma_oracle.c; real RCCL's order is its
-// own, hence the rtol of the real G > 1 runs), writes the result to the
-// receive buffer with a blocking copy and returns.  Stream order is thereby
-// preserved: everything the library enqueues afterwards sees the result.
-// Every wait times out (ncclSystemError) instead of hanging.
+//  * one process per rank (cbx_init_rank, ncclCommInitRank): the send buffer
+//    of every rank goes through a file under $FAKE_RCCL_DIR (default /tmp);
+//  * one process, G communicators (cbx_init with G devices,
+//    ncclCommInitAll(ndev > 1), the reference's own form,
+//    executioncontext.c:185-201): the all-reduces issued between
+//    ncclGroupStart and ncclGroupEnd are matched by their order on each
+//    communicator, as in NCCL, and run at ncclGroupEnd.  An ungrouped call on
+//    such a communicator is an error (real NCCL would deadlock on it).
+//
+// Each all-reduce synchronises the stream it was given (so every kernel the
+// library ordered before it has finished), sums the ranks' send buffers on
+// the host, writes the result to every receive buffer with a blocking copy
+// and returns.  Stream order is thereby preserved: everything the library
+// enqueues afterwards sees the result.  Every file wait times out
+// (ncclSystemError) instead of hanging.
+//
+// Summation order ($FAKE_RCCL_ORDER, read when the communicator is created):
+//   "rank" (default): in rank order from +0, the oracle's order
+//                     (oracle/sma_oracle.c), so results are bit-exact;
+//   "ring":           as a ring all-reduce does it: the buffer is cut into
+//                     chunks, the reduction of chunk c starts at rank
+//                     (c + 1) mod G and walks the ring, and every rank then
+//                     receives the same reduced chunk (the all-gather).  For
+//                     G >= 3 this is NOT the oracle's order, so it exercises
+//                     the stated G > 1 tolerance and the
+//                     cross-rank identity of z (sma.c:168-174).
 //
 // Built by scripts/build_fake_rccl.sh as tests/native/libfakerccl.so; a
 // variant of the library linked against it (libcrossbow_sma_fakerccl.so) is
-// what tests/test_gpu_multirank.py loads.  Never linked into the product.
+// what tests/test_gpu_multirank.py and tests/test_gpu_multidevice.py load.
+// Never linked into the product.
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
@@ -33,15 +50,33 @@
 #include <thread>
 #include <vector>
 
+struct Clique;
+
 struct ncclComm {
   int nranks = 1;
   int rank = 0;
   int device = 0;
+  bool ring = false;
   std::string tag;  // hex of the unique id
   unsigned long long seq = 0;
+  Clique *clique = nullptr;  // single-process communicators (ncclCommInitAll, ndev > 1)
+};
+
+struct Clique {
+  std::vector<ncclComm *> comms;
+  int live = 0;
 };
 
 namespace {
+
+// Elements per ring chunk: small enough that a few-thousand-element test
+// buffer spans several chunks, so every start rank occurs.
+constexpr size_t kRingChunk = 1024;
+
+bool ring_order_from_env() {
+  const char *o = std::getenv("FAKE_RCCL_ORDER");
+  return o && std::strcmp(o, "ring") == 0;
+}
 
 std::string dir() {
   const char *d = std::getenv("FAKE_RCCL_DIR");
@@ -81,6 +116,95 @@ bool read_file(const std::string &p, void *data, size_t bytes) {
   return ok;
 }
 
+// sum[k] over the ranks' buffers src[0..G-1], in rank order from +0 or in
+// the ring's order (see the header).
+void reduce(const std::vector<const float *> &src, size_t count, bool ring, float *sum) {
+  const int G = (int)src.size();
+  if (!ring || G < 3) {
+    for (size_t k = 0; k < count; ++k) sum[k] = 0.0f;
+    for (int r = 0; r < G; ++r)
+      for (size_t k = 0; k < count; ++k) sum[k] = sum[k] + src[r][k];
+    return;
+  }
+  for (size_t c0 = 0, c = 0; c0 < count; c0 += kRingChunk, ++c) {
+    const size_t c1 = std::min(count, c0 + kRingChunk);
+    const int start = (int)((c + 1) % (size_t)G);
+    for (size_t k = c0; k < c1; ++k) sum[k] = src[start][k];
+    for (int j = 1; j < G; ++j) {
+      const float *x = src[(start + j) % G];
+      for (size_t k = c0; k < c1; ++k) sum[k] = sum[k] + x[k];
+    }
+  }
+}
+
+struct PendingOp {
+  const void *send;
+  void *recv;
+  size_t count;
+  ncclComm *comm;
+  hipStream_t stream;
+};
+
+thread_local int g_depth = 0;
+thread_local std::vector<PendingOp> g_ops;
+
+// One grouped all-reduce of a single-process clique: ops[r] is rank r's.
+ncclResult_t run_clique(const std::vector<PendingOp *> &ops) {
+  const int G = (int)ops.size();
+  const size_t count = ops[0]->count;
+  std::vector<std::vector<float>> host(G, std::vector<float>(count));
+  std::vector<const float *> src(G);
+  for (int r = 0; r < G; ++r) {
+    if (ops[r]->count != count) return ncclInvalidArgument;
+    if (hipSetDevice(ops[r]->comm->device) != hipSuccess) return ncclSystemError;
+    if (hipStreamSynchronize(ops[r]->stream) != hipSuccess) return ncclSystemError;
+    if (hipMemcpy(host[r].data(), ops[r]->send, count * sizeof(float), hipMemcpyDeviceToHost) != hipSuccess)
+      return ncclSystemError;
+    src[r] = host[r].data();
+  }
+  std::vector<float> sum(count);
+  reduce(src, count, ops[0]->comm->ring, sum.data());
+  for (int r = 0; r < G; ++r) {
+    if (hipSetDevice(ops[r]->comm->device) != hipSuccess) return ncclSystemError;
+    if (hipMemcpy(ops[r]->recv, sum.data(), count * sizeof(float), hipMemcpyHostToDevice) != hipSuccess)
+      return ncclSystemError;
+  }
+  return ncclSuccess;
+}
+
+// The per-rank (multi-process) all-reduce through files.
+ncclResult_t run_ranked(const void *send, void *recv, size_t count, ncclComm *c, hipStream_t stream) {
+  if (hipStreamSynchronize(stream) != hipSuccess) return ncclSystemError;
+  const size_t bytes = count * sizeof(float);
+  std::vector<std::vector<float>> host(c->nranks);
+  std::vector<const float *> src(c->nranks);
+  host[c->rank].resize(count);
+  if (hipMemcpy(host[c->rank].data(), send, bytes, hipMemcpyDeviceToHost) != hipSuccess) return ncclSystemError;
+  const unsigned long long seq = c->seq++;
+  if (c->nranks > 1 && !write_file(path(c, seq, c->rank, "bin"), host[c->rank].data(), bytes)) return ncclSystemError;
+  for (int r = 0; r < c->nranks; ++r) {
+    if (r != c->rank) {
+      host[r].resize(count);
+      const std::string p = path(c, seq, r, "bin");
+      if (!wait_for(p) || !read_file(p, host[r].data(), bytes)) return ncclSystemError;
+    }
+    src[r] = host[r].data();
+  }
+  std::vector<float> sum(count);
+  reduce(src, count, c->ring, sum.data());
+  if (hipMemcpy(recv, sum.data(), bytes, hipMemcpyHostToDevice) != hipSuccess) return ncclSystemError;
+  if (c->nranks > 1) {
+    // Every rank acknowledges; a rank removes its data file once all have read it.
+    const char one = 1;
+    if (!write_file(path(c, seq, c->rank, "ack"), &one, 1)) return ncclSystemError;
+    for (int r = 0; r < c->nranks; ++r)
+      if (!wait_for(path(c, seq, r, "ack"))) return ncclSystemError;
+    std::remove(path(c, seq, c->rank, "bin").c_str());
+    if (seq > 0) std::remove(path(c, seq - 1, c->rank, "ack").c_str());  // every rank is past seq - 1
+  }
+  return ncclSuccess;
+}
+
 }  // namespace
 
 extern "C" {
@@ -103,6 +227,7 @@ ncclResult_t ncclCommInitRank(ncclComm_t *comm, int nranks, ncclUniqueId id, int
   ncclComm *c = new ncclComm();
   c->nranks = nranks;
   c->rank = rank;
+  c->ring = ring_order_from_env();
   (void)hipGetDevice(&c->device);
   c->tag = hex_tag(id);
   *comm = c;
@@ -110,26 +235,68 @@ ncclResult_t ncclCommInitRank(ncclComm_t *comm, int nranks, ncclUniqueId id, int
 }
 
 ncclResult_t ncclCommInitAll(ncclComm_t *comm, int ndev, const int *devlist) {
-  if (!comm || ndev != 1) return ncclInvalidArgument;  // one device: the all-reduce is a copy
-  ncclComm *c = new ncclComm();
-  c->device = devlist ? devlist[0] : 0;
-  c->tag = "local";
-  comm[0] = c;
+  if (!comm || ndev < 1) return ncclInvalidArgument;
+  Clique *q = ndev > 1 ? new Clique() : nullptr;
+  for (int r = 0; r < ndev; ++r) {
+    ncclComm *c = new ncclComm();
+    c->nranks = ndev;
+    c->rank = r;
+    c->device = devlist ? devlist[r] : r;
+    c->ring = ring_order_from_env();
+    c->tag = "local";
+    c->clique = q;
+    if (q) q->comms.push_back(c);
+    comm[r] = c;
+  }
+  if (q) q->live = ndev;
   return ncclSuccess;
 }
 
 ncclResult_t ncclCommDestroy(ncclComm_t comm) {
+  if (!comm) return ncclInvalidArgument;
+  Clique *q = comm->clique;
   delete comm;
+  if (q && --q->live == 0) delete q;
   return ncclSuccess;
 }
 
-ncclResult_t ncclGroupStart() { return ncclSuccess; }
-ncclResult_t ncclGroupEnd() { return ncclSuccess; }
+ncclResult_t ncclGroupStart() {
+  ++g_depth;
+  return ncclSuccess;
+}
+
+ncclResult_t ncclGroupEnd() {
+  if (g_depth <= 0) return ncclInvalidUsage;
+  if (--g_depth > 0) return ncclSuccess;
+  std::vector<PendingOp> ops;
+  ops.swap(g_ops);
+  // NCCL matches the grouped calls of a clique by their order on each
+  // communicator: the k-th call on every rank forms the k-th collective.
+  std::vector<bool> done(ops.size(), false);
+  for (size_t a = 0; a < ops.size(); ++a) {
+    if (done[a]) continue;
+    Clique *q = ops[a].comm->clique;
+    const int G = (int)q->comms.size();
+    std::vector<PendingOp *> coll(G, nullptr);
+    int have = 0;
+    for (size_t b = a; b < ops.size() && have < G; ++b) {
+      if (done[b] || ops[b].comm->clique != q || coll[ops[b].comm->rank]) continue;
+      coll[ops[b].comm->rank] = &ops[b];
+      done[b] = true;
+      ++have;
+    }
+    if (have != G) return ncclInvalidUsage;  // a rank of the clique did not take part
+    const ncclResult_t r = run_clique(coll);
+    if (r != ncclSuccess) return r;
+  }
+  return ncclSuccess;
+}
 
 const char *ncclGetErrorString(ncclResult_t r) {
   switch (r) {
     case ncclSuccess: return "fake rccl: success";
     case ncclInvalidArgument: return "fake rccl: invalid argument (float sum only)";
+    case ncclInvalidUsage: return "fake rccl: invalid usage (ungrouped call on a multi-device clique, or a rank missing)";
     case ncclSystemError: return "fake rccl: a peer never arrived (timeout) or file I/O failed";
     default: return "fake rccl: error";
   }
@@ -138,32 +305,12 @@ const char *ncclGetErrorString(ncclResult_t r) {
 ncclResult_t ncclAllReduce(const void *send, void *recv, size_t count, ncclDataType_t type, ncclRedOp_t op,
                            ncclComm_t c, hipStream_t stream) {
   if (!c || type != ncclFloat || op != ncclSum) return ncclInvalidArgument;
-  if (hipStreamSynchronize(stream) != hipSuccess) return ncclSystemError;
-  const size_t bytes = count * sizeof(float);
-  std::vector<float> mine(count), sum(count, 0.0f), peer(count);
-  if (hipMemcpy(mine.data(), send, bytes, hipMemcpyDeviceToHost) != hipSuccess) return ncclSystemError;
-  const unsigned long long seq = c->seq++;
-  if (c->nranks > 1 && !write_file(path(c, seq, c->rank, "bin"), mine.data(), bytes)) return ncclSystemError;
-  for (int r = 0; r < c->nranks; ++r) {
-    const float *src = mine.data();
-    if (r != c->rank) {
-      const std::string p = path(c, seq, r, "bin");
-      if (!wait_for(p) || !read_file(p, peer.data(), bytes)) return ncclSystemError;
-      src = peer.data();
-    }
-    for (size_t k = 0; k < count; ++k) sum[k] = sum[k] + src[k];  // rank order, from +0
+  if (c->clique) {
+    if (g_depth == 0) return ncclInvalidUsage;
+    g_ops.push_back(PendingOp{send, recv, count, c, stream});
+    return ncclSuccess;
   }
-  if (hipMemcpy(recv, sum.data(), bytes, hipMemcpyHostToDevice) != hipSuccess) return ncclSystemError;
-  if (c->nranks > 1) {
-    // Every rank acknowledges; a rank removes its data file once all have read it.
-    const char one = 1;
-    if (!write_file(path(c, seq, c->rank, "ack"), &one, 1)) return ncclSystemError;
-    for (int r = 0; r < c->nranks; ++r)
-      if (!wait_for(path(c, seq, r, "ack"))) return ncclSystemError;
-    std::remove(path(c, seq, c->rank, "bin").c_str());
-    if (seq > 0) std::remove(path(c, seq - 1, c->rank, "ack").c_str());  // every rank is past seq - 1
-  }
-  return ncclSuccess;
+  return run_ranked(send, recv, count, c, stream);
 }
 
 }  // extern "C"

@@ -14,6 +14,13 @@
  * (oracle/sma_oracle.c) bit for bit; overrideModelData restores it;
  * acquireAccess / upgradeAccess hand out replicas round robin as boxed
  * Integers; addModel / delModel; free.  Exit 0 = pass.
+ *
+ * `jni_driver G` runs the same sequence over G devices in one process (the
+ * reference's own multi-GPU form, executioncontext.c:185-201): init gets G
+ * copies of device 0, so this needs the library build linked against the
+ * loopback collective (scripts/build_fake_rccl.sh builds that variant as
+ * tests/native/jni_driver_fakerccl); the checkpoint then holds one set of
+ * files per device, each checked against the oracle run with the same G.
  */
 #define _GNU_SOURCE
 #include <stdarg.h>
@@ -154,15 +161,17 @@ static void read_floats (const char *path, float *out, size_t n) {
 
 static int same_bits (const float *a, const float *b, size_t n) { return memcmp (a, b, n * sizeof (float)) == 0; }
 
-int main (void) {
+int main (int argc, char **argv) {
 	JNIEnv env = &table;
 	struct _jobject self = { OBJ_CLASS, 0, NULL, 0 };
-	const int n1 = 40000, n2 = 3331, n = n1 + n2, R = 3;
+	const int G = argc > 1 ? atoi (argv[1]) : 1;
+	const int n1 = 40000, n2 = 3331, n = n1 + n2, R = 3, size = R * G;
 	const float alpha = 0.1f, momentum = 0.9f;
+	EXPECT (G >= 1 && G <= 8);
 
-	/* TheGPU.init: one device */
-	jint devs[1] = { 0 };
-	struct _jobject d = int_array (devs, 1);
+	/* TheGPU.init: G devices */
+	jint devs[8] = { 0 };
+	struct _jobject d = int_array (devs, G);
 	EXPECT (CALL (init, &d, 2, 2, 2, 0, 0) == 0);
 
 	/* Model.GPURegister (Model.java:338-371): two variables, theModel's values */
@@ -189,13 +198,13 @@ int main (void) {
 	/* ModelManager (ModelManager.java:87): R replicas per GPU, BSP */
 	EXPECT (CALL (setModelManager, R, CBX_SYNC_BSP) == 0);
 	cbx_context *ctx = crossbow_sma_context ();
-	EXPECT (ctx != NULL && cbx_num_replicas (ctx) == R);
+	EXPECT (ctx != NULL && cbx_num_replicas (ctx) == size && cbx_num_devices (ctx) == G);
 
 	/* TaskProcessor (TaskProcessor.java:90-120): reserve a replica per task,
 	 * the task runs, the callback handler releases it (callbackhandler.c:154-155). */
 	jint clock[1] = { -1 };
 	struct _jobject ca = int_array (clock, 1);
-	for (int t = 0; t < R; ++t) {
+	for (int t = 0; t < size; ++t) {
 		jobject id = CALL (acquireAccess, &ca);
 		EXPECT (id != NULL && id->kind == OBJ_INTEGER && id->value == t && clock[0] == 0);
 		clock[0] = -1;
@@ -206,13 +215,13 @@ int main (void) {
 		EXPECT (cbx_replica_release (ctx, id->value) == 0);
 		free (id);
 	}
-	EXPECT (boxes == R);
+	EXPECT (boxes == size);
 
 	/* ResultCollector -> ModelManager.trySynchronise (ModelManager.java:293-353) */
-	EXPECT (CALL (lockAny) == R);
+	EXPECT (CALL (lockAny) == size);
 	EXPECT (CALL (merge, JNI_FALSE) == 0);  /* first locked replica with updates */
 	EXPECT (CALL (synchronise, 0, 1, 0, JNI_FALSE) == 0);
-	EXPECT (CALL (unlockAny) == R);
+	EXPECT (CALL (unlockAny) == size);
 
 	/* checkpointModel writes dir/000001 in the reference's format */
 	char dir[] = "/tmp/cbx_jni_driverXXXXXX";
@@ -221,62 +230,75 @@ int main (void) {
 	EXPECT (CALL (checkpointModel, &js) == 0);
 
 	/* The oracle: replicas and theModel start as z0, s_i = 0 (no task
-	 * produced a snapshot), last = 0; one SMA step over all three. */
-	float *z = malloc (sizeof (float) * n), *last = calloc ((size_t) n, sizeof (float));
-	float *s[3], *w[3];
-	memcpy (z, z0, sizeof (float) * n);
-	for (int i = 0; i < R; ++i) {
+	 * produced a snapshot), last = 0; one SMA step over all replicas of
+	 * all G devices (replica i on device i % G). */
+	float *z[8], *last[8];
+	for (int g = 0; g < G; ++g) {
+		z[g] = malloc (sizeof (float) * n);
+		last[g] = calloc ((size_t) n, sizeof (float));
+		memcpy (z[g], z0, sizeof (float) * n);
+	}
+	float *s[24], *w[24];
+	int locked[24], copy[24];
+	for (int i = 0; i < size; ++i) {
 		s[i] = calloc ((size_t) n, sizeof (float));
 		w[i] = malloc (sizeof (float) * n);
 		memcpy (w[i], z0, sizeof (float) * n);
+		locked[i] = 1;
+		copy[i] = 0;
 	}
-	int locked[3] = { 1, 1, 1 }, copy[3] = { 0, 0, 0 };
-	float *scratch = malloc (sizeof (float) * 2 * (size_t) n);
-	EXPECT (cbo_sma_fma (1, R, (size_t) n, alpha, momentum, &z, &last, s, w, locked, copy, 0, scratch) == 0);
+	float *scratch = malloc (sizeof (float) * (size_t) (G + 1) * (size_t) n);
+	EXPECT (cbo_sma_fma (G, size, (size_t) n, alpha, momentum, z, last, s, w, locked, copy, 0, scratch) == 0);
 
 	float *got = malloc (sizeof (float) * n);
 	char path[512];
-	snprintf (path, sizeof path, "%s/000001/gpu-00-theModel-data.dat", dir);
-	read_floats (path, got, (size_t) n);
-	EXPECT (same_bits (got, z, (size_t) n));
-	snprintf (path, sizeof path, "%s/000001/gpu-00-theModel-last.dat", dir);
-	read_floats (path, got, (size_t) n);
-	EXPECT (same_bits (got, last, (size_t) n));
-	for (int i = 0; i < R; ++i) {
-		snprintf (path, sizeof path, "%s/000001/gpu-00-replica-%03d-data.dat", dir, i);
+	for (int g = 0; g < G; ++g) {
+		/* one device per file set; a selection repeating device 0 names them by position */
+		snprintf (path, sizeof path, "%s/000001/gpu-%02d-theModel-data.dat", dir, g);
+		read_floats (path, got, (size_t) n);
+		EXPECT (same_bits (got, z[g], (size_t) n));
+		snprintf (path, sizeof path, "%s/000001/gpu-%02d-theModel-last.dat", dir, g);
+		read_floats (path, got, (size_t) n);
+		EXPECT (same_bits (got, last[g], (size_t) n));
+		EXPECT (same_bits (z[g], z[0], (size_t) n));  /* every device applied the same D */
+	}
+	for (int i = 0; i < size; ++i) {
+		snprintf (path, sizeof path, "%s/000001/gpu-%02d-replica-%03d-data.dat", dir, i % G, i);
 		read_floats (path, got, (size_t) n);
 		EXPECT (same_bits (got, w[i], (size_t) n));
 	}
-	EXPECT (! same_bits (z, z0, (size_t) n));  /* the step did move z */
+	EXPECT (! same_bits (z[0], z0, (size_t) n));  /* the step did move z */
 
 	/* Another step, then overrideModelData from 000001 and a new checkpoint:
 	 * 000002 must hold 000001's values again. */
-	EXPECT (CALL (lockAny) == R);
+	EXPECT (CALL (lockAny) == size);
 	EXPECT (CALL (synchronise, 0, 2, 0, JNI_FALSE) == 0);
-	EXPECT (CALL (unlockAny) == R);
+	EXPECT (CALL (unlockAny) == size);
 	char version[512];
 	snprintf (version, sizeof version, "%s/000001", dir);
 	struct _jobject jv = string (version);
 	EXPECT (CALL (overrideModelData, &jv) == 0);
 	EXPECT (CALL (overrideModelData, NULL) == 0);  /* GPU.c:1169: a null directory is a no-op */
 	EXPECT (CALL (checkpointModel, &js) == 0);
-	snprintf (path, sizeof path, "%s/000002/gpu-00-theModel-data.dat", dir);
-	read_floats (path, got, (size_t) n);
-	EXPECT (same_bits (got, z, (size_t) n));
+	for (int g = 0; g < G; ++g) {
+		snprintf (path, sizeof path, "%s/000002/gpu-%02d-theModel-data.dat", dir, g);
+		read_floats (path, got, (size_t) n);
+		EXPECT (same_bits (got, z[g], (size_t) n));
+	}
 
 	/* Autotune's addModel / delModel (GPU.c:1178-1199) */
-	EXPECT (CALL (lockAny) == R);
-	EXPECT (CALL (addModel) == 0);
-	EXPECT (cbx_num_replicas (ctx) == R + 1);
-	EXPECT (CALL (unlockAny) == R + 1);
-	EXPECT (CALL (lockAny) == R + 1);
+	EXPECT (CALL (lockAny) == size);
+	EXPECT (CALL (addModel) == 0);  /* one more replica per device */
+	EXPECT (cbx_num_replicas (ctx) == size + G);
+	EXPECT (CALL (unlockAny) == size + G);
+	EXPECT (CALL (lockAny) == size + G);
 	EXPECT (CALL (delModel) == 0);
-	EXPECT (cbx_num_replicas (ctx) == R);
-	EXPECT (CALL (unlockAny) == R);
+	EXPECT (cbx_num_replicas (ctx) == size);
+	EXPECT (CALL (unlockAny) == size);
 
 	EXPECT (CALL (free) == 0);
 	EXPECT (crossbow_sma_context () == NULL);
-	printf ("jni_driver: ok\n");
+	printf ("jni_driver: ok (G=%d)\n", G);
 	fflush (stdout);
 	_exit (0);
 }

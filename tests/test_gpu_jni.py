@@ -8,6 +8,14 @@ bit for bit against the oracle; then overrideModelData, acquireAccess /
 upgradeAccess (boxed Integers), addModel / delModel and free.
 scripts/build_jni_harness.sh builds the shim against tests/jni_stub/jni.h and
 the driver (both on the CPU side, beforehand; __graft_entry__.build() does it).
+
+With G > 1 the same natives drive G devices from one process, the reference's
+own multi-GPU form (init with G devices -> ncclCommInitAll, grouped
+all-reduces; executioncontext.c:185-201).  The box has one GPU, so init gets
+G copies of device 0 and the shim is linked against the library build over
+the loopback collective (tests/native/fake_rccl.cpp, scripts/build_fake_rccl.sh);
+the checkpoint then holds every device's files, each bit for bit equal to the
+oracle run with the same G.
 """
 from __future__ import annotations
 
@@ -18,6 +26,8 @@ import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 EXE = os.path.join(ROOT, "tests", "native", "jni_driver")
+# the same driver over the library build linked against the loopback collective
+EXE_LOOPBACK = os.path.join(ROOT, "tests", "native", "jni_driver_fakerccl")
 
 pytestmark = pytest.mark.gpu
 
@@ -27,3 +37,11 @@ def test_jni_natives_end_to_end():
     r = subprocess.run([EXE], capture_output=True, text=True, timeout=110)
     assert r.returncode == 0, (r.stdout + r.stderr)[-4000:]
     assert "jni_driver: ok" in r.stdout
+
+
+@pytest.mark.parametrize("G", [2, 4, 8])
+def test_jni_natives_single_process_multi_device(G):
+    assert os.path.exists(EXE_LOOPBACK), "run scripts/build_fake_rccl.sh (or __graft_entry__.build()) first"
+    r = subprocess.run([EXE_LOOPBACK, str(G)], capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0, (r.stdout + r.stderr)[-4000:]
+    assert f"jni_driver: ok (G={G})" in r.stdout

@@ -1,0 +1,115 @@
+"""The reference's own multi-GPU form on ONE GPU: one process drives G devices.
+
+Crossbow runs one JVM over all selected GPUs: ncclCommInitAll over the G
+devices (clib-multigpu/executioncontext.c:185-201) and, per step, grouped
+ncclAllReduce calls issued from one thread (synch/common.c:14-54).  The JNI
+drop-in reaches it through cbx_init(devices, G) (TheGPU_jni.c -> context.hip).
+
+Here cbx_init gets G copies of device 0 and the library build linked
+against the loopback collective (tests/native/fake_rccl.cpp), whose
+ncclCommInitAll(ndev > 1) forms an in-process clique and runs the grouped
+all-reduces at ncclGroupEnd.  So the per-device hipSetDevice loops, the
+grouped all-reduce across local communicators, the bucketed pipeline over G
+local devices, Phase D, S-SGD, the pipelined host-staged step, BN averaging,
+autotune and checkpoint / override over several local devices all run the
+product code.  Rank-order loopback: bit for bit against the oracle with the
+same G and against the committed golden fixtures; ring-order loopback: the
+G > 1 tolerance plus z / last bitwise identical on every device.
+
+The worker runs in a spawned, torch-free process (crossbow_amd/_abi.py), so
+no real RCCL is loaded beside the loopback one.  Shared machinery:
+tests/multidev_common.py.
+"""
+from __future__ import annotations
+
+import os
+import tempfile
+
+import pytest
+
+from tests import multidev_common as C
+from tests.multidev_common import Case
+
+pytestmark = pytest.mark.gpu
+
+CASES = [
+    Case("sma", 50_001, 2, 0.9, 3),
+    Case("sma-copy-ssp", 50_001, 2, 0.9, 3, copy={1: 3}, held={0: 1}),
+    Case("sma-buckets-group", 300_007, 3, 0.9, 2, bucket=65_536, copy={1: 0}, group=2),
+    Case("sma-buckets-cross", 300_007, 2, 0.9, 5, bucket=65_536, copy={2: 1}, held={3: 0}, mode=1, stride=2),
+    Case("sma-no-momentum", 20_011, 1, 0.0, 2, bucket=4096, utype=3),
+    Case("sma-staged", 100_003, 2, 0.9, 2, copy={1: 2}, staged=3),
+    Case("ssgd", 40_009, 2, 0.9, 2, utype=1),
+    Case("ssgd-buckets", 40_009, 2, 0.9, 2, bucket=4096, utype=1),
+    Case("sma-ring", 50_001, 2, 0.9, 4, copy={2: 1}, order="ring"),
+    Case("sma-ring-buckets-cross", 300_007, 2, 0.9, 4, bucket=65_536, mode=1, order="ring"),
+]
+
+
+def _jobs(G):
+    if G == 3:  # a non-power-of-two clique: the plain step in both orders
+        names = ("sma", "sma-ring")
+    elif G == 8:
+        names = ("sma-copy-ssp", "sma-buckets-cross", "ssgd-buckets", "sma-ring", "sma-ring-buckets-cross")
+    else:
+        names = [c.name for c in CASES]
+    jobs = [("case", n) for n in names if G >= 3 or not n.startswith("sma-ring")]
+    jobs += [("golden", gc["name"]) for gc in C.golden_cases(G)]
+    return jobs + [("bn", "bn"), ("autotune", "autotune")]
+
+
+def _worker(G, jobs, ckdir, q):
+    try:
+        L, A = C.load_variant()
+        cases = {c.name: c for c in CASES}
+        goldens = {gc["name"]: gc for gc in C.golden_cases(G)}
+        local = list(range(G))
+        out = []
+        for kind, name in jobs:
+            os.environ["FAKE_RCCL_ORDER"] = cases[name].order if kind == "case" else "rank"
+            g = C.init_local(L, A, G)
+            try:
+                if kind == "case":
+                    res = C.run_case(g, G, local, cases[name])
+                elif kind == "golden":
+                    res = {"bad": C.run_golden(g, G, local, goldens[name])}
+                elif kind == "bn":
+                    res = {"bad": C.run_bn(g, G, local, poison=True)}
+                else:
+                    res = {"bad": C.run_autotune_checkpoint(g, G, local, ckdir)}
+            finally:
+                g.free()
+            out.append((name, res))
+        q.put((out, None))
+    except Exception:  # pragma: no cover - reported to the parent
+        import traceback
+        q.put((None, traceback.format_exc()))
+
+
+@pytest.mark.skipif(not os.path.exists(C.VARIANT), reason="run scripts/build_fake_rccl.sh first")
+@pytest.mark.parametrize("G", [2, 3, 4, 8])
+def test_one_process_many_devices_vs_oracle(G):
+    import multiprocessing as mp
+    jobs = _jobs(G)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    with tempfile.TemporaryDirectory() as ckdir:
+        p = ctx.Process(target=_worker, args=(G, jobs, os.path.join(ckdir, "ckpt"), q))
+        p.start()
+        try:
+            res, err = q.get(timeout=110)
+        finally:
+            p.join(timeout=30)
+            if p.is_alive():
+                p.kill()
+    assert err is None, err
+    assert [name for name, _ in res] == [name for _, name in jobs]
+    failures = [(name, r["bad"]) for name, r in res if r["bad"]]
+    assert not failures, failures
+    cases = {c.name: c for c in CASES}
+    for (kind, name), (_, r) in zip(jobs, res):
+        if kind != "case":
+            continue
+        assert len(set(r["digest"].values())) == 1, f"{name}: z / last differ across devices"
+        if cases[name].order == "ring":
+            assert r["differs"] > 0, f"{name}: ring order never left the oracle's order"
