@@ -228,6 +228,10 @@ struct Device {
   unsigned long long cross_foreign = 0;  // ... and nothing else was enqueued since
   unsigned cross_parity = 0;
   ncclComm_t comm = nullptr;
+  // Peer-read all-reduce (cbx_set_allreduce_algorithm PEER): kernel A done /
+  // this device's shard of D reduced; the other devices' streams wait on them.
+  hipEvent_t peer_a = nullptr;
+  hipEvent_t peer_r = nullptr;
   cbx::BnSegment *bn_table = nullptr;  // batch-norm averaging: segment table (device)
   size_t bn_table_bytes = 0;
   float *bn_scratch = nullptr;         // packed statistics, all-reduced
@@ -307,6 +311,8 @@ struct cbx_context {
   int pipeline_mode = 0;  // 0 bucketed within a step, 1 across steps, 2 as 1 with B on comm_stream (G > 1 split path)
   int cross_wait_stride = 1;  // modes 1/2: buckets per cross-step wait
   int allreduce_group = 1;     // pipelined split path: buckets per comm-stream wait
+  int allreduce_algo = CBX_ALLREDUCE_RCCL;
+  bool peer_ready = false;     // hipDeviceEnablePeerAccess done between every pair of devices
   // Bucket events as kernel stop events (default); CBX_SEPARATE_EVENT_RECORDS=1
   // at context creation restores separate hipEventRecord markers, for A/B runs.
   bool dispatch_events = !(getenv("CBX_SEPARATE_EVENT_RECORDS") && getenv("CBX_SEPARATE_EVENT_RECORDS")[0] == '1');
@@ -503,6 +509,8 @@ void close_device(Device &d) {
   if (d.a_stream) (void)hipStreamSynchronize(d.a_stream);
   for (hipEvent_t e : d.bucket_b) (void)hipEventDestroy(e);
   if (d.cross_entry) (void)hipEventDestroy(d.cross_entry);
+  if (d.peer_a) (void)hipEventDestroy(d.peer_a);
+  if (d.peer_r) (void)hipEventDestroy(d.peer_r);
   if (d.decision) (void)hipFree(d.decision);
   if (d.a_stream) (void)hipStreamDestroy(d.a_stream);
   for (hipStream_t st : {d.h2d_stream, d.d2h_stream})
@@ -642,6 +650,91 @@ int ensure_one_rank_comm(cbx_context *c) {
   return CBX_OK;
 }
 
+// ---------------------------------------------------------------------------
+// Peer-read all-reduce, single process over G devices (sma_internal.h,
+// PeerArgs).  Per device, all on its sync stream:
+//   A(g)  [wait A(h) of every other device]  R(g)  [wait R(h) ...]  B(g)
+// R(g) sums shard g of every device's acc into this device's D (device
+// order from +0), B(g) reads each shard of D from its owner.  The next
+// step's A(h) follows B(h) on h's stream, and B(h) waited for every R, so
+// no device overwrites an acc another device is still reading; R of the
+// next step waits for every A of it, which follow every B of this one.
+// ---------------------------------------------------------------------------
+int ensure_peer_access(cbx_context *c) {
+  if (c->peer_ready) return CBX_OK;
+  for (Device &a : c->devs)
+    for (Device &b : c->devs) {
+      if (a.hip_id == b.hip_id) continue;  // one device reads itself directly
+      int can = 0;
+      HIP_TRY(hipDeviceCanAccessPeer(&can, a.hip_id, b.hip_id));
+      if (!can) return fail(CBX_ERR_UNSUPPORTED, "device %d cannot access device %d's memory", a.hip_id, b.hip_id);
+      HIP_TRY(hipSetDevice(a.hip_id));
+      hipError_t e = hipDeviceEnablePeerAccess(b.hip_id, 0);
+      if (e == hipErrorPeerAccessAlreadyEnabled) (void)hipGetLastError();
+      else if (e != hipSuccess) return fail(CBX_ERR_HIP, "hipDeviceEnablePeerAccess(%d -> %d): %s", a.hip_id, b.hip_id, hipGetErrorString(e));
+    }
+  for (Device &d : c->devs) {
+    HIP_TRY(hipSetDevice(d.hip_id));
+    if (!d.peer_a) HIP_TRY(hipEventCreateWithFlags(&d.peer_a, hipEventDisableTiming));
+    if (!d.peer_r) HIP_TRY(hipEventCreateWithFlags(&d.peer_r, hipEventDisableTiming));
+  }
+  c->peer_ready = true;
+  return CBX_OK;
+}
+
+int sma_step_peer(cbx_context *c, std::vector<cbx::SmaArgs> &args, bool mom) {
+  TRY(ensure_peer_access(c));
+  const int G = (int)c->devs.size();
+  const int64_t pad = cbx::kPadFloat4;
+  const int64_t s4 = ((c->n4 + G - 1) / G + pad - 1) / pad * pad;  // float4s per shard
+  cbx::PeerArgs p;
+  std::memset(&p, 0, sizeof(p));
+  p.G = G;
+  p.shard4 = s4;
+  for (int h = 0; h < G; ++h) {
+    p.ctrl_in[h] = base_ctrl(c->devs[h], CBX_BUF_GRADIENT);
+    p.D[h] = reinterpret_cast<const cbx::v4f *>(base_dev(c, c->devs[h], CBX_BUF_DIFF));
+  }
+  for (int k = 0; k < G; ++k) {
+    Device &d = c->devs[k];
+    HIP_TRY(hipSetDevice(d.hip_id));
+    cbx::LaunchConfig cfg = c->cfg;
+    cfg.num_cus = d.num_cus;
+    HIP_TRY(cbx::launch_sma_accumulate(args[k], true, cfg, d.stream, {ring_event(c, d, EV_START), ring_event(c, d, EV_A)}));
+    HIP_TRY(hipEventRecord(d.peer_a, d.stream));
+  }
+  for (int k = 0; k < G; ++k) {
+    Device &d = c->devs[k];
+    HIP_TRY(hipSetDevice(d.hip_id));
+    for (int h = 0; h < G; ++h)
+      if (h != k) HIP_TRY(hipStreamWaitEvent(d.stream, c->devs[h].peer_a, 0));
+    const int64_t start = std::min<int64_t>((int64_t)k * s4, c->n4);
+    cbx::PeerArgs r = p;
+    for (int h = 0; h < G; ++h)
+      r.acc[h] = reinterpret_cast<const cbx::v4f *>(base_dev(c, c->devs[h], CBX_BUF_GRADIENT)) + start;
+    r.out = reinterpret_cast<cbx::v4f *>(base_dev(c, d, CBX_BUF_DIFF)) + start;
+    r.ctrl_out = base_ctrl(d, CBX_BUF_DIFF);
+    r.n4 = std::min(s4, c->n4 - start);  // 0 for a trailing empty shard: block 0 still sums the control block
+    cbx::LaunchConfig cfg = c->apply_cfg;
+    cfg.num_cus = d.num_cus;
+    HIP_TRY(cbx::launch_sma_peer_reduce(r, cfg, d.stream, {nullptr, ring_event(c, d, EV_AR)}));
+    HIP_TRY(hipEventRecord(d.peer_r, d.stream));
+  }
+  for (int k = 0; k < G; ++k) {
+    Device &d = c->devs[k];
+    HIP_TRY(hipSetDevice(d.hip_id));
+    for (int h = 0; h < G; ++h)
+      if (h != k) HIP_TRY(hipStreamWaitEvent(d.stream, c->devs[h].peer_r, 0));
+    cbx::LaunchConfig cfg = c->apply_cfg;
+    cfg.num_cus = d.num_cus;
+    HIP_TRY(cbx::launch_sma_peer_apply(args[k], p, mom, cfg, d.stream, {nullptr, step_stop_event(c, d, EV_B)}));
+    ring_advance(c, d, 1);
+    d.cross_valid = false;
+  }
+  c->last_step_split = true;
+  return CBX_OK;
+}
+
 int sma_step(cbx_context *c, int first) {
   const bool mom = c->has_last && c->model.conf.momentum > 0;  // sma.c:150 (base conf)
   std::vector<cbx::SmaArgs> args(c->devs.size());
@@ -653,7 +746,9 @@ int sma_step(cbx_context *c, int first) {
   }
 
   TRY(ensure_one_rank_comm(c));
-  if (c->G == 1 && !c->force_split) {
+  if (c->allreduce_algo == CBX_ALLREDUCE_PEER && c->G > 1) {
+    TRY(sma_step_peer(c, args, mom));
+  } else if (c->G == 1 && !c->force_split) {
     // Single GPU: Phase B is the identity, so A + C (+ D) fuse into one pass.
     // (sma.c:63 waits on base->updated; every producer of z is this stream,
     // so stream order already gives that dependency.)
@@ -2625,6 +2720,18 @@ int cbx_set_allreduce_group(cbx_context *c, int group) {
   TRY(check_ctx(c));
   if (group < 1 || group > 4096) return fail(CBX_ERR_INVALID, "all-reduce group must be 1..4096");
   c->allreduce_group = group;
+  return CBX_OK;
+}
+
+int cbx_set_allreduce_algorithm(cbx_context *c, int algorithm) {
+  TRY(check_ctx(c));
+  if (algorithm != CBX_ALLREDUCE_RCCL && algorithm != CBX_ALLREDUCE_PEER)
+    return fail(CBX_ERR_INVALID, "all-reduce algorithm must be CBX_ALLREDUCE_RCCL or CBX_ALLREDUCE_PEER");
+  if (algorithm == CBX_ALLREDUCE_PEER && c->per_rank && c->G > 1)
+    return fail(CBX_ERR_UNSUPPORTED, "the peer-read all-reduce needs one process over every device (cbx_init)");
+  if (algorithm == CBX_ALLREDUCE_PEER && c->G > cbx::kMaxDevices)
+    return fail(CBX_ERR_UNSUPPORTED, "the peer-read all-reduce takes at most %d devices", cbx::kMaxDevices);
+  c->allreduce_algo = algorithm;
   return CBX_OK;
 }
 

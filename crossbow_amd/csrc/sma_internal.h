@@ -170,6 +170,35 @@ hipError_t launch_sma_accumulate(const SmaArgs &a, bool write_ctrl,
 // Multi-GPU kernel B: Phase C (+ D, gated by the reduced control slot).
 hipError_t launch_sma_apply(const SmaArgs &a, bool momentum,
                             const LaunchConfig &cfg, hipStream_t stream, Timing t = {});
+// Peer-read all-reduce of the single-process multi-device form (one process
+// drives every GPU, the reference's own form, executioncontext.c:185-201):
+// instead of an RCCL pass, kernels read the peers' buffers directly over
+// xGMI (hipDeviceEnablePeerAccess), the way the reference's non-NCCL path
+// copies peer buffers (synch/common.c:64-95).  Two-shot: device g reduces
+// shard g of every device's acc (peer reads) into its own D, then kernel B
+// on every device reads each shard of D from its owner and applies Phase C.
+// Per GPU that moves 2 (G-1)/G * 4n bytes over xGMI, as a ring all-reduce
+// does, but over all G-1 links at once, with no RCCL kernel and no extra D
+// pass.  The sums run in device order from +0: the oracle's order, so the
+// result is bit-exact and identical on every device.
+constexpr int kMaxDevices = 16;
+struct PeerArgs {
+  const v4f *acc[kMaxDevices];        // reduce: every device's acc at this device's shard
+  const float *ctrl_in[kMaxDevices];  // reduce: every device's acc control block
+  const v4f *D[kMaxDevices];          // apply: every device's D (whole buffer; shard h is valid on device h)
+  v4f *out;                           // reduce: this device's D at its shard
+  float *ctrl_out;                    // reduce: this device's D control block
+  int64_t n4;                         // reduce: float4s of the shard (may be 0)
+  int64_t shard4;                     // float4s per shard (a multiple of kPadFloat4)
+  int G;
+  int pad_;
+};
+// D[shard] = sum over devices of acc[shard] in device order; the control
+// blocks are summed the same way (block 0).
+hipError_t launch_sma_peer_reduce(const PeerArgs &p, const LaunchConfig &cfg, hipStream_t stream, Timing t = {});
+// Kernel B reading D from each shard's owner: Phase C (+ D on copy).
+hipError_t launch_sma_peer_apply(const SmaArgs &a, const PeerArgs &p, bool momentum, const LaunchConfig &cfg,
+                                 hipStream_t stream, Timing t = {});
 // The replica's local optimiser step of one task (the producer of s and w,
 // clib-multigpu/kernels/optimisers/sma.cu:3-100), fused into one pass.
 struct OptArgs {

@@ -256,6 +256,87 @@ __global__ __launch_bounds__(256) void sma_apply_kernel(const SmaArgs a) {
 }
 
 // ---------------------------------------------------------------------------
+// Peer-read two-shot all-reduce (single process, G devices; sma_internal.h).
+// Reduce: this device's shard of D = sum over devices of acc, every load of a
+// trip (G streams, G-1 of them remote over xGMI) in flight before the adds.
+// ---------------------------------------------------------------------------
+template <int G_, int P, int U>
+__global__ __launch_bounds__(256) void sma_peer_reduce_kernel(const PeerArgs p) {
+  constexpr int GG = (G_ > 0) ? G_ : kMaxDevices;
+  const int G = (G_ > 0) ? G_ : p.G;
+  if (p.ctrl_out != nullptr && blockIdx.x == 0 && threadIdx.x < kCtrlFloats) {
+    float s = 0.0f;  // common.c:45-52 sums the control block with the data
+    for (int h = 0; h < G; ++h) s = s + p.ctrl_in[h][threadIdx.x];
+    p.ctrl_out[threadIdx.x] = s;
+  }
+  const uint32_t trip = gridDim.x * blockDim.x * U;
+  const uint32_t n4 = (uint32_t)p.n4;
+  for (uint32_t base = first_elem<U>(); base < n4; base += trip) {
+    v4f x[U][GG];
+#pragma unroll
+    for (int h = 0; h < GG; ++h) {
+      if (G_ <= 0 && h >= G) break;
+#pragma unroll
+      for (int u = 0; u < U; ++u) x[u][h] = ldo<P>(p.acc[h], (base + u * 64u) * 16u);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      v4f sum = 0.0f;  // device order from +0: the oracle's (and the loopback's rank) order
+#pragma unroll
+      for (int h = 0; h < GG; ++h) {
+        if (G_ <= 0 && h >= G) break;
+        sum = sum + x[u][h];
+      }
+      sto<P>(p.out, (base + u * 64u) * 16u, sum);
+    }
+  }
+}
+
+// Kernel B of the peer path: D of element i comes from the owner of its
+// shard.  Shards are multiples of kPadFloat4 float4s and a wave's 64*U float4s
+// never straddle one, so the owner is wave-uniform (readfirstlane: the
+// pointer is fetched with a scalar load).
+template <bool MOM, int P, int U>
+__global__ __launch_bounds__(256) void sma_peer_apply_kernel(const SmaArgs a, const PeerArgs p) {
+  const bool copy = a.ctrl_in[0] > 0.0f;
+  const uint32_t trip = gridDim.x * blockDim.x * U;
+  const uint32_t n4 = (uint32_t)a.n4;
+  const uint32_t shard4 = (uint32_t)p.shard4;
+  const v4f mb = kBaseMomentum;
+  const v4f one = 1.0f;
+  for (uint32_t base = first_elem<U>(); base < n4; base += trip) {
+    int owner = __builtin_amdgcn_readfirstlane((int)(base / shard4));
+    if (owner > p.G - 1) owner = p.G - 1;
+    const v4f *D = p.D[owner];
+    v4f Dv[U], zv[U], lv[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t i = (base + u * 64u) * 16u;
+      Dv[u] = ldo<P>(D, i);
+      zv[u] = ldo<P>(a.z, i);
+      if constexpr (MOM) lv[u] = ldo<P>(a.last, i);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t i = (base + u * 64u) * 16u;
+      if constexpr (MOM) {
+        Dv[u] = vfma(mb, lv[u], Dv[u]);
+        sto<P>(a.last, i, Dv[u]);
+      }
+      zv[u] = vfma(one, Dv[u], zv[u]);
+      sto<P>(a.z, i, zv[u]);
+    }
+    if (copy) {
+      for (int r = 0; r < a.nrep; ++r) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) sto<P>(a.w[r], (base + u * 64u) * 16u, zv[u]);
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Replica optimiser step (clib-multigpu/kernels/optimisers/sma.cu:3-100).  The
 // reference issues up to 6 full-model ops per task (saxpy wd, sscal, saxpy mu,
 // copy last, copy diff, saxpy); here one pass reads w, g (, last) once and
@@ -578,7 +659,54 @@ hipError_t apply_u(const SmaArgs &a, const LaunchConfig &cfg0, hipStream_t s, Ti
   return hipGetLastError();
 }
 
+template <int G_, int P>
+hipError_t peer_reduce_g(const PeerArgs &p, const LaunchConfig &cfg0, hipStream_t s, Timing t) {
+  const LaunchConfig cfg = small_launch_shape(cfg0, p.n4);
+  const dim3 g = grid_for(p.n4, cfg);
+  const unsigned lds = lds_for_occupancy(cfg, p.G, 1, g.x);
+  if (cfg.unroll == 2)
+    hipExtLaunchKernelGGL((sma_peer_reduce_kernel<G_, P, 2>), g, dim3(cfg.block), lds, s, t.start, t.stop, 0, p);
+  else
+    hipExtLaunchKernelGGL((sma_peer_reduce_kernel<G_, P, 1>), g, dim3(cfg.block), lds, s, t.start, t.stop, 0, p);
+  return hipGetLastError();
+}
+
+template <int P>
+hipError_t peer_reduce_p(const PeerArgs &p, const LaunchConfig &cfg, hipStream_t s, Timing t) {
+  switch (p.G) {
+    case 2: return peer_reduce_g<2, P>(p, cfg, s, t);
+    case 4: return peer_reduce_g<4, P>(p, cfg, s, t);
+    case 8: return peer_reduce_g<8, P>(p, cfg, s, t);
+    default: return peer_reduce_g<-1, P>(p, cfg, s, t);
+  }
+}
+
+template <bool MOM, int P>
+hipError_t peer_apply_u(const SmaArgs &a, const PeerArgs &p, const LaunchConfig &cfg0, hipStream_t s, Timing t) {
+  const LaunchConfig cfg = small_launch_shape(cfg0, a.n4);
+  const dim3 g = grid_for(a.n4, cfg);
+  const unsigned lds = lds_for_occupancy(cfg, MOM ? 3 : 2, MOM ? 2 : 1, g.x);
+  if (cfg.unroll == 2)
+    hipExtLaunchKernelGGL((sma_peer_apply_kernel<MOM, P, 2>), g, dim3(cfg.block), lds, s, t.start, t.stop, 0, a, p);
+  else
+    hipExtLaunchKernelGGL((sma_peer_apply_kernel<MOM, P, 1>), g, dim3(cfg.block), lds, s, t.start, t.stop, 0, a, p);
+  return hipGetLastError();
+}
+
 }  // namespace
+
+hipError_t launch_sma_peer_reduce(const PeerArgs &p, const LaunchConfig &cfg, hipStream_t stream, Timing t) {
+  if (p.G < 1 || p.G > kMaxDevices) return hipErrorInvalidValue;
+  return cfg.policy == 1 ? peer_reduce_p<1>(p, cfg, stream, t) : peer_reduce_p<0>(p, cfg, stream, t);
+}
+
+hipError_t launch_sma_peer_apply(const SmaArgs &a, const PeerArgs &p, bool momentum, const LaunchConfig &cfg,
+                                 hipStream_t stream, Timing t) {
+  if (p.G < 1 || p.G > kMaxDevices || p.shard4 <= 0 || p.shard4 % kPadFloat4 != 0) return hipErrorInvalidValue;
+  if (cfg.policy == 1)
+    return momentum ? peer_apply_u<true, 1>(a, p, cfg, stream, t) : peer_apply_u<false, 1>(a, p, cfg, stream, t);
+  return momentum ? peer_apply_u<true, 0>(a, p, cfg, stream, t) : peer_apply_u<false, 0>(a, p, cfg, stream, t);
+}
 
 hipError_t launch_sma_fused(const SmaArgs &a, bool momentum, bool copy, const LaunchConfig &cfg,
                             hipStream_t stream, Timing t) {

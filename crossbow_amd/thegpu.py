@@ -398,6 +398,10 @@ class TheGPU:
         """Split path: buckets all-reduced behind one wait on the group's last kernel A."""
         check(self._L.cbx_set_allreduce_group(self._ctx, group))
 
+    def set_allreduce_algorithm(self, algorithm: int) -> None:
+        """ALLREDUCE_RCCL (default) or ALLREDUCE_PEER (one process over every device: peer reads over xGMI)."""
+        check(self._L.cbx_set_allreduce_algorithm(self._ctx, algorithm))
+
     def set_bucket_elements(self, elements: int) -> None:
         check(self._L.cbx_set_bucket_elements(self._ctx, elements))
 

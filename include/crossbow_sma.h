@@ -361,6 +361,21 @@ int cbx_set_cross_wait_stride (cbx_context *ctx, int stride);
  * pipeline itself is this library's (common.c:14-54 all-reduces one flat
  * buffer).                                                                */
 int cbx_set_allreduce_group (cbx_context *ctx, int group);
+/* How the SMA step's all-reduce crosses devices (G > 1):
+ *   CBX_ALLREDUCE_RCCL (0, default): grouped ncclAllReduce, bucketed and
+ *     pipelined as configured above (synch/common.c:3-57);
+ *   CBX_ALLREDUCE_PEER (1): one process over every device only (cbx_init
+ *     with G devices).  No RCCL pass: after hipDeviceEnablePeerAccess,
+ *     device g sums shard g of every device's acc by direct peer reads, then
+ *     kernel B on each device reads every shard of D from its owner
+ *     (two-shot over all xGMI links at once; the reference's non-NCCL path
+ *     copies peer buffers, common.c:64-95).  Sums in device order: bit-exact
+ *     against the rank-order oracle and identical on every device.  The
+ *     host-staged step and S-SGD keep RCCL.
+ * CBX_ERR_UNSUPPORTED for PEER on a one-process-per-GPU context.          */
+#define CBX_ALLREDUCE_RCCL 0
+#define CBX_ALLREDUCE_PEER 1
+int cbx_set_allreduce_algorithm (cbx_context *ctx, int algorithm);
 /* Force the multi-GPU pipeline (kernel A + RCCL all-reduce + kernel B) even
  * at G = 1 (a one-rank communicator), so a single-GPU host exercises it.  */
 int cbx_set_force_split (cbx_context *ctx, int force);

@@ -136,6 +136,8 @@ class Case:
     stride: int = 1            # cbx_set_cross_wait_stride
     group: int = 1             # cbx_set_allreduce_group
     order: str = "rank"        # loopback summation order ("rank" or "ring")
+    algo: int = 0              # cbx_set_allreduce_algorithm: 0 RCCL, 1 peer reads (one process only)
+    algo_at: Dict[int, int] = field(default_factory=dict)  # step -> algorithm switched to before it
 
 
 def digest(*arrs) -> str:
@@ -194,6 +196,8 @@ def run_case(g: Ctx, world: int, local: List[int], case: Case) -> dict:
     g("cbx_set_pipeline_mode", case.mode)
     g("cbx_set_cross_wait_stride", case.stride)
     g("cbx_set_allreduce_group", case.group)
+    if case.algo:
+        g("cbx_set_allreduce_algorithm", case.algo)
     size = world * R
     assert g("cbx_num_replicas") == size and g("cbx_num_devices") == world
     mine = [i for i in range(size) if i % world in local]
@@ -223,6 +227,8 @@ def run_case(g: Ctx, world: int, local: List[int], case: Case) -> dict:
     acc = [np.zeros(n, np.float32) for _ in range(world)]
     task = 0
     for step in range(case.steps):
+        if step in case.algo_at:
+            g("cbx_set_allreduce_algorithm", case.algo_at[step])
         if case.utype == 1:  # S-SGD task steps: the global task list, each process runs its replicas' tasks
             for k in range(wpc):
                 i = k % size
@@ -277,9 +283,11 @@ def run_case(g: Ctx, world: int, local: List[int], case: Case) -> dict:
     return {"bad": check.bad, "digest": dig, "differs": check.differs}
 
 
-def run_golden(g: Ctx, world: int, local: List[int], gcase: dict) -> List[str]:
+def run_golden(g: Ctx, world: int, local: List[int], gcase: dict, algo: int = 0) -> List[str]:
     """One committed fixture (tests/golden/, G = world): one step, bit for bit."""
     A = g.A
+    if algo:
+        g("cbx_set_allreduce_algorithm", algo)
     st = gcase["state"]
     n = st.n
     R = st.size // st.G

@@ -16,6 +16,12 @@ product code.  Rank-order loopback: bit for bit against the oracle with the
 same G and against the committed golden fixtures; ring-order loopback: the
 G > 1 tolerance plus z / last bitwise identical on every device.
 
+The peer-read all-reduce (cbx_set_allreduce_algorithm PEER: two-shot over
+direct peer reads, no RCCL pass) runs only in this form; its cases, and the
+golden fixtures run through it, are bit for bit against the oracle (device
+order from +0 is the oracle's order).  On one GPU every "peer" is device 0
+itself, so this pins the algorithm, not its xGMI speed.
+
 The worker runs in a spawned, torch-free process (crossbow_amd/_abi.py), so
 no real RCCL is loaded beside the loopback one.  Shared machinery:
 tests/multidev_common.py.
@@ -43,18 +49,27 @@ CASES = [
     Case("ssgd-buckets", 40_009, 2, 0.9, 2, bucket=4096, utype=1),
     Case("sma-ring", 50_001, 2, 0.9, 4, copy={2: 1}, order="ring"),
     Case("sma-ring-buckets-cross", 300_007, 2, 0.9, 4, bucket=65_536, mode=1, order="ring"),
+    # the peer-read two-shot all-reduce (cbx_set_allreduce_algorithm PEER): no RCCL pass
+    Case("sma-peer", 50_001, 2, 0.9, 3, copy={1: 3}, held={0: 1}, algo=1),
+    Case("sma-peer-no-momentum", 20_011, 1, 0.0, 2, utype=3, algo=1),
+    Case("sma-peer-empty-shards", 1031, 2, 0.9, 3, copy={2: 0}, algo=1),  # n4 = one pad: trailing shards empty
+    Case("sma-peer-big", 300_007, 3, 0.9, 2, algo=1),
+    # switching between the algorithms, and from the cross-step pipeline, between steps
+    Case("sma-peer-switch", 300_007, 2, 0.9, 5, bucket=65_536, mode=1, copy={3: 1}, algo_at={1: 1, 2: 0, 4: 1}),
 ]
 
 
 def _jobs(G):
-    if G == 3:  # a non-power-of-two clique: the plain step in both orders
-        names = ("sma", "sma-ring")
+    if G == 3:  # a non-power-of-two clique: the plain step in both orders, and the peer path
+        names = ("sma", "sma-ring", "sma-peer", "sma-peer-empty-shards")
     elif G == 8:
-        names = ("sma-copy-ssp", "sma-buckets-cross", "ssgd-buckets", "sma-ring", "sma-ring-buckets-cross")
+        names = ("sma-copy-ssp", "sma-buckets-cross", "ssgd-buckets", "sma-ring", "sma-ring-buckets-cross",
+                 "sma-peer", "sma-peer-empty-shards", "sma-peer-switch")
     else:
         names = [c.name for c in CASES]
     jobs = [("case", n) for n in names if G >= 3 or not n.startswith("sma-ring")]
     jobs += [("golden", gc["name"]) for gc in C.golden_cases(G)]
+    jobs += [("golden-peer", gc["name"]) for gc in C.golden_cases(G)]
     return jobs + [("bn", "bn"), ("autotune", "autotune")]
 
 
@@ -71,8 +86,8 @@ def _worker(G, jobs, ckdir, q):
             try:
                 if kind == "case":
                     res = C.run_case(g, G, local, cases[name])
-                elif kind == "golden":
-                    res = {"bad": C.run_golden(g, G, local, goldens[name])}
+                elif kind in ("golden", "golden-peer"):
+                    res = {"bad": C.run_golden(g, G, local, goldens[name], algo=1 if kind == "golden-peer" else 0)}
                 elif kind == "bn":
                     res = {"bad": C.run_bn(g, G, local, poison=True)}
                 else:

@@ -81,6 +81,8 @@ def _rank_main(rank, world, jobs, uids, fake_dir, q):
             os.environ["FAKE_RCCL_ORDER"] = case.order if (kind == "case") else "rank"
             g = C.init_rank(L, A, rank, world, uid)
             try:
+                # the peer-read all-reduce needs one process over every device
+                assert L.cbx_set_allreduce_algorithm(g.c, A.ALLREDUCE_PEER) == A.CBX_ERR_UNSUPPORTED
                 if kind == "case":
                     res = C.run_case(g, world, [rank], case)
                 elif kind == "golden":
