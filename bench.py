@@ -257,9 +257,10 @@ def main():
     tuning = None
     pipeline_mode = 0
     wait_stride = 1
+    ar_group = 1
     if split and args.bucket_mb == 0:
         # warm-up autotune of the bucket count on the live communicator (same choice on every rank)
-        bucket_elems, pipeline_mode, wait_stride, tuning = D.tune_buckets(gpu, n, world, step)
+        bucket_elems, pipeline_mode, wait_stride, ar_group, tuning = D.tune_buckets(gpu, n, world, step)
 
     for _ in range(args.warmup):
         step()
@@ -305,6 +306,7 @@ def main():
                         else -(-n // min(bucket_elems, n)) if bucket_elems else "library default (8)"),
             "pipeline_mode": None if not split else pipeline_mode,
             "cross_wait_stride": None if not split else wait_stride,
+            "allreduce_group": None if not split else ar_group,
             "bucket_tuning_ms_per_step": tuning,
             "kernel_config": dict(block=args.block, blocks_per_cu=args.blocks_per_cu, policy=args.policy,
                                   unroll=args.unroll, waves_per_cu=args.waves_per_cu, bucket_mb=args.bucket_mb),

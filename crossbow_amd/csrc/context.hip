@@ -308,14 +308,11 @@ struct cbx_context {
   int64_t bucket_elems = 0;
   bool force_split = false;
   bool last_step_split = false;
-  int pipeline_mode = 0;  // 0 bucketed within a step, 1 across steps, 2 as 1 with B on comm_stream (G > 1 split path)
-  int cross_wait_stride = 1;  // modes 1/2: buckets per cross-step wait
+  int pipeline_mode = 0;  // 0 bucketed within a step, 1 across steps (G > 1 split path)
+  int cross_wait_stride = 1;  // mode 1: buckets per cross-step wait
   int allreduce_group = 1;     // pipelined split path: buckets per comm-stream wait
   int allreduce_algo = CBX_ALLREDUCE_RCCL;
   bool peer_ready = false;     // hipDeviceEnablePeerAccess done between every pair of devices
-  // Bucket events as kernel stop events (default); CBX_SEPARATE_EVENT_RECORDS=1
-  // at context creation restores separate hipEventRecord markers, for A/B runs.
-  bool dispatch_events = !(getenv("CBX_SEPARATE_EVENT_RECORDS") && getenv("CBX_SEPARATE_EVENT_RECORDS")[0] == '1');
   // Bumped by every C-ABI call that may enqueue work on a sync stream other
   // than the barrier path itself: a cross-step pipelined step then joins the
   // whole sync stream instead of waiting bucket by bucket.
@@ -789,20 +786,12 @@ int sma_step(cbx_context *c, int first) {
     //   stream      : [wait red(0)] B(0) [wait red(1)] B(1) ...
     // A step joins the whole sync stream instead when anything else was
     // enqueued since the last cross-pipelined step (foreign_ops).
-    const bool cross = pipelined && c->pipeline_mode >= 1;
-    // Mode 2: as mode 1, but kernel B(k) runs on comm_stream right behind
-    // AR(k), so no event separates them and the sync stream joins once per
-    // step (after the last B) instead of waiting once per bucket:
-    //   a_stream    : [wait b(0)'] A(0) [wait b(1)'] A(1) ...
-    //   comm_stream : [wait acc(0)] AR(0) B(0) [wait acc(1)] AR(1) B(1) ...
-    //   stream      :                                  ... [wait B(nb-1)]
-    const bool b_on_comm = cross && c->pipeline_mode == 2;
+    const bool cross = pipelined && c->pipeline_mode == 1;
     // Per-bucket events ride on the kernels' own dispatch packets (stop
     // event) instead of a separate hipEventRecord marker, which left a
     // ~10 us gap on the sync stream per bucket: -2 to -8 % per step
     // (scripts/dispatch_event_ab.py, profiles/r01/dispatch_event_ab.json).
-    const bool dispatch_events = c->dispatch_events;
-    // Modes 1/2: A(k) waits for B(k + stride - 1) of the last step once per
+    // Mode 1: A(k) waits for B(k + stride - 1) of the last step once per
     // `stride` buckets (it implies B(k..): same stream).  Each satisfied
     // cross-queue wait still costs the waiting queue ~10 us; fewer waits
     // trade that for less cross-step overlap (cbx_set_cross_wait_stride).
@@ -869,7 +858,7 @@ int sma_step(cbx_context *c, int first) {
         NCCL_TRY(ncclAllReduce(src, dst, count, ncclFloat, ncclSum, d.comm, on_comm ? d.comm_stream : d.stream));
       }
       NCCL_TRY(ncclGroupEnd());
-      if (on_comm && !b_on_comm) {
+      if (on_comm) {
         for (size_t k = 0; k < c->devs.size(); ++k) {
           Device &d = c->devs[k];
           HIP_TRY(hipSetDevice(d.hip_id));
@@ -892,10 +881,8 @@ int sma_step(cbx_context *c, int first) {
         hipStream_t st = cross ? d.a_stream : d.stream;
         if (cross && !join[k] && b % wait_stride == 0)  // B(b .. b+stride-1) of the last step
           HIP_TRY(hipStreamWaitEvent(st, d.bucket_b[std::min<int64_t>(b + wait_stride - 1, nb - 1)], 0));
-        const bool in_dispatch = pipelined && dispatch_events;
-        if (in_dispatch) t.stop = d.bucket_acc[b];
+        if (pipelined) t.stop = d.bucket_acc[b];
         HIP_TRY(cbx::launch_sma_accumulate(offset_args(args[k], start, len), b == 0, cfg, st, t));
-        if (pipelined && !in_dispatch) HIP_TRY(hipEventRecord(d.bucket_acc[b], st));
       }
       return CBX_OK;
     };
@@ -905,8 +892,7 @@ int sma_step(cbx_context *c, int first) {
       for (size_t k = 0; k < c->devs.size(); ++k) {
         Device &d = c->devs[k];
         HIP_TRY(hipSetDevice(d.hip_id));
-        hipStream_t st = b_on_comm ? d.comm_stream : d.stream;
-        if (pipelined && !b_on_comm) HIP_TRY(hipStreamWaitEvent(d.stream, d.bucket_red[b], 0));
+        if (pipelined) HIP_TRY(hipStreamWaitEvent(d.stream, d.bucket_red[b], 0));
         cbx::LaunchConfig cfg = c->apply_cfg;
         cfg.num_cus = d.num_cus;
         cbx::Timing t;
@@ -919,12 +905,10 @@ int sma_step(cbx_context *c, int first) {
           a.decision_mode = b == 0 ? 1 : 2;
           a.decision = d.decision + (d.cross_parity & 1u);
         }
-        const bool in_dispatch = cross && dispatch_events && !t.stop;
+        const bool in_dispatch = cross && !t.stop;
         if (in_dispatch) t.stop = d.bucket_b[b];
-        HIP_TRY(cbx::launch_sma_apply(a, mom, cfg, st, t));
-        if (cross && !in_dispatch) HIP_TRY(hipEventRecord(d.bucket_b[b], st));
-        // The step's last kernel ran on comm_stream: join it into the sync stream.
-        if (b_on_comm && b == nb - 1) HIP_TRY(hipStreamWaitEvent(d.stream, t.stop, 0));
+        HIP_TRY(cbx::launch_sma_apply(a, mom, cfg, d.stream, t));
+        if (cross && !in_dispatch) HIP_TRY(hipEventRecord(d.bucket_b[b], d.stream));
       }
       return CBX_OK;
     };
@@ -941,9 +925,9 @@ int sma_step(cbx_context *c, int first) {
       // comm-stream wait on the group's last kernel A (cbx_set_allreduce_group).
       // Every event is recorded before the wait on it is enqueued: a group's
       // all-reduces follow its last A, and B(j) follows AR(j).  Mode 0 applies
-      // the previous group while this one is on the link; modes 1/2 apply a
+      // the previous group while this one is on the link; mode 1 applies a
       // group right behind its all-reduces.  ar_group 1 is the per-bucket order
-      // A(b) AR(b) B(b-1) (mode 0) / A(b) AR(b) B(b) (modes 1/2).
+      // A(b) AR(b) B(b-1) (mode 0) / A(b) AR(b) B(b) (mode 1).
       const int64_t ar_group = std::max(1, c->allreduce_group);
       int64_t applied = 0;
       for (int64_t b = 0; b < nb; ++b) {
@@ -1982,12 +1966,24 @@ int cbx_del_model(cbx_context *c) {
   TRY(check_manager(c));
   if (c->R <= 1) return fail(CBX_ERR_STATE, "cannot delete the last replica of a device");  // :511
   const int size_ = c->size - c->G;
-  for (int id = size_; id < c->size; ++id) {
+  // crossbowThetaQueueShrink (:537): the slots leave the rotation first, so
+  // no task reserves a removed id from now on; a task still holding its
+  // reservation gets 0 from cbx_upgrade_access.
+  for (int id = size_; id < c->size; ++id) c->theta[id].state.store(kThetaSkip, std::memory_order_release);
+  // A task may hold a removed replica (ASP / SSP barriers do not lock busy
+  // ones): wait until it releases it (cbx_replica_release still takes the
+  // id) before its buffers go.  Then shrink the count, so no lookup sees the
+  // removed ids any more.
+  for (int id = size_; id < c->size; ++id)
+    if (!c->locked[id]) pthread_mutex_lock(&c->replicas[id]->lock);
+  const int old_size = c->size;
+  c->size = size_;
+  for (int id = size_; id < old_size; ++id) {
     Replica *r = c->replicas[id];
     if (r->local >= 0) {
       Device &d = c->devs[r->local];
       HIP_TRY(hipSetDevice(d.hip_id));
-      HIP_TRY(hipStreamSynchronize(d.stream));  // :530
+      HIP_TRY(hipDeviceSynchronize());  // :530, every stream (task streams included)
       if (r->slot >= d.base_slots) {
         const size_t k = (size_t)(r->slot - d.base_slots);
         HIP_TRY(hipFree(d.extra[k]));
@@ -2001,16 +1997,11 @@ int cbx_del_model(cbx_context *c) {
       r->client = nullptr;
       d.replicas.erase(std::remove(d.replicas.begin(), d.replicas.end(), id), d.replicas.end());
     }
-    // crossbowThetaQueueShrink (:537): the slot leaves the rotation.  A task
-    // still holding its reservation gets -1 from cbx_upgrade_access.
-    c->theta[id].state.store(kThetaSkip, std::memory_order_release);
-    if (c->locked[id]) pthread_mutex_unlock(&r->lock);
+    pthread_mutex_unlock(&r->lock);
     c->retired.push_back(r);  // freed by cbx_free: a task may still hold a reference
   }
-  // Shrink the count first: a task that reads it afterwards no longer picks
-  // the removed ids.  The arrays keep their capacity (reserved at creation),
-  // so they never move under a reader.
-  c->size = size_;
+  // The arrays keep their capacity (reserved at creation), so they never
+  // move under a reader.
   c->replicas.resize(size_);
   c->locked.resize(size_);
   c->R -= 1;
@@ -2372,11 +2363,14 @@ int cbx_replica_release(cbx_context *c, int id) {
   TRY(check_replica_q(c, id, true));
   // modelmanager.c:200-204: unlock, then free the theta slot.  The reference
   // spins until the slot is BUSY; a slot nobody reserved is an error here.
+  // A slot cbx_del_model took out of the rotation (SKIP) while the task held
+  // it is still released: the delete waits for this unlock.
   std::atomic<int> &st = c->theta[id].state;
-  if (st.load(std::memory_order_acquire) != kThetaBusy)
+  if (st.load(std::memory_order_acquire) == kThetaFree)
     return fail(CBX_ERR_STATE, "replica %d was not reserved (cbx_acquire_access)", id);
   pthread_mutex_unlock(&c->replicas[id]->lock);
-  st.store(kThetaFree, std::memory_order_release);
+  int busy = kThetaBusy;
+  st.compare_exchange_strong(busy, kThetaFree, std::memory_order_acq_rel);
   return CBX_OK;
 }
 
@@ -2704,7 +2698,7 @@ int cbx_set_apply_kernel_config(cbx_context *c, int block, int unroll, int waves
 
 int cbx_set_pipeline_mode(cbx_context *c, int mode) {
   TRY(check_ctx(c));
-  if (mode < 0 || mode > 2) return fail(CBX_ERR_INVALID, "pipeline mode must be 0, 1 or 2");
+  if (mode < 0 || mode > 1) return fail(CBX_ERR_INVALID, "pipeline mode must be 0 or 1");
   c->pipeline_mode = mode;
   return CBX_OK;
 }

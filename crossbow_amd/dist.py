@@ -56,8 +56,8 @@ def max_over_ranks(value: float, world: int) -> float:
     return float(t.item())
 
 
-def tune_buckets(gpu, n: int, world: int, step: Callable[[], None], candidates=(1, 2, 4, 8, 16),
-                 steps: int = 10, warmup: int = 2, modes=(0, 1, 2), strides=(1, 2, 4), passes: int = 2,
+def tune_buckets(gpu, n: int, world: int, step: Callable[[], None], candidates=(1, 2, 4, 8),
+                 steps: int = 10, warmup: int = 2, modes=(0, 1), strides=(1, 2, 4), passes: int = 2,
                  group_candidates=(2, 4)):
     """Pick the bucket count of the G > 1 pipeline (kernel A / RCCL
     all-reduce / kernel B per bucket) by timing each candidate on the live
@@ -71,14 +71,22 @@ def tune_buckets(gpu, n: int, world: int, step: Callable[[], None], candidates=(
     Every rank times every candidate, the times are max-reduced over ranks,
     and all ranks take the same argmin, so the RCCL call sequence stays
     identical on every rank.  ``step()`` runs one barrier step.
-    With more than one bucket each count is also timed in every pipeline
-    mode (``gpu.set_pipeline_mode``: 0 within a step, 1 across steps, 2 across
-    steps with kernel B on the all-reduce's stream), and modes 1/2 with each
-    cross-step wait stride below the bucket count (``gpu.set_cross_wait_stride``).
-    The candidates are timed in ``passes`` interleaved passes and each keeps
-    its best pass, so one noisy sample (a few percent on one GPU) does not
-    decide.  Returns (bucket_elements, mode, stride, {key: ms_per_step}) with
-    keys "<buckets>/<mode>" for stride 1 and "<buckets>/<mode>/s<stride>".
+
+    The search keeps only the knobs the one-GPU A/B data showed to matter by
+    more than 2 %: 1/2/4/8 buckets (16 was slower than 8 everywhere,
+    profiles/r01/bench_force_split_tuned.json), pipeline mode 0 (within a
+    step) and 1 (across steps, ``gpu.set_pipeline_mode``), mode 1 at each
+    cross-step wait stride below the bucket count (``gpu.set_cross_wait_stride``,
+    3-6 % at 8 buckets, profiles/r01/cross_wait_stride_ab.json), then the
+    all-reduce grouping of the winner (``gpu.set_allreduce_group``, 4-9 % in
+    mode 0, profiles/r01/allreduce_group_ab.json).  The group is reset to 1
+    first, so an earlier setting never skews the sweep.  Candidates are timed
+    in ``passes`` interleaved passes and each keeps its best pass, so one
+    noisy sample (a few percent on one GPU) does not decide.
+
+    Returns (bucket_elements, mode, stride, group, {key: ms_per_step}) with
+    keys "<buckets>/<mode>" for stride 1, "<buckets>/<mode>/s<stride>", and
+    "<key of the winner>/g<group>".
     """
     import time
 
@@ -87,6 +95,18 @@ def tune_buckets(gpu, n: int, world: int, step: Callable[[], None], candidates=(
             return [(0, 1)]
         return [(m, s) for m in modes for s in ((1,) if m == 0 else strides) if s == 1 or s < nb]
 
+    def timed_steps():
+        for _ in range(warmup):
+            step()
+        gpu.wait()
+        barrier(world)
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            step()
+        gpu.wait()
+        return max_over_ranks((time.perf_counter() - t0) * 1e3 / steps, world)
+
+    gpu.set_allreduce_group(1)
     results = {}
     for _ in range(max(1, passes)):
         for nb in candidates:
@@ -95,15 +115,7 @@ def tune_buckets(gpu, n: int, world: int, step: Callable[[], None], candidates=(
                 gpu.set_bucket_elements(elems)
                 gpu.set_pipeline_mode(mode)
                 gpu.set_cross_wait_stride(stride)
-                for _ in range(warmup):
-                    step()
-                gpu.wait()
-                barrier(world)
-                t0 = time.perf_counter()
-                for _ in range(steps):
-                    step()
-                gpu.wait()
-                ms = max_over_ranks((time.perf_counter() - t0) * 1e3 / steps, world)
+                ms = timed_steps()
                 key = (nb, mode, stride)
                 results[key] = min(ms, results.get(key, ms))
     best = min(results, key=lambda k: (results[k], k))
@@ -113,30 +125,23 @@ def tune_buckets(gpu, n: int, world: int, step: Callable[[], None], candidates=(
     gpu.set_pipeline_mode(mode)
     gpu.set_cross_wait_stride(stride)
     out = {tuning_key(*k): v for k, v in results.items()}
-    # Then the all-reduce grouping of the winner (gpu.set_allreduce_group):
-    # fewer comm-stream waits, later all-reduce starts.  On one GPU groups of
-    # 2-4 cut 8-16-bucket mode-0 steps by 4-9 % (profiles/r01/allreduce_group_ab.json);
-    # over xGMI the later start may cost more than the waits save, so it is timed.
+    # Then the all-reduce grouping of the winner: fewer comm-stream waits,
+    # later all-reduce starts.  Over xGMI the later start may cost more than
+    # the waits save, so it is timed, not assumed.
+    group = 1
     groups = [grp for grp in group_candidates if 1 < grp < nb]
     if groups:
         timed = {1: results[best]}
         for _ in range(max(1, passes)):
             for grp in groups:
                 gpu.set_allreduce_group(grp)
-                for _ in range(warmup):
-                    step()
-                gpu.wait()
-                barrier(world)
-                t0 = time.perf_counter()
-                for _ in range(steps):
-                    step()
-                gpu.wait()
-                ms = max_over_ranks((time.perf_counter() - t0) * 1e3 / steps, world)
+                ms = timed_steps()
                 timed[grp] = min(ms, timed.get(grp, ms))
         for grp in groups:
             out[tuning_key(nb, mode, stride) + f"/g{grp}"] = timed[grp]
-        gpu.set_allreduce_group(min(timed, key=lambda g: (timed[g], g)))
-    return elems, mode, stride, out
+        group = min(timed, key=lambda g: (timed[g], g))
+    gpu.set_allreduce_group(group)
+    return elems, mode, stride, group, out
 
 
 def tuning_key(nb: int, mode: int, stride: int = 1) -> str:

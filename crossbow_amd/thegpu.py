@@ -387,11 +387,11 @@ class TheGPU:
         check(self._L.cbx_set_apply_kernel_config(self._ctx, block, unroll, waves_per_cu))
 
     def set_pipeline_mode(self, mode: int) -> None:
-        """0: buckets overlap within a step; 1: also across steps; 2: as 1, kernel B on the all-reduce stream."""
+        """0: buckets overlap within a step; 1: also across steps."""
         check(self._L.cbx_set_pipeline_mode(self._ctx, mode))
 
     def set_cross_wait_stride(self, stride: int) -> None:
-        """Modes 1/2: buckets per cross-step wait of kernel A on last step's kernel B."""
+        """Mode 1: buckets per cross-step wait of kernel A on last step's kernel B."""
         check(self._L.cbx_set_cross_wait_stride(self._ctx, stride))
 
     def set_allreduce_group(self, group: int) -> None:

@@ -342,12 +342,10 @@ int cbx_set_bucket_elements (cbx_context *ctx, long long bucket_elements);
  * stream and A(k) waits only for B(k) of the previous step, so the next
  * step's first buckets run while this step's last all-reduces are on the
  * link.  Any other C-ABI call between two steps that may enqueue device
- * work makes the next step join the whole sync stream first.  2 as 1, but
- * kernel B(k) runs on the all-reduce's stream right behind AR(k) (no event
- * between them; the sync stream joins once, after the last B).  Same
- * results bit for bit in every mode.                                      */
+ * work makes the next step join the whole sync stream first.  Same results
+ * bit for bit in both modes.                                              */
 int cbx_set_pipeline_mode (cbx_context *ctx, int mode);
-/* Modes 1 and 2: kernel A(k) waits for kernel B of the previous step once
+/* Mode 1: kernel A(k) waits for kernel B of the previous step once
  * per `stride` buckets, on B(k + stride - 1), which implies the earlier
  * ones.  1 (default) waits per bucket; larger strides pay fewer
  * cross-queue waits for less overlap between steps.  1..4096.            */

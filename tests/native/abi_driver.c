@@ -4,7 +4,9 @@
  * manager, BSP/SSP barriers, SMA / S-SGD / DEFAULT steps, the optimiser
  * step, pinned staging (serial and pipelined), checkpoint / override (with
  * batch-norm statistics),
- * autotune add / del, BN averaging, timing queries and teardown.
+ * autotune add / del (also while task threads reserve, lock and release
+ * replicas: the ids they hold may be deleted under them), BN averaging,
+ * timing queries and teardown.
  *
  * Built with host-side AddressSanitizer + UndefinedBehaviorSanitizer
  * (scripts/build_sanitized.sh: -Xarch_host -fsanitize=..., GPU code is not
@@ -13,6 +15,8 @@
  */
 #define _GNU_SOURCE
 #include <math.h>
+#include <pthread.h>
+#include <stdatomic.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -75,6 +79,59 @@ static int all_finite (const float *p, size_t n) {
 	for (size_t k = 0; k < n; ++k)
 		if (! isfinite (p[k])) return 0;
 	return 1;
+}
+
+/* Task threads against autotune: they reserve replicas through the theta
+ * queue (acquireAccess / upgradeAccess, getNextOrWait), lock, release, while
+ * the barrier thread adds and deletes one replica per device every step.
+ * Calls on a deleted id may fail; nothing may touch freed memory (ASan). */
+struct stress {
+	cbx_context *c;
+	atomic_int stop;
+	atomic_long tasks;
+};
+
+static void *stress_task (void *arg) {
+	struct stress *s = arg;
+	int k = 0;
+	while (! atomic_load (&s->stop)) {
+		int clock = -1, id;
+		if (k++ % 3 == 0) {
+			id = cbx_get_next_or_wait (s->c, 0);  /* reserve + lock */
+			if (id < 0) continue;
+		} else {
+			id = cbx_acquire_access (s->c, &clock);
+			if (id < 0) continue;
+			if (cbx_upgrade_access (s->c, id, &clock) != 1) continue;  /* deleted meanwhile */
+			if (cbx_replica_lock (s->c, id) < 0) continue;
+		}
+		(void) cbx_replica_task_done (s->c, id);
+		(void) cbx_replica_clock (s->c, id);
+		(void) cbx_replica_release (s->c, id);  /* unlock + free the slot; fails on a deleted id */
+		atomic_fetch_add (&s->tasks, 1);
+	}
+	return NULL;
+}
+
+static void stress_autotune (int n1, int n2) {
+	struct stress s;
+	s.c = setup (n1, n2, 2, CBX_SYNC_ASP, CBX_UPDATE_SMA, 0.9f);
+	atomic_init (&s.stop, 0);
+	atomic_init (&s.tasks, 0);
+	pthread_t th[3];
+	for (int t = 0; t < 3; ++t) EXPECT (pthread_create (&th[t], NULL, stress_task, &s) == 0);
+	for (int clock = 1; clock <= 24; ++clock) {
+		CHECK (cbx_lock_any (s.c));
+		CHECK (cbx_synchronise (s.c, 0, clock, clock % 2 ? 1 : -1, 0));  /* add, then delete */
+		CHECK (cbx_unlock_any (s.c));
+		usleep (200);
+	}
+	atomic_store (&s.stop, 1);
+	for (int t = 0; t < 3; ++t) EXPECT (pthread_join (th[t], NULL) == 0);
+	EXPECT (cbx_num_replicas (s.c) == 2);
+	EXPECT (atomic_load (&s.tasks) > 0);
+	CHECK (cbx_wait (s.c));
+	CHECK (cbx_free (s.c));
 }
 
 int main (void) {
@@ -183,12 +240,12 @@ int main (void) {
 	CHECK (cbx_synchronise_staged (c, 0, 2, 0, 3));
 	CHECK (cbx_unlock_any (c));
 	CHECK (cbx_set_pipeline_mode (c, 1));  /* across steps */
-	EXPECT (cbx_set_pipeline_mode (c, 3) == CBX_ERR_INVALID);
+	EXPECT (cbx_set_pipeline_mode (c, 2) == CBX_ERR_INVALID);
 	EXPECT (cbx_set_pipeline_mode (c, -1) == CBX_ERR_INVALID);
 	EXPECT (cbx_set_cross_wait_stride (c, 0) == CBX_ERR_INVALID);
 	for (int clock = 3; clock < 9; ++clock) {
 		if (clock == 5) CHECK (cbx_replica_set_copy (c, 1, 1));
-		if (clock == 6) CHECK (cbx_set_pipeline_mode (c, 2));  /* B behind its all-reduce */
+		if (clock == 6) CHECK (cbx_set_pipeline_mode (c, 0));  /* back to within-step buckets */
 		if (clock == 7) CHECK (cbx_set_cross_wait_stride (c, 3));
 		CHECK (cbx_lock_any (c));
 		CHECK (cbx_synchronise (c, 0, clock, 0, 0));
@@ -207,6 +264,8 @@ int main (void) {
 		EXPECT (all_finite (host, (size_t) n));
 		CHECK (cbx_free (c));
 	}
+
+	stress_autotune (n1, n2);
 
 	/* BN statistics averaging is a no-op with one device but walks its tables */
 	c = setup (n1, n2, 1, CBX_SYNC_BSP, CBX_UPDATE_SMA, 0.0f);

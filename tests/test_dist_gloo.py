@@ -224,7 +224,7 @@ class _FakeGpu:
         import time
         nb = 1 if self.elems >= self.n else -(-self.n // self.elems)
         # rank 0 is fastest at 8 buckets, rank 1 at 2; the max over ranks is lowest at 4
-        cost = {0: {1: 9, 2: 7, 4: 4, 8: 1, 16: 6}, 1: {1: 9, 2: 1, 4: 4, 8: 7, 16: 8}}[self.rank][nb]
+        cost = {0: {1: 9, 2: 7, 4: 4, 8: 1}, 1: {1: 9, 2: 1, 4: 4, 8: 7}}[self.rank][nb]
         cost += 2 if (self.mode >= 1 and self.rank == 1) else 0  # cross-step modes slower on rank 1
         cost += self.stride - 1  # and fewer cross-step waits slower everywhere
         cost += {0: -1, 1: 2}[self.rank] if self.group > 1 else 0  # grouping helps rank 0 only: max says no
@@ -240,8 +240,9 @@ def _tune_main(rank, world, port, q):
         from crossbow_amd import dist as D
         D.init(world, rank, backend="gloo")
         g = _FakeGpu(rank, 1000)
-        elems, mode, stride, res = D.tune_buckets(g, 1000, world, g.step, steps=2, warmup=1)
-        q.put((rank, (elems, g.elems, mode, g.mode, stride, g.stride, g.group, sorted(res)), None))
+        g.group = 3  # a group left over from an earlier setting must not skew the sweep
+        elems, mode, stride, group, res = D.tune_buckets(g, 1000, world, g.step, steps=2, warmup=1)
+        q.put((rank, (elems, g.elems, mode, g.mode, stride, g.stride, group, g.group, sorted(res)), None))
         D.finalize(world)
     except Exception:  # pragma: no cover
         import traceback
@@ -271,12 +272,13 @@ def test_bucket_tuning_agrees_across_ranks():
                 p.kill()
     for rank in range(world):
         assert out[rank][1] is None, out[rank][1]
-    (e0, set0, m0, setm0, s0, sets0, g0, cands), (e1, set1, m1, setm1, s1, sets1, g1, _) = out[0][0], out[1][0]
+    (e0, set0, m0, setm0, s0, sets0, g0, setg0, cands), (e1, set1, m1, setm1, s1, sets1, g1, setg1, _) = \
+        out[0][0], out[1][0]
     assert e0 == e1 == set0 == set1 == 250, (out[0][0], out[1][0])
     assert m0 == m1 == setm0 == setm1 == 0
     assert s0 == s1 == sets0 == sets1 == 1
-    assert g0 == g1 == 1  # the all-reduce group of the winner, by the max over ranks
-    want = ["1/0"] + [f"{nb}/{m}" for nb in (2, 4, 8, 16) for m in (0, 1, 2)]
-    want += [f"{nb}/{m}/s{s}" for nb in (4, 8, 16) for m in (1, 2) for s in (2, 4) if s < nb]
+    assert g0 == g1 == setg0 == setg1 == 1  # the all-reduce group of the winner, by the max over ranks
+    want = ["1/0"] + [f"{nb}/{m}" for nb in (2, 4, 8) for m in (0, 1)]
+    want += [f"{nb}/1/s{s}" for nb in (4, 8) for s in (2, 4) if s < nb]
     want += ["4/0/g2"]  # groups 1 < g < buckets, timed for the winner only
     assert cands == sorted(want)

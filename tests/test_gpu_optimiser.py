@@ -282,7 +282,7 @@ def test_default_clock_loop_bitexact(momentum, on_torch_stream, aux):
         g.free()
 
 
-@pytest.mark.parametrize("pipeline", ["fused", "cross-step", "cross-step-bcomm"])
+@pytest.mark.parametrize("pipeline", ["fused", "cross-step", "cross-step-stride"])
 def test_threaded_clock_loop_bitexact(pipeline):
     # The clock loop with the reference's threading: one task thread per
     # replica, each on its own task (torch) stream, locking its replica,
@@ -303,7 +303,8 @@ def test_threaded_clock_loop_bitexact(pipeline):
         if pipeline.startswith("cross-step"):
             g.set_force_split(True)
             g.set_bucket_elements(8192)
-            g.set_pipeline_mode(2 if pipeline.endswith("bcomm") else 1)
+            g.set_pipeline_mode(1)
+            g.set_cross_wait_stride(2 if pipeline.endswith("stride") else 1)
         st = O.make_state(n, 1, R, alpha, momentum)
         upload(g, st)
         lasts = [np.zeros(n, np.float32) for _ in range(R)]

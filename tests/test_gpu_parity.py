@@ -650,7 +650,7 @@ def test_step_event_covers_the_step(mode, timing):
         g.free()
 
 
-@pytest.mark.parametrize("pipeline", ["fused", "cross-step", "cross-step-bcomm"])
+@pytest.mark.parametrize("pipeline", ["fused", "cross-step", "cross-step-stride"])
 def test_concurrent_task_threads_and_barrier(pipeline):
     # The reference's threading: task threads lock a replica,
     # run its optimiser step and release it, while the result-collector
@@ -678,7 +678,8 @@ def test_concurrent_task_threads_and_barrier(pipeline):
         if pipeline.startswith("cross-step"):  # kernels A across steps, racing the task threads' optimiser steps
             g.set_force_split(True)
             g.set_bucket_elements(16_384)
-            g.set_pipeline_mode(2 if pipeline.endswith("bcomm") else 1)
+            g.set_pipeline_mode(1)
+            g.set_cross_wait_stride(2 if pipeline.endswith("stride") else 1)
         g.fill_synthetic(3)
 
         def worker(k):
@@ -721,8 +722,8 @@ def test_concurrent_task_threads_and_barrier(pipeline):
 
 @pytest.mark.parametrize("momentum", [0.0, 0.9])
 @pytest.mark.parametrize("bucket", [65_536, 4096])
-@pytest.mark.parametrize("xmode,stride,group", [(1, 1, 1), (2, 1, 1), (1, 3, 1), (2, 2, 1), (1, 1, 2), (2, 3, 4)])
-def test_cross_step_pipeline(momentum, bucket, xmode, stride, group):
+@pytest.mark.parametrize("stride,group", [(1, 1), (2, 1), (3, 1), (2, 3), (1, 2), (3, 4)])
+def test_cross_step_pipeline(momentum, bucket, stride, group):
     # cbx_set_pipeline_mode(1): kernels A on their own stream, each waiting
     # only for B of the same bucket in the previous step.  Eight steps with
     # Phase D requests, SSP holds, a host write between two steps (which
@@ -735,13 +736,13 @@ def test_cross_step_pipeline(momentum, bucket, xmode, stride, group):
     try:
         g.set_force_split(True)
         g.set_bucket_elements(bucket)
-        g.set_pipeline_mode(xmode)
+        g.set_pipeline_mode(1)
         g.set_cross_wait_stride(stride)
         g.set_allreduce_group(group)  # all-reduces per comm-stream wait; mode 0 steps use it too
         upload(g, st)
         want = st.clone()
-        plan = [{}, {"copy": 1}, {"hold": 2}, {}, {"write": 0}, {"mode": 0}, {"mode": xmode, "copy": 2, "hold": 0},
-                {"mode": 3 - xmode}, {"mode": xmode}]
+        plan = [{}, {"copy": 1}, {"hold": 2}, {}, {"write": 0}, {"mode": 0}, {"mode": 1, "copy": 2, "hold": 0},
+                {"mode": 0}, {"mode": 1}]
         for step, p in enumerate(plan):
             want.locked[:] = 1
             if "mode" in p:
@@ -807,7 +808,7 @@ def test_cross_step_pipeline_randomised_long_run():
             elif u < 0.26:
                 g.set_bucket_elements(rng.choice([4096, 16_384, 65_536, 1 << 40]))
             elif u < 0.30:
-                g.set_pipeline_mode(rng.choice([0, 1, 2]))
+                g.set_pipeline_mode(rng.choice([0, 1]))
                 g.set_cross_wait_stride(rng.choice([1, 2, 3, 8]))
                 g.set_allreduce_group(rng.choice([1, 1, 2, 5]))
             g.lockAny()
