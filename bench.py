@@ -314,17 +314,29 @@ def main():
     }
     kname = "sma_fused_kernel" if not split else "sma_accumulate_kernel"
     achieved = kernel_bytes / (kern_ms * 1e-3) / 1e9
-    traffic = None
+    traffic, traffic_note = None, None
     try:
+        from crossbow_amd.build import code_object_digest
+        running = code_object_digest(_lib.LIB_PATH)
         with open(args.traffic_json) as f:
             tj = json.load(f)
         key = f"{kname}/{args.model}/R{args.replicas}/m{1 if args.momentum > 0 else 0}"
-        traffic = tj.get(key, {}).get("hbm_bytes_per_launch")
-    except (OSError, ValueError):
-        pass
+        entry = tj.get(key)
+        if entry is None:
+            traffic_note = f"no PMC measurement for {key} in {os.path.relpath(args.traffic_json, ROOT)}"
+        elif entry.get("code_object_sha256") != running:
+            # a measurement of another build of the kernels says nothing about this one
+            traffic_note = (f"stale: measured on code object {str(entry.get('code_object_sha256'))[:12]}, "
+                            f"running {running[:12]}; re-run scripts/gpu_pmc.sh")
+        else:
+            traffic = entry.get("hbm_bytes_per_launch")
+            traffic_note = (f"PMC FETCH_SIZE x2 + WRITE_SIZE, separate passes, of this code object "
+                            f"({running[:12]}); traffic / alg = {traffic / kernel_bytes:.4f}")
+    except (OSError, ValueError) as e:
+        traffic_note = f"unavailable: {e}"
     result["roofline"] = {"bound": "hbm", "kernel": kname, "achieved": round(achieved, 1),
                           "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                          "traffic": traffic, "alg_bytes_per_launch": kernel_bytes,
+                          "traffic": traffic, "traffic_note": traffic_note, "alg_bytes_per_launch": kernel_bytes,
                           "launch_ms_mean": round(kern_ms, 4), "launch_ms_median": round(statistics.median(kern), 4),
                           "launches": len(kern),
                           "timed_in": "timed region" if not split else "calibration steps (one bucket, in order)"}
@@ -370,22 +382,34 @@ def main():
                 "d2h_GBs": round(d2h / (t[_lib.T_D2H] * 1e-3) / 1e9, 2),
                 "end_to_end_GBs": round(step_bytes / tot / 1e9, 2),
             }
-            # The same step through cbx_synchronise_staged: uploads, kernels and
-            # downloads pipelined over buckets on three streams.
-            piped = []
-            for _ in range(3):
-                clock += 1
-                gpu.lockAny()
-                gpu.synchronise_staged(0, clock, 0, args.staged_buckets)
-                gpu.unlockAny()
-                gpu.wait()
-                piped.append(gpu.last_timing(0))
-            p = sorted(piped, key=lambda x: x[_lib.T_STEP])[1]
+            # The same step through cbx_synchronise_staged, both staging modes:
+            # DMA (uploads, kernels and downloads pipelined over buckets on
+            # three streams) and zero-copy (the kernels read and write the
+            # pinned mirror over PCIe themselves; the library default).
+            def staged(mode):
+                nonlocal clock
+                gpu.set_staging_mode(mode)
+                runs = []
+                for _ in range(3):
+                    clock += 1
+                    gpu.lockAny()
+                    gpu.synchronise_staged(0, clock, 0, args.staged_buckets)
+                    gpu.unlockAny()
+                    gpu.wait()
+                    runs.append(gpu.last_timing(0))
+                return sorted(runs, key=lambda x: x[_lib.T_STEP])[1]
+            p = staged(_lib.STAGING_DMA)
             result["host_staged"]["pipelined"] = {
                 "buckets": args.staged_buckets, "step_ms": round(p[_lib.T_STEP], 3),
                 "h2d_ms": round(p[_lib.T_H2D], 3), "d2h_ms": round(p[_lib.T_D2H], 3),
                 "end_to_end_GBs": round(step_bytes / (p[_lib.T_STEP] * 1e-3) / 1e9, 2),
                 "timed": "HIP events: sync stream at entry to sync stream after the last download"}
+            z = staged(_lib.STAGING_ZEROCOPY)
+            result["host_staged"]["zerocopy"] = {
+                "step_ms": round(z[_lib.T_STEP], 3),
+                "end_to_end_GBs": round(step_bytes / (z[_lib.T_STEP] * 1e-3) / 1e9, 2),
+                "pcie_GBs_both_ways": round((h2d + d2h) / (z[_lib.T_STEP] * 1e-3) / 1e9, 2),
+                "timed": "HIP events on the fused staged kernel's own dispatch (one launch: host in, host + device out)"}
         if not args.no_cpu_baseline:
             # multithreaded first: OpenBLAS's pool must not start out bound to core 0
             threads = max(1, min(16, len(os.sched_getaffinity(0))))

@@ -63,6 +63,33 @@ def build_lib(force: bool = False, verbose: bool = False) -> str:
     return LIB
 
 
+def code_object_digest(path: str = LIB) -> str:
+    """sha256 of the library's device code (its ``.hip_fatbin`` section: the
+    gfx950 code objects of every kernel).  profiles/traffic.json stores it
+    with each PMC measurement, and bench.py reports a measured HBM traffic
+    only for the code object that is running (else null, with the reason)."""
+    import hashlib
+    import struct
+    with open(path, "rb") as f:
+        elf = f.read()
+    if elf[:4] != b"\x7fELF" or elf[4] != 2:
+        raise ValueError(f"{path}: not an ELF64 file")
+    shoff, = struct.unpack_from("<Q", elf, 0x28)
+    shentsize, shnum, shstrndx = struct.unpack_from("<HHH", elf, 0x3A)
+
+    def section(i):
+        name, _, _, _, off, size = struct.unpack_from("<IIQQQQ", elf, shoff + i * shentsize)
+        return name, off, size
+
+    _, stroff, _ = section(shstrndx)
+    for i in range(shnum):
+        name, off, size = section(i)
+        end = elf.index(b"\0", stroff + name)
+        if elf[stroff + name:end] == b".hip_fatbin":
+            return hashlib.sha256(elf[off:off + size]).hexdigest()
+    raise ValueError(f"{path}: no .hip_fatbin section")
+
+
 def find_jni_include():
     cands = []
     jh = os.environ.get("JAVA_HOME")

@@ -312,6 +312,8 @@ struct cbx_context {
   int cross_wait_stride = 1;  // mode 1: buckets per cross-step wait
   int allreduce_group = 1;     // pipelined split path: buckets per comm-stream wait
   int allreduce_algo = CBX_ALLREDUCE_RCCL;
+  int staging_mode = CBX_STAGING_ZEROCOPY;  // cbx_synchronise_staged: zero-copy kernels or DMA copies
+  cbx::LaunchConfig staged_cfg = cbx::staged_launch_config();
   bool peer_ready = false;     // hipDeviceEnablePeerAccess done between every pair of devices
   // Bumped by every C-ABI call that may enqueue work on a sync stream other
   // than the barrier path itself: a cross-step pipelined step then joins the
@@ -1008,6 +1010,163 @@ int stage_range(cbx_context *c, void *dst, const void *src, int64_t start4, int6
   return CBX_OK;
 }
 
+// The same staged step through zero-copy kernels (staging mode ZEROCOPY,
+// sma_internal.h StagedArgs): the kernels read z, last, s_i, w_i from the
+// pinned host mirror and write w_i, z, last to it and to the device, so the
+// link carries each byte once and both directions at once, with no copy
+// engine and no copy call per buffer and bucket.  G = 1: one fused launch.
+// G > 1 (or forced split), per bucket k:
+//   stream      : A(k) A(k+1) ...                         (reads the host)
+//   comm_stream : [wait A(k)] AR(k) B(k) [wait A(k+1)] ... (writes the host)
+// so kernel B of bucket k writes back over PCIe while kernel A of bucket k+1
+// reads.  Replicas outside the step (not locked, or below `first`) are
+// staged in by copy, as cbx_stage_in would.
+int sma_step_staged_zerocopy(cbx_context *c, int first, int buckets, std::vector<cbx::SmaArgs> &args,
+                             int copies_total, bool mom) {
+  const bool fused = c->G == 1 && !c->force_split;
+  const int64_t pad = cbx::kPadFloat4;
+  int64_t b4 = c->n4;
+  if (!fused) {
+    b4 = ((c->n4 / buckets + pad - 1) / pad) * pad;
+    if (b4 <= 0 || b4 > c->n4) b4 = c->n4;
+  }
+  const int64_t nb = (c->n4 + b4 - 1) / b4;
+  std::vector<cbx::StagedArgs> sa(c->devs.size());
+  for (size_t k = 0; k < c->devs.size(); ++k) {
+    Device &d = c->devs[k];
+    const cbx::SmaArgs &a = args[k];
+    cbx::StagedArgs &x = sa[k];
+    std::memset(&x, 0, sizeof(x));
+    int r = 0;
+    HIP_TRY(hipSetDevice(d.hip_id));
+    for (int id : d.replicas) {
+      Replica &rep = *c->replicas[id];
+      if (id < first || !c->locked[id]) {
+        // not in the step: its inputs still reach the device (cbx_stage_in)
+        const size_t bytes = (size_t)c->n * 4;
+        HIP_TRY(hipMemcpyAsync(replica_dev(d, rep, CBX_BUF_DIFF), replica_host(d, rep, CBX_BUF_DIFF), bytes,
+                               hipMemcpyHostToDevice, d.stream));
+        HIP_TRY(hipMemcpyAsync(replica_dev(d, rep, CBX_BUF_DATA), replica_host(d, rep, CBX_BUF_DATA), bytes,
+                               hipMemcpyHostToDevice, d.stream));
+        continue;
+      }
+      x.sh[r] = reinterpret_cast<const cbx::v4f *>(replica_host(d, rep, CBX_BUF_DIFF));
+      x.wh[r] = reinterpret_cast<cbx::v4f *>(replica_host(d, rep, CBX_BUF_DATA));
+      x.sd[r] = const_cast<cbx::v4f *>(a.s[r]);
+      x.wd[r] = a.w[r];
+      ++r;
+    }
+    x.nrep = a.nrep;
+    x.zh = reinterpret_cast<cbx::v4f *>(base_host(d, CBX_BUF_DATA));
+    x.zd = a.z;
+    if (c->has_last) {
+      x.lh = reinterpret_cast<cbx::v4f *>(base_host(d, CBX_BUF_LAST));
+      x.ld = a.last;
+      if (!mom) {  // `last` exists but is not part of the step: staged in by copy
+        HIP_TRY(hipMemcpyAsync(x.ld, x.lh, (size_t)c->n * 4, hipMemcpyHostToDevice, d.stream));
+      }
+    }
+    x.acc = a.acc;
+    x.D = a.D;
+    x.ctrl_out = a.ctrl_out;
+    x.ctrl_in = a.ctrl_in;
+    x.alpha = a.alpha;
+    x.copies = a.copies;
+  }
+  auto at = [&](const cbx::StagedArgs &x, int64_t s4, int64_t l4) {
+    cbx::StagedArgs y = x;
+    for (int r = 0; r < x.nrep; ++r) {
+      y.sh[r] = x.sh[r] + s4;
+      y.sd[r] = x.sd[r] + s4;
+      y.wh[r] = x.wh[r] + s4;
+      y.wd[r] = x.wd[r] + s4;
+    }
+    y.zh = x.zh + s4;
+    y.zd = x.zd + s4;
+    if (x.lh) {
+      y.lh = x.lh + s4;
+      y.ld = x.ld + s4;
+    }
+    y.acc = x.acc + s4;
+    y.D = x.D + s4;
+    y.n4 = l4;
+    return y;
+  };
+  for (Device &d : c->devs) {
+    HIP_TRY(hipSetDevice(d.hip_id));
+    d.ev_valid[EV_H2D0] = d.ev_valid[EV_H2D1] = d.ev_valid[EV_D2H0] = d.ev_valid[EV_D2H1] = false;
+    if (!fused) {
+      while ((int64_t)d.bucket_acc.size() < nb) {
+        hipEvent_t ea, er, eb;
+        HIP_TRY(hipEventCreate(&ea));
+        HIP_TRY(hipEventCreateWithFlags(&er, hipEventDisableTiming));
+        HIP_TRY(hipEventCreate(&eb));
+        d.bucket_acc.push_back(ea);
+        d.bucket_red.push_back(er);
+        d.bucket_b.push_back(eb);
+      }
+    }
+  }
+  if (fused) {
+    Device &d = c->devs[0];
+    HIP_TRY(hipSetDevice(d.hip_id));
+    cbx::LaunchConfig cfg = c->staged_cfg;
+    cfg.num_cus = d.num_cus;
+    sa[0].n4 = c->n4;
+    HIP_TRY(cbx::launch_sma_fused_staged(sa[0], mom, copies_total > 0, cfg, d.stream,
+                                         {ring_event(c, d, EV_START), step_stop_event(c, d, EV_B)}));
+    ring_advance(c, d, 2);
+    c->last_step_split = false;
+    return CBX_OK;
+  }
+  for (int64_t b = 0; b < nb; ++b) {
+    const int64_t s4 = b * b4, l4 = std::min(b4, c->n4 - s4);
+    for (size_t k = 0; k < c->devs.size(); ++k) {
+      Device &d = c->devs[k];
+      HIP_TRY(hipSetDevice(d.hip_id));
+      cbx::LaunchConfig cfg = c->staged_cfg;
+      cfg.num_cus = d.num_cus;
+      cbx::Timing t;
+      if (b == 0) t.start = ring_event(c, d, EV_START);
+      t.stop = d.bucket_acc[b];
+      HIP_TRY(cbx::launch_sma_accumulate_staged(at(sa[k], s4, l4), b == 0, cfg, d.stream, t));
+      HIP_TRY(hipStreamWaitEvent(d.comm_stream, d.bucket_acc[b], 0));
+    }
+    NCCL_TRY(ncclGroupStart());
+    for (Device &d : c->devs) {
+      HIP_TRY(hipSetDevice(d.hip_id));
+      const float *src = base_dev(c, d, CBX_BUF_GRADIENT) + s4 * 4;
+      float *dst = base_dev(c, d, CBX_BUF_DIFF) + s4 * 4;
+      size_t count = (size_t)l4 * 4;
+      if (b == 0) {  // the control block rides with bucket 0 (common.c:45-52 + sma.c:113-120)
+        src -= cbx::kCtrlFloats;
+        dst -= cbx::kCtrlFloats;
+        count += cbx::kCtrlFloats;
+      }
+      NCCL_TRY(ncclAllReduce(src, dst, count, ncclFloat, ncclSum, d.comm, d.comm_stream));
+    }
+    NCCL_TRY(ncclGroupEnd());
+    for (size_t k = 0; k < c->devs.size(); ++k) {
+      Device &d = c->devs[k];
+      HIP_TRY(hipSetDevice(d.hip_id));
+      cbx::LaunchConfig cfg = c->staged_cfg;
+      cfg.num_cus = d.num_cus;
+      cbx::Timing t;
+      if (b == nb - 1) t.stop = d.bucket_b[b];
+      HIP_TRY(cbx::launch_sma_apply_staged(at(sa[k], s4, l4), mom, cfg, d.comm_stream, t));
+    }
+  }
+  for (Device &d : c->devs) {
+    HIP_TRY(hipSetDevice(d.hip_id));
+    HIP_TRY(hipStreamWaitEvent(d.stream, d.bucket_b[nb - 1], 0));  // the step ends on the sync stream
+    TRY(mark(c, d, EV_B));
+    ring_advance(c, d, 2);
+    d.cross_valid = false;
+  }
+  c->last_step_split = true;
+  return CBX_OK;
+}
+
 int sma_step_staged(cbx_context *c, int first, int buckets) {
   const bool mom = c->has_last && c->model.conf.momentum > 0;  // sma.c:150
   std::vector<cbx::SmaArgs> args(c->devs.size());
@@ -1019,6 +1178,16 @@ int sma_step_staged(cbx_context *c, int first, int buckets) {
   }
   TRY(ensure_one_rank_comm(c));
   TRY(alloc_host_mirror(c));
+  if (c->staging_mode == CBX_STAGING_ZEROCOPY) {
+    TRY(sma_step_staged_zerocopy(c, first, buckets, args, copies_total, mom));
+    TRY(finish_step(c));
+    for (Device &d : c->devs)
+      for (int id : d.replicas) {
+        if (id < first || !c->locked[id]) continue;
+        c->replicas[id]->conf.copy = 0;  // sma.c:220
+      }
+    return CBX_OK;
+  }
   const bool fused = c->G == 1 && !c->force_split;
   const int64_t pad = cbx::kPadFloat4;
   int64_t b4 = ((c->n4 / buckets + pad - 1) / pad) * pad;
@@ -1295,15 +1464,18 @@ int load_buffer(float *dev, size_t bytes, const std::string &path, std::vector<c
 int alloc_host_mirror(cbx_context *c) {
   for (Device &d : c->devs) {
     HIP_TRY(hipSetDevice(d.hip_id));
+    // Coherent (fine-grained) pinned memory: the zero-copy staged kernels
+    // read and write it over PCIe, and the host reads / writes it between
+    // steps, so no GPU cache may hold a stale line of it.
     if (!d.host) {
-      HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&d.host), d.arena_bytes, hipHostMallocDefault));
+      HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&d.host), d.arena_bytes, hipHostMallocCoherent));
       std::memset(d.host, 0, d.arena_bytes);
     }
     d.extra_host.resize(d.extra.size(), nullptr);
     for (size_t k = 0; k < d.extra.size(); ++k) {
       if (!d.extra[k] || d.extra_host[k]) continue;
       const size_t bytes = d.stride * kReplicaSlots;
-      HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&d.extra_host[k]), bytes, hipHostMallocDefault));
+      HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&d.extra_host[k]), bytes, hipHostMallocCoherent));
       std::memset(d.extra_host[k], 0, bytes);
     }
   }
@@ -2726,6 +2898,14 @@ int cbx_set_allreduce_algorithm(cbx_context *c, int algorithm) {
   if (algorithm == CBX_ALLREDUCE_PEER && c->G > cbx::kMaxDevices)
     return fail(CBX_ERR_UNSUPPORTED, "the peer-read all-reduce takes at most %d devices", cbx::kMaxDevices);
   c->allreduce_algo = algorithm;
+  return CBX_OK;
+}
+
+int cbx_set_staging_mode(cbx_context *c, int mode) {
+  TRY(check_ctx(c));
+  if (mode != CBX_STAGING_ZEROCOPY && mode != CBX_STAGING_DMA)
+    return fail(CBX_ERR_INVALID, "staging mode must be CBX_STAGING_ZEROCOPY or CBX_STAGING_DMA");
+  c->staging_mode = mode;
   return CBX_OK;
 }
 

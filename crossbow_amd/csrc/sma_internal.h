@@ -99,6 +99,17 @@ inline LaunchConfig sma_apply_launch_config() {
   c.waves_per_cu = -1;
   return c;
 }
+// The zero-copy staged kernels (PCIe-bound): one-wave blocks, two float4 per
+// lane, a grid-stride loop over 4 blocks per CU, uncapped (scripts/pcie_bench.hip:
+// the link saturates with a few hundred blocks in flight).
+inline LaunchConfig staged_launch_config() {
+  LaunchConfig c;
+  c.block = 64;
+  c.unroll = 2;
+  c.blocks_per_cu = 4;
+  c.waves_per_cu = 0;
+  return c;
+}
 inline LaunchConfig ssgd_apply_launch_config() {
   LaunchConfig c;
   c.block = 64;
@@ -170,6 +181,42 @@ hipError_t launch_sma_accumulate(const SmaArgs &a, bool write_ctrl,
 // Multi-GPU kernel B: Phase C (+ D, gated by the reduced control slot).
 hipError_t launch_sma_apply(const SmaArgs &a, bool momentum,
                             const LaunchConfig &cfg, hipStream_t stream, Timing t = {});
+// Host-staged step through zero-copy (cbx_synchronise_staged, staging mode
+// CBX_STAGING_ZEROCOPY): the kernels read their inputs straight from the
+// pinned host mirror over PCIe and write their outputs to the host mirror AND
+// the device buffers, so each byte crosses the link once, both directions at
+// once, with no DMA-engine copies and no per-bucket copy calls
+// (scripts/pcie_bench.hip: 1.84 GB up + 1.02 GB down in 34-35 ms through
+// kernels).  The device ends as cbx_stage_in + cbx_synchronise +
+// cbx_stage_out leave it: s_i staged in, w_i / z / last updated.
+struct StagedArgs {
+  const v4f *sh[kMaxReplicas];  // host s_i (read)
+  v4f *sd[kMaxReplicas];        // device s_i (written: the staged-in snapshot)
+  v4f *wh[kMaxReplicas];        // host w_i (read; written back)
+  v4f *wd[kMaxReplicas];        // device w_i (written)
+  v4f *zh, *zd;                 // base model: host (read; written back) / device
+  v4f *lh, *ld;                 // base momentum: host / device (may be null)
+  v4f *acc;                     // kernel A: Phase A output (device)
+  const v4f *D;                 // kernel B: all-reduced acc (device)
+  float *ctrl_out;              // kernel A: acc control block
+  const float *ctrl_in;         // kernel B: D control block
+  int64_t n4;
+  float alpha;
+  float copies;
+  int nrep;
+  int pad_;
+};
+// G = 1: Phase A + C (+ D) in one pass, host in, host and device out.
+hipError_t launch_sma_fused_staged(const StagedArgs &a, bool momentum, bool copy, const LaunchConfig &cfg,
+                                   hipStream_t stream, Timing t = {});
+// G > 1 kernel A: reads z, s_i, w_i from the host; writes s_i, w_i, z to the
+// device, w_i to the host, acc (and the control block) to the device.
+hipError_t launch_sma_accumulate_staged(const StagedArgs &a, bool write_ctrl, const LaunchConfig &cfg,
+                                        hipStream_t stream, Timing t = {});
+// G > 1 kernel B: reads D, z (device) and last (host); writes z, last to the
+// host and the device (and w_i to both on Phase D).
+hipError_t launch_sma_apply_staged(const StagedArgs &a, bool momentum, const LaunchConfig &cfg,
+                                   hipStream_t stream, Timing t = {});
 // Peer-read all-reduce of the single-process multi-device form (one process
 // drives every GPU, the reference's own form, executioncontext.c:185-201):
 // instead of an RCCL pass, kernels read the peers' buffers directly over

@@ -256,6 +256,175 @@ __global__ __launch_bounds__(256) void sma_apply_kernel(const SmaArgs a) {
 }
 
 // ---------------------------------------------------------------------------
+// Host-staged step through zero-copy (sma_internal.h, StagedArgs).  Same
+// arithmetic, in the same order, as the device-resident kernels above; host
+// memory is read and written with plain loads / stores (PCIe-bound: ~55 GB/s
+// each way), device memory with the nontemporal ones.
+// ---------------------------------------------------------------------------
+template <int R, bool MOM, bool COPY, int U>
+__global__ __launch_bounds__(256) void sma_fused_staged_kernel(const StagedArgs a) {
+  constexpr int RR = (R > 0) ? R : kChunk;
+  const uint32_t trip = gridDim.x * blockDim.x * U;
+  const uint32_t n4 = (uint32_t)a.n4;
+  const v4f al = a.alpha, nal = -a.alpha, mb = kBaseMomentum, one = 1.0f, mone = -1.0f;
+  for (uint32_t base = first_elem<U>(); base < n4; base += trip) {
+    v4f zv[U], lv[U], acc[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t i = (base + u * 64u) * 16u;
+      zv[u] = ldo<0>(a.zh, i);
+      if constexpr (MOM) lv[u] = ldo<0>(a.lh, i);
+      acc[u] = 0.0f;
+    }
+    const int nrep = (R >= 0) ? R : a.nrep;
+    for (int c = 0; c < nrep; c += RR) {
+      v4f sv[U][RR], wv[U][RR];
+#pragma unroll
+      for (int r = 0; r < RR; ++r) {
+        if (R < 0 && c + r >= nrep) break;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const uint32_t i = (base + u * 64u) * 16u;
+          sv[u][r] = ldo<0>(a.sh[c + r], i);
+          if constexpr (!COPY) wv[u][r] = ldo<0>(a.wh[c + r], i);
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int r = 0; r < RR; ++r) {
+        if (R < 0 && c + r >= nrep) break;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const uint32_t i = (base + u * 64u) * 16u;
+          sto<1>(a.sd[c + r], i, sv[u][r]);
+          const v4f d = vfma(mone, zv[u], sv[u][r]);
+          if constexpr (!COPY) {
+            wv[u][r] = vfma(nal, d, wv[u][r]);
+            sto<0>(a.wh[c + r], i, wv[u][r]);
+            sto<1>(a.wd[c + r], i, wv[u][r]);
+          }
+          acc[u] = vfma(al, d, acc[u]);
+        }
+      }
+      if constexpr (R >= 0) break;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t i = (base + u * 64u) * 16u;
+      v4f D = acc[u];
+      if constexpr (MOM) {
+        D = vfma(mb, lv[u], D);
+        sto<0>(a.lh, i, D);
+        sto<1>(a.ld, i, D);
+      }
+      zv[u] = vfma(one, D, zv[u]);
+      sto<0>(a.zh, i, zv[u]);
+      sto<1>(a.zd, i, zv[u]);
+    }
+    if constexpr (COPY) {
+      for (int r = 0; r < nrep; ++r) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          sto<0>(a.wh[r], (base + u * 64u) * 16u, zv[u]);
+          sto<1>(a.wd[r], (base + u * 64u) * 16u, zv[u]);
+        }
+      }
+    }
+  }
+}
+
+template <int R, int U>
+__global__ __launch_bounds__(256) void sma_accumulate_staged_kernel(const StagedArgs a) {
+  constexpr int RR = (R > 0) ? R : kChunk;
+  if (a.ctrl_out != nullptr && blockIdx.x == 0 && threadIdx.x < kCtrlFloats)
+    a.ctrl_out[threadIdx.x] = (threadIdx.x == 0) ? a.copies : 0.0f;
+  const uint32_t trip = gridDim.x * blockDim.x * U;
+  const uint32_t n4 = (uint32_t)a.n4;
+  const v4f al = a.alpha, nal = -a.alpha, mone = -1.0f;
+  for (uint32_t base = first_elem<U>(); base < n4; base += trip) {
+    v4f zv[U], acc[U];
+    const int nrep = (R >= 0) ? R : a.nrep;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t i = (base + u * 64u) * 16u;
+      acc[u] = 0.0f;
+      zv[u] = ldo<0>(a.zh, i);
+      sto<1>(a.zd, i, zv[u]);  // kernel B reads z from the device
+    }
+    for (int c = 0; c < nrep; c += RR) {
+      v4f sv[U][RR], wv[U][RR];
+#pragma unroll
+      for (int r = 0; r < RR; ++r) {
+        if (R < 0 && c + r >= nrep) break;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const uint32_t i = (base + u * 64u) * 16u;
+          sv[u][r] = ldo<0>(a.sh[c + r], i);
+          wv[u][r] = ldo<0>(a.wh[c + r], i);
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int r = 0; r < RR; ++r) {
+        if (R < 0 && c + r >= nrep) break;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const uint32_t i = (base + u * 64u) * 16u;
+          sto<1>(a.sd[c + r], i, sv[u][r]);
+          const v4f d = vfma(mone, zv[u], sv[u][r]);
+          wv[u][r] = vfma(nal, d, wv[u][r]);
+          sto<0>(a.wh[c + r], i, wv[u][r]);
+          sto<1>(a.wd[c + r], i, wv[u][r]);
+          acc[u] = vfma(al, d, acc[u]);
+        }
+      }
+      if constexpr (R >= 0) break;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) sto<1>(a.acc, (base + u * 64u) * 16u, acc[u]);
+  }
+}
+
+template <bool MOM, int U>
+__global__ __launch_bounds__(256) void sma_apply_staged_kernel(const StagedArgs a) {
+  const bool copy = a.ctrl_in[0] > 0.0f;
+  const uint32_t trip = gridDim.x * blockDim.x * U;
+  const uint32_t n4 = (uint32_t)a.n4;
+  const v4f mb = kBaseMomentum, one = 1.0f;
+  for (uint32_t base = first_elem<U>(); base < n4; base += trip) {
+    v4f Dv[U], zv[U], lv[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t i = (base + u * 64u) * 16u;
+      Dv[u] = ldo<1>(a.D, i);
+      zv[u] = ldo<1>(a.zd, i);
+      if constexpr (MOM) lv[u] = ldo<0>(a.lh, i);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t i = (base + u * 64u) * 16u;
+      if constexpr (MOM) {
+        Dv[u] = vfma(mb, lv[u], Dv[u]);
+        sto<0>(a.lh, i, Dv[u]);
+        sto<1>(a.ld, i, Dv[u]);
+      }
+      zv[u] = vfma(one, Dv[u], zv[u]);
+      sto<0>(a.zh, i, zv[u]);
+      sto<1>(a.zd, i, zv[u]);
+    }
+    if (copy) {
+      for (int r = 0; r < a.nrep; ++r) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          sto<0>(a.wh[r], (base + u * 64u) * 16u, zv[u]);
+          sto<1>(a.wd[r], (base + u * 64u) * 16u, zv[u]);
+        }
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Peer-read two-shot all-reduce (single process, G devices; sma_internal.h).
 // Reduce: this device's shard of D = sum over devices of acc, every load of a
 // trip (G streams, G-1 of them remote over xGMI) in flight before the adds.
@@ -693,7 +862,77 @@ hipError_t peer_apply_u(const SmaArgs &a, const PeerArgs &p, const LaunchConfig 
   return hipGetLastError();
 }
 
+// Zero-copy staged launches: PCIe-bound, so no occupancy cap (the cap keeps
+// DRAM pages few for the HBM-bound kernels; here the link is the limit and
+// more waves keep more host reads in flight).
+template <int R, bool MOM, bool COPY>
+hipError_t fused_staged_u(const StagedArgs &a, const LaunchConfig &cfg, hipStream_t s, Timing t) {
+  const dim3 g = grid_for(a.n4, cfg);
+  if (cfg.unroll == 2)
+    hipExtLaunchKernelGGL((sma_fused_staged_kernel<R, MOM, COPY, 2>), g, dim3(cfg.block), 0, s, t.start, t.stop, 0, a);
+  else
+    hipExtLaunchKernelGGL((sma_fused_staged_kernel<R, MOM, COPY, 1>), g, dim3(cfg.block), 0, s, t.start, t.stop, 0, a);
+  return hipGetLastError();
+}
+
+template <bool MOM, bool COPY>
+hipError_t fused_staged_r(const StagedArgs &a, const LaunchConfig &cfg, hipStream_t s, Timing t) {
+  switch (a.nrep) {
+    case 0: return fused_staged_u<0, MOM, COPY>(a, cfg, s, t);
+    case 1: return fused_staged_u<1, MOM, COPY>(a, cfg, s, t);
+    case 2: return fused_staged_u<2, MOM, COPY>(a, cfg, s, t);
+    case 4: return fused_staged_u<4, MOM, COPY>(a, cfg, s, t);
+    case 8: return fused_staged_u<8, MOM, COPY>(a, cfg, s, t);
+    default: return fused_staged_u<-1, MOM, COPY>(a, cfg, s, t);
+  }
+}
+
+template <int R>
+hipError_t acc_staged_u(const StagedArgs &a, const LaunchConfig &cfg, hipStream_t s, Timing t) {
+  const dim3 g = grid_for(a.n4, cfg);
+  if (cfg.unroll == 2)
+    hipExtLaunchKernelGGL((sma_accumulate_staged_kernel<R, 2>), g, dim3(cfg.block), 0, s, t.start, t.stop, 0, a);
+  else
+    hipExtLaunchKernelGGL((sma_accumulate_staged_kernel<R, 1>), g, dim3(cfg.block), 0, s, t.start, t.stop, 0, a);
+  return hipGetLastError();
+}
+
+template <bool MOM>
+hipError_t apply_staged_u(const StagedArgs &a, const LaunchConfig &cfg, hipStream_t s, Timing t) {
+  const dim3 g = grid_for(a.n4, cfg);
+  if (cfg.unroll == 2)
+    hipExtLaunchKernelGGL((sma_apply_staged_kernel<MOM, 2>), g, dim3(cfg.block), 0, s, t.start, t.stop, 0, a);
+  else
+    hipExtLaunchKernelGGL((sma_apply_staged_kernel<MOM, 1>), g, dim3(cfg.block), 0, s, t.start, t.stop, 0, a);
+  return hipGetLastError();
+}
+
 }  // namespace
+
+hipError_t launch_sma_fused_staged(const StagedArgs &a, bool momentum, bool copy, const LaunchConfig &cfg,
+                                   hipStream_t stream, Timing t) {
+  if (momentum) return copy ? fused_staged_r<true, true>(a, cfg, stream, t) : fused_staged_r<true, false>(a, cfg, stream, t);
+  return copy ? fused_staged_r<false, true>(a, cfg, stream, t) : fused_staged_r<false, false>(a, cfg, stream, t);
+}
+
+hipError_t launch_sma_accumulate_staged(const StagedArgs &a, bool write_ctrl, const LaunchConfig &cfg,
+                                        hipStream_t stream, Timing t) {
+  StagedArgs b = a;
+  if (!write_ctrl) b.ctrl_out = nullptr;
+  switch (b.nrep) {
+    case 0: return acc_staged_u<0>(b, cfg, stream, t);
+    case 1: return acc_staged_u<1>(b, cfg, stream, t);
+    case 2: return acc_staged_u<2>(b, cfg, stream, t);
+    case 4: return acc_staged_u<4>(b, cfg, stream, t);
+    case 8: return acc_staged_u<8>(b, cfg, stream, t);
+    default: return acc_staged_u<-1>(b, cfg, stream, t);
+  }
+}
+
+hipError_t launch_sma_apply_staged(const StagedArgs &a, bool momentum, const LaunchConfig &cfg, hipStream_t stream,
+                                   Timing t) {
+  return momentum ? apply_staged_u<true>(a, cfg, stream, t) : apply_staged_u<false>(a, cfg, stream, t);
+}
 
 hipError_t launch_sma_peer_reduce(const PeerArgs &p, const LaunchConfig &cfg, hipStream_t stream, Timing t) {
   if (p.G < 1 || p.G > kMaxDevices) return hipErrorInvalidValue;

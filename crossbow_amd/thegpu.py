@@ -402,6 +402,10 @@ class TheGPU:
         """ALLREDUCE_RCCL (default) or ALLREDUCE_PEER (one process over every device: peer reads over xGMI)."""
         check(self._L.cbx_set_allreduce_algorithm(self._ctx, algorithm))
 
+    def set_staging_mode(self, mode: int) -> None:
+        """synchronise_staged: STAGING_ZEROCOPY (kernels read / write the pinned mirror) or STAGING_DMA (copies)."""
+        check(self._L.cbx_set_staging_mode(self._ctx, mode))
+
     def set_bucket_elements(self, elements: int) -> None:
         check(self._L.cbx_set_bucket_elements(self._ctx, elements))
 

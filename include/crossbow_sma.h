@@ -374,6 +374,19 @@ int cbx_set_allreduce_group (cbx_context *ctx, int group);
 #define CBX_ALLREDUCE_RCCL 0
 #define CBX_ALLREDUCE_PEER 1
 int cbx_set_allreduce_algorithm (cbx_context *ctx, int algorithm);
+/* How cbx_synchronise_staged moves the model between the pinned host mirror
+ * and the device (north_star: the path starts and ends in host memory):
+ *   CBX_STAGING_ZEROCOPY (0, default): the SMA kernels read their inputs
+ *     from the host mirror over PCIe and write their outputs to it and to
+ *     the device, both link directions at once, no copy engine;
+ *   CBX_STAGING_DMA (1): copy-engine uploads and downloads per bucket on
+ *     their own streams, overlapping the kernels (databuffer.c:95-122 is the
+ *     reference's synchronous staging).
+ * Both leave host and device exactly as cbx_stage_in + cbx_synchronise +
+ * cbx_stage_out do.                                                        */
+#define CBX_STAGING_ZEROCOPY 0
+#define CBX_STAGING_DMA 1
+int cbx_set_staging_mode (cbx_context *ctx, int mode);
 /* Force the multi-GPU pipeline (kernel A + RCCL all-reduce + kernel B) even
  * at G = 1 (a one-rank communicator), so a single-GPU host exercises it.  */
 int cbx_set_force_split (cbx_context *ctx, int force);

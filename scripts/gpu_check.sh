@@ -17,10 +17,12 @@ run() {  # run <name> <seconds> cmd...
   return $rc
 }
 STEPS=${STEPS:-smoke,tests,bench,rocprof}
-[[ $STEPS == *smoke* ]] && { run smoke 300 python __graft_entry__.py --smoke || true; }
-[[ $STEPS == *tests* ]] && { run pytest_gpu 900 python -m pytest tests -m gpu -q -x -p no:cacheprovider || true; }
+[[ $STEPS == *smoke* ]] && { run smoke 300 python -c "import __graft_entry__ as e; e.smoke()" || true; }
+[[ $STEPS == *tests* ]] && { run pytest_gpu 900 python -u -m pytest tests -m gpu -v -x --timeout 120 --timeout-method thread -p no:cacheprovider || true; }
 [[ $STEPS == *bench* ]] && { run bench 600 python bench.py ${BENCH_ARGS:-} || true; }
 [[ $STEPS == *launcher* ]] && { run launcher 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29531 bench.py --gpus 1 --steps 10 --warmup 3 --no-cpu-baseline || true; }
 [[ $STEPS == *sweep* ]] && { run sweep 600 python scripts/sweep.py ${SWEEP_ARGS:-} || true; }
+[[ $STEPS == *pcie* ]] && { run pcie_bench 300 ./scripts/pcie_bench || true; }
+[[ $STEPS == *c2* ]] && { run c2_latency 300 rocprofv3 --kernel-trace --stats -d gpurun_out/c2prof -o run --output-format csv -- python3 scripts/c2_latency.py || true; }
 [[ $STEPS == *rocprof* ]] && { run rocprof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/rocprof -o run --output-format csv -- python3 bench.py --no-cpu-baseline --no-staged --no-copy-ceiling ${BENCH_ARGS:-} || true; }
 exit 0

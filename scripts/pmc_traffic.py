@@ -51,8 +51,15 @@ def main():
     p.add_argument("--key-suffix", required=True, help="e.g. resnet50/R8/m1 (matches bench.py)")
     p.add_argument("--alg-bytes", action="append", default=[],
                    help="KERNEL=BYTES algorithmic bytes per launch of KERNEL (repeatable), for the ratio")
+    p.add_argument("--lib", default=os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                                 "crossbow_amd", "libcrossbow_sma.so"),
+                   help="the library the PMC passes ran (its device-code digest is stored with each entry)")
     p.add_argument("dirs", nargs="+")
     a = p.parse_args()
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from crossbow_amd.build import code_object_digest
+    digest = code_object_digest(a.lib)
     vals = collect(a.dirs)
     kernels = sorted({k for k, _ in vals})
     out = {}
@@ -76,6 +83,7 @@ def main():
                 entry["alg_bytes_per_launch"] = float(alg[kern])
                 entry["traffic_over_alg"] = entry["hbm_bytes_per_launch"] / float(alg[kern])
         entry["correction"] = "read = 2*FETCH_SIZE KiB (gfx950 half-count of 16B/lane streams), write = WRITE_SIZE KiB"
+        entry["code_object_sha256"] = digest  # .hip_fatbin of the library that ran (crossbow_amd.build)
         out[f"{kern}/{a.key_suffix}"] = entry
     os.makedirs(os.path.dirname(os.path.abspath(a.out)), exist_ok=True)
     with open(a.out, "w") as f:

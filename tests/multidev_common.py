@@ -131,6 +131,7 @@ class Case:
     copy: Dict[int, int] = field(default_factory=dict)   # step -> replica asking for Phase D
     held: Dict[int, int] = field(default_factory=dict)   # step -> replica busy on the task side (SSP)
     staged: int = 0            # > 0: cbx_synchronise_staged over that many buckets
+    staging: int = 0           # cbx_set_staging_mode: 0 zero-copy kernels, 1 DMA copies
     utype: int = 7             # update model: 7 SMA, 3 SYNCHRONOUSEAMSGD, 1 WORKER (S-SGD)
     mode: int = 0              # cbx_set_pipeline_mode
     stride: int = 1            # cbx_set_cross_wait_stride
@@ -198,6 +199,7 @@ def run_case(g: Ctx, world: int, local: List[int], case: Case) -> dict:
     g("cbx_set_allreduce_group", case.group)
     if case.algo:
         g("cbx_set_allreduce_algorithm", case.algo)
+    g("cbx_set_staging_mode", case.staging)
     size = world * R
     assert g("cbx_num_replicas") == size and g("cbx_num_devices") == world
     mine = [i for i in range(size) if i % world in local]

@@ -169,3 +169,20 @@ def test_cpp_model_manager_policy(tmp_path):
     assert r.returncode == 0, r.stderr
     r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=60)
     assert r.returncode == 0 and "ok" in r.stdout, r.stdout + r.stderr
+
+
+def test_code_object_digest_ties_traffic_to_the_build():
+    # bench.py reports profiles/traffic.json's PMC bytes only for the code
+    # object they were measured on: the digest is the library's .hip_fatbin.
+    import json
+
+    from crossbow_amd import _lib
+    from crossbow_amd.build import code_object_digest
+    d = code_object_digest(_lib.LIB_PATH)
+    assert re.fullmatch(r"[0-9a-f]{64}", d)
+    assert code_object_digest(_lib.LIB_PATH) == d
+    with open(os.path.join(ROOT, "profiles", "traffic.json")) as f:
+        tj = json.load(f)
+    for key, entry in tj.items():
+        if key.startswith("sma_") and "code_object_sha256" in entry:
+            assert re.fullmatch(r"[0-9a-f]{64}", entry["code_object_sha256"]), key

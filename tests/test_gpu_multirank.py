@@ -44,7 +44,8 @@ CASES = [
     Case("sma-5-buckets-cross-stride", 300_007, 2, 0.9, 5, bucket=65_536, copy={2: 1}, held={3: 0}, mode=1,
          stride=2, group=3),
     Case("sma-no-momentum", 20_011, 1, 0.0, 2, bucket=4096, utype=3),
-    Case("sma-staged", 100_003, 2, 0.9, 2, copy={1: 2}, staged=3),
+    Case("sma-staged", 100_003, 2, 0.9, 3, copy={1: 2}, held={0: 3}, staged=3),  # zero-copy staging kernels
+    Case("sma-staged-dma", 100_003, 2, 0.9, 2, copy={0: 1}, held={1: 2}, staged=3, staging=1),
     Case("ssgd", 40_009, 2, 0.9, 2, utype=1),
     Case("ssgd-buckets", 40_009, 2, 0.9, 2, bucket=4096, utype=1),
     # RCCL's (ring) summation order: the stated tolerance and cross-rank identity

@@ -404,46 +404,65 @@ def test_staged_roundtrip():
         g.free()
 
 
-@pytest.mark.parametrize("n,buckets,split,copy_step", [
-    (4099, 1, False, None), (4099, 7, False, 1), (300_001, 16, False, None), (300_001, 4096, False, 0),
-    (300_001, 5, True, None), (300_001, 16, True, 1), (1_111_946, 16, False, None),
+@pytest.mark.parametrize("staging", ["zerocopy", "dma"])
+@pytest.mark.parametrize("n,buckets,split,copy_step,held,momentum", [
+    (4099, 1, False, None, None, 0.9), (4099, 7, False, 1, None, 0.9), (300_001, 16, False, None, 2, 0.9),
+    (300_001, 4096, False, 0, None, 0.9), (300_001, 5, True, None, None, 0.9), (300_001, 16, True, 1, 3, 0.9),
+    (1_111_946, 16, False, None, None, 0.9), (65_537, 3, True, 0, None, 0.0), (65_537, 1, False, None, 1, 0.0),
 ])
-def test_staged_pipelined(n, buckets, split, copy_step):
-    # cbx_synchronise_staged: host mirrors in, host mirrors out, uploads /
-    # kernels / downloads overlapped per bucket.  Two steps back to back: the
-    # second uploads what the first downloaded.  Bit-exact with the oracle.
+def test_staged_pipelined(staging, n, buckets, split, copy_step, held, momentum):
+    # cbx_synchronise_staged: host mirrors in, host mirrors out.  zerocopy: the
+    # kernels read / write the pinned mirror over PCIe themselves; dma: uploads /
+    # kernels / downloads overlapped per bucket.  Three steps back to back: each
+    # reads what the last wrote; a replica held by a task (SSP) stays out of
+    # one step but is still staged in.  Bit-exact with the oracle, host and device.
     from crossbow_amd import BUF_DATA, BUF_DIFF, BUF_LAST
+    from crossbow_amd._lib import STAGING_DMA, STAGING_ZEROCOPY
     R = 4
-    st = O.make_state(n, 1, R, 0.1, 0.9)
-    g = make_gpu(n, R, 0.1, 0.9)
+    st = O.make_state(n, 1, R, 0.1, momentum)
+    g = make_gpu(n, R, 0.1, momentum, sync=1 if held is not None else 0)
     try:
+        g.set_staging_mode(STAGING_ZEROCOPY if staging == "zerocopy" else STAGING_DMA)
         if split:
             g.set_force_split(True)
         g.base_host_view(0, BUF_DATA)[:] = st.z[0]
-        g.base_host_view(0, BUF_LAST)[:] = st.last[0]
+        if momentum > 0:
+            g.base_host_view(0, BUF_LAST)[:] = st.last[0]
         for i in range(R):
             g.replica_host_view(i, BUF_DIFF)[:] = st.s[i]
             g.replica_host_view(i, BUF_DATA)[:] = st.w[i]
         g.set_timing(True)
         want = st.clone()
-        for step in range(2):
+        for step in range(3):
+            want.locked[:] = 1
             if copy_step == step:
                 g.set_replica_copy(1, True)
                 want.copy[1] = 1
+            if held is not None and step == 1:
+                g.replica_lock(held)  # busy on the task side: lockAny (SSP) skips it
+                want.locked[held] = 0
             g.lockAny()
             g.synchronise_staged(0, step + 1, 0, buckets)
             g.unlockAny()
+            if held is not None and step == 1:
+                g.replica_unlock(held)
             O.sma_step(want)
         g.wait()
         t = g.last_timing(0)
-        assert t[3] > 0 and t[4] > 0 and t[5] > 0, t
-        assert t[3] >= max(t[4], t[5]) * 0.99, "the step span covers uploads and downloads"
+        assert t[3] > 0, t
+        if staging == "dma":
+            assert t[4] > 0 and t[5] > 0, t
+            assert t[3] >= max(t[4], t[5]) * 0.99, "the step span covers uploads and downloads"
         assert_bitexact(g.base_host_view(0, BUF_DATA), want.z[0], "z staged out")
-        assert_bitexact(g.base_host_view(0, BUF_LAST), want.last[0], "last staged out")
+        if momentum > 0:
+            assert_bitexact(g.base_host_view(0, BUF_LAST), want.last[0], "last staged out")
+            assert_bitexact(g.base_read(0, BUF_LAST), want.last[0], "last on device")
         for i in range(R):
             assert_bitexact(g.replica_host_view(i, BUF_DATA), want.w[i], f"w[{i}] staged out")
             assert_bitexact(g.replica_host_view(i, BUF_DIFF), st.s[i], f"s[{i}] host mirror untouched")
-        # the device copy equals the host copy after the step
+            # the device holds what stage_in + synchronise + stage_out leave there
+            assert_bitexact(g.replica_read(i, BUF_DATA), want.w[i], f"w[{i}] on device")
+            assert_bitexact(g.replica_read(i, BUF_DIFF), st.s[i], f"s[{i}] on device")
         assert_bitexact(g.base_read(0, BUF_DATA), want.z[0], "z on device")
         if copy_step is not None:
             assert g.replica_copy(1) == 0
