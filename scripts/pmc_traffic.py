@@ -54,6 +54,8 @@ def main():
     p.add_argument("--lib", default=os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
                                                  "crossbow_amd", "libcrossbow_sma.so"),
                    help="the library the PMC passes ran (its device-code digest is stored with each entry)")
+    p.add_argument("--only", action="append", default=[],
+                   help="record only this kernel (repeatable; default: every kernel in the passes)")
     p.add_argument("dirs", nargs="+")
     a = p.parse_args()
     import sys
@@ -61,7 +63,7 @@ def main():
     from crossbow_amd.build import code_object_digest
     digest = code_object_digest(a.lib)
     vals = collect(a.dirs)
-    kernels = sorted({k for k, _ in vals})
+    kernels = sorted({k for k, _ in vals if not a.only or k in a.only})
     out = {}
     if os.path.exists(a.out):
         with open(a.out) as f:
