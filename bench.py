@@ -69,6 +69,10 @@ def parse():
     p.add_argument("--staged-buckets", type=int, default=8,
                    help="buckets of the pipelined host-staged step (cbx_synchronise_staged)")
     p.add_argument("--no-optimiser", action="store_true", help="skip the replica optimiser-step measurement")
+    p.add_argument("--rehearse-one-gpu", action="store_true",
+                   help="N > 1 rehearsal on a one-GPU box: every rank on device 0, each its own RCCL 'host' "
+                        "(NCCL_HOSTID), so real RCCL links the ranks by sockets over loopback; the numbers say "
+                        "nothing about xGMI, the run checks the N > 1 code path end to end")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
                    help="PMC-derived HBM bytes per launch (written by scripts/pmc_traffic.py)")
     return p.parse_args()
@@ -196,6 +200,9 @@ def main():
     args = parse()
     from crossbow_amd import dist as D
     rank, world, local_rank = D.env_rank()
+    if args.rehearse_one_gpu:
+        D.rehearsal_env(rank)
+        local_rank = 0
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: launch N>1 with torch.distributed.run")
 
@@ -341,6 +348,9 @@ def main():
                           "launches": len(kern),
                           "timed_in": "timed region" if not split else "calibration steps (one bucket, in order)"}
     result["step_ms_device_median"] = round(statistics.median(steps_ms), 4)
+    if args.rehearse_one_gpu:
+        result["rehearsal"] = (f"{G} ranks on ONE GPU over RCCL's socket transport (NCCL_HOSTID per rank): "
+                               "a check of the N > 1 code path, not an N-GPU measurement")
     if split:
         ar_ms = statistics.median(calib["allreduce"])
         algbw = 4 * n / (ar_ms * 1e-3) / 1e9

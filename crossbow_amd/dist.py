@@ -21,6 +21,17 @@ def env_rank() -> Tuple[int, int, int]:
             int(os.environ.get("LOCAL_RANK", "0")))
 
 
+def rehearsal_env(rank: int) -> None:
+    """Several ranks on ONE device with the real RCCL (rehearsals on a one-GPU
+    box): RCCL refuses two ranks of one host on one device, so each rank
+    claims a host of its own (NCCL_HOSTID) and the ranks connect through
+    RCCL's socket transport over loopback.  Set before the first RCCL call."""
+    os.environ["NCCL_HOSTID"] = f"cbx-rehearsal-rank-{rank}"
+    os.environ["NCCL_SOCKET_IFNAME"] = "lo"
+    os.environ["NCCL_IB_DISABLE"] = "1"
+    os.environ["NCCL_NET"] = "Socket"
+
+
 def init(world: int, rank: int, backend: str = "gloo") -> None:
     import torch.distributed as dist
     if world > 1 and not dist.is_initialized():

@@ -285,8 +285,9 @@ def run_case(g: Ctx, world: int, local: List[int], case: Case) -> dict:
     return {"bad": check.bad, "digest": dig, "differs": check.differs}
 
 
-def run_golden(g: Ctx, world: int, local: List[int], gcase: dict, algo: int = 0) -> List[str]:
-    """One committed fixture (tests/golden/, G = world): one step, bit for bit."""
+def run_golden(g: Ctx, world: int, local: List[int], gcase: dict, algo: int = 0, exact: bool = True) -> List[str]:
+    """One committed fixture (tests/golden/, G = world): one step, bit for bit
+    (or, with `exact` False, within the G > 1 tolerance: real RCCL's order)."""
     A = g.A
     if algo:
         g("cbx_set_allreduce_algorithm", algo)
@@ -315,7 +316,7 @@ def run_golden(g: Ctx, world: int, local: List[int], gcase: dict, algo: int = 0)
         if i in mine:
             g("cbx_replica_unlock", i)
     g("cbx_wait")
-    check = Checker(exact=True)
+    check = Checker(exact=exact)
     for d in local:
         check(f"{gcase['name']} z[{d}]", g.read("cbx_base_read", d, A.BUF_DATA, n), gcase["z_out"][d])
         if gcase["last_out"] is not None:
@@ -338,11 +339,12 @@ def _hip():
     return hip
 
 
-def run_bn(g: Ctx, world: int, local: List[int], poison: bool) -> List[str]:
+def run_bn(g: Ctx, world: int, local: List[int], poison: bool, exact: bool = True) -> List[str]:
     """BN running-statistics averaging (cudnnbatchnormparams.c:157-222) of
     three layers.  With `poison`, a device whose layer does not count holds
     NaN / Inf there: the reference never reads it (:177-184), so the average
-    must be the oracle's, finite, on every device."""
+    must be the oracle's, finite, on every device.  `exact` False: within the
+    G > 1 tolerance (real RCCL's summation order)."""
     O = oracle()
     A = g.A
     n = 4096
@@ -392,12 +394,13 @@ def run_bn(g: Ctx, world: int, local: List[int], poison: bool) -> List[str]:
                 assert hip.hipMemcpy(got.ctypes.data, ptr, 4 * e, 2) == 0
                 if not np.all(np.isfinite(want)):
                     bad.append(f"oracle bn {what}[{l}] on device {d} is not finite")
-                if not np.array_equal(got.view(np.uint32), want.view(np.uint32)):
-                    bad.append(f"bn {what}[{l}] on device {d} differs")
+                check = Checker(exact=exact)
+                check(f"bn {what}[{l}] on device {d}", got, want)
+                bad += check.bad
     return bad
 
 
-def run_autotune_checkpoint(g: Ctx, world: int, local: List[int], ckdir: str) -> List[str]:
+def run_autotune_checkpoint(g: Ctx, world: int, local: List[int], ckdir: str, exact: bool = True) -> List[str]:
     """synchronise(autotune = +1 / -1) adds / deletes one replica per device
     after the step (executioncontext.c:2321-2328, modelmanager.c:362-557): a
     new replica copies its device's first replica and joins the next step.
@@ -429,7 +432,7 @@ def run_autotune_checkpoint(g: Ctx, world: int, local: List[int], ckdir: str) ->
         st = O.SmaState(world, len(s), n, 0.1, mom, st.z, st.last, s, w)
         assert g("cbx_num_replicas") == st.size
     g("cbx_wait")
-    check = Checker(exact=True)
+    check = Checker(exact=exact)
     for d in local:
         check(f"autotune z[{d}]", g.read("cbx_base_read", d, A.BUF_DATA, n), st.z[d])
         check(f"autotune last[{d}]", g.read("cbx_base_read", d, A.BUF_LAST, n), st.last[d])
@@ -437,6 +440,10 @@ def run_autotune_checkpoint(g: Ctx, world: int, local: List[int], ckdir: str) ->
         if i % world in local:
             check(f"autotune w[{i}]", g.read("cbx_replica_read", i, A.BUF_DATA, n), st.w[i])
     bad = check.bad
+    if not exact:  # the files must hold the device's own values, byte for byte
+        st.z = {d: g.read("cbx_base_read", d, A.BUF_DATA, n) for d in local}
+        st.last = {d: g.read("cbx_base_read", d, A.BUF_LAST, n) for d in local}
+        st.w = {i: g.read("cbx_replica_read", i, A.BUF_DATA, n) for i in range(st.size) if i % world in local}
     # checkpoint (executioncontext.c:2340-2364) into the shared directory
     os.makedirs(ckdir, exist_ok=True)
     hip = _hip()
