@@ -265,9 +265,10 @@ def main():
     pipeline_mode = 0
     wait_stride = 1
     ar_group = 1
+    ar_algo = 0
     if split and args.bucket_mb == 0:
         # warm-up autotune of the bucket count on the live communicator (same choice on every rank)
-        bucket_elems, pipeline_mode, wait_stride, ar_group, tuning = D.tune_buckets(gpu, n, world, step)
+        bucket_elems, pipeline_mode, wait_stride, ar_group, ar_algo, tuning = D.tune_buckets(gpu, n, world, step)
 
     for _ in range(args.warmup):
         step()
@@ -314,6 +315,7 @@ def main():
             "pipeline_mode": None if not split else pipeline_mode,
             "cross_wait_stride": None if not split else wait_stride,
             "allreduce_group": None if not split else ar_group,
+            "allreduce_algorithm": None if not split else ("reduce-scatter+all-gather" if ar_algo == 2 else "all-reduce"),
             "bucket_tuning_ms_per_step": tuning,
             "kernel_config": dict(block=args.block, blocks_per_cu=args.blocks_per_cu, policy=args.policy,
                                   unroll=args.unroll, waves_per_cu=args.waves_per_cu, bucket_mb=args.bucket_mb),

@@ -30,7 +30,7 @@ BUF_DATA, BUF_GRADIENT, BUF_DIFF, BUF_LAST = 0, 1, 2, 3
 T_KERNEL, T_ALLREDUCE, T_APPLY, T_STEP, T_H2D, T_D2H, T_COUNT = range(7)
 SYNC_BSP, SYNC_SSP, SYNC_ASP = 0, 1, 2
 UPDATE_DEFAULT, UPDATE_WORKER, UPDATE_SYNCHRONOUSEAMSGD, UPDATE_SMA = 0, 1, 3, 7
-ALLREDUCE_RCCL, ALLREDUCE_PEER = 0, 1
+ALLREDUCE_RCCL, ALLREDUCE_PEER, ALLREDUCE_RSAG = 0, 1, 2
 STAGING_ZEROCOPY, STAGING_DMA = 0, 1
 
 

@@ -789,6 +789,7 @@ int sma_step(cbx_context *c, int first) {
     // A step joins the whole sync stream instead when anything else was
     // enqueued since the last cross-pipelined step (foreign_ops).
     const bool cross = pipelined && c->pipeline_mode == 1;
+    const bool rsag = c->allreduce_algo == CBX_ALLREDUCE_RSAG;
     // Per-bucket events ride on the kernels' own dispatch packets (stop
     // event) instead of a separate hipEventRecord marker, which left a
     // ~10 us gap on the sync stream per bucket: -2 to -8 % per step
@@ -845,21 +846,62 @@ int sma_step(cbx_context *c, int first) {
           HIP_TRY(hipStreamWaitEvent(d.comm_stream, d.bucket_acc[wait_acc], 0));
         }
       }
-      NCCL_TRY(ncclGroupStart());
-      for (size_t k = 0; k < c->devs.size(); ++k) {
-        Device &d = c->devs[k];
-        HIP_TRY(hipSetDevice(d.hip_id));
-        const float *src = base_dev(c, d, CBX_BUF_GRADIENT) + start * 4;
-        float *dst = base_dev(c, d, CBX_BUF_DIFF) + start * 4;
-        size_t count = (size_t)len * 4;
-        if (b == 0) {
-          src -= cbx::kCtrlFloats;
-          dst -= cbx::kCtrlFloats;
-          count += cbx::kCtrlFloats;
+      if (rsag) {
+        // Reduce-scatter form: shard g of the bucket (len / G float4s) is
+        // reduced on rank g, which applies the base momentum to its shard of
+        // last; the all-gather of last (or of D without momentum) then hands
+        // every rank the whole bucket of D' for kernel B.  The control block
+        // rides a 64-float all-reduce grouped with bucket 0's reduce-scatter.
+        const int64_t sh4 = len / c->G;
+        NCCL_TRY(ncclGroupStart());
+        for (size_t k = 0; k < c->devs.size(); ++k) {
+          Device &d = c->devs[k];
+          HIP_TRY(hipSetDevice(d.hip_id));
+          hipStream_t st = on_comm ? d.comm_stream : d.stream;
+          if (b == 0)
+            NCCL_TRY(ncclAllReduce(base_ctrl(d, CBX_BUF_GRADIENT), base_ctrl(d, CBX_BUF_DIFF), cbx::kCtrlFloats,
+                                   ncclFloat, ncclSum, d.comm, st));
+          NCCL_TRY(ncclReduceScatter(base_dev(c, d, CBX_BUF_GRADIENT) + start * 4,
+                                     base_dev(c, d, CBX_BUF_DIFF) + (start + d.g * sh4) * 4, (size_t)sh4 * 4,
+                                     ncclFloat, ncclSum, d.comm, st));
         }
-        NCCL_TRY(ncclAllReduce(src, dst, count, ncclFloat, ncclSum, d.comm, on_comm ? d.comm_stream : d.stream));
+        NCCL_TRY(ncclGroupEnd());
+        const int gather = mom ? CBX_BUF_LAST : CBX_BUF_DIFF;
+        for (size_t k = 0; k < c->devs.size(); ++k) {
+          if (!mom) break;
+          Device &d = c->devs[k];
+          HIP_TRY(hipSetDevice(d.hip_id));
+          cbx::SmaArgs a = offset_args(args[k], start + d.g * sh4, sh4);
+          cbx::LaunchConfig cfg = c->apply_cfg;
+          cfg.num_cus = d.num_cus;
+          HIP_TRY(cbx::launch_sma_shard_momentum(a, cfg, on_comm ? d.comm_stream : d.stream));
+        }
+        NCCL_TRY(ncclGroupStart());
+        for (size_t k = 0; k < c->devs.size(); ++k) {
+          Device &d = c->devs[k];
+          HIP_TRY(hipSetDevice(d.hip_id));
+          float *buf = base_dev(c, d, gather) + start * 4;
+          NCCL_TRY(ncclAllGather(buf + d.g * sh4 * 4, buf, (size_t)sh4 * 4, ncclFloat, d.comm,
+                                 on_comm ? d.comm_stream : d.stream));
+        }
+        NCCL_TRY(ncclGroupEnd());
+      } else {
+        NCCL_TRY(ncclGroupStart());
+        for (size_t k = 0; k < c->devs.size(); ++k) {
+          Device &d = c->devs[k];
+          HIP_TRY(hipSetDevice(d.hip_id));
+          const float *src = base_dev(c, d, CBX_BUF_GRADIENT) + start * 4;
+          float *dst = base_dev(c, d, CBX_BUF_DIFF) + start * 4;
+          size_t count = (size_t)len * 4;
+          if (b == 0) {
+            src -= cbx::kCtrlFloats;
+            dst -= cbx::kCtrlFloats;
+            count += cbx::kCtrlFloats;
+          }
+          NCCL_TRY(ncclAllReduce(src, dst, count, ncclFloat, ncclSum, d.comm, on_comm ? d.comm_stream : d.stream));
+        }
+        NCCL_TRY(ncclGroupEnd());
       }
-      NCCL_TRY(ncclGroupEnd());
       if (on_comm) {
         for (size_t k = 0; k < c->devs.size(); ++k) {
           Device &d = c->devs[k];
@@ -900,6 +942,7 @@ int sma_step(cbx_context *c, int first) {
         cbx::Timing t;
         if (b == nb - 1) t.stop = step_stop_event(c, d, EV_B);
         cbx::SmaArgs a = offset_args(args[k], start, len);
+        if (rsag && mom) a.D = a.last;  // the gathered D' (kernel B then adds it without momentum)
         if (cross) {
           // The next step's AR(0) may overwrite D's control block before this
           // step's later buckets run: B(0) publishes the Phase-D decision to a
@@ -909,7 +952,7 @@ int sma_step(cbx_context *c, int first) {
         }
         const bool in_dispatch = cross && !t.stop;
         if (in_dispatch) t.stop = d.bucket_b[b];
-        HIP_TRY(cbx::launch_sma_apply(a, mom, cfg, d.stream, t));
+        HIP_TRY(cbx::launch_sma_apply(a, mom && !rsag, cfg, d.stream, t));
         if (cross && !in_dispatch) HIP_TRY(hipEventRecord(d.bucket_b[b], d.stream));
       }
       return CBX_OK;
@@ -2891,8 +2934,11 @@ int cbx_set_allreduce_group(cbx_context *c, int group) {
 
 int cbx_set_allreduce_algorithm(cbx_context *c, int algorithm) {
   TRY(check_ctx(c));
-  if (algorithm != CBX_ALLREDUCE_RCCL && algorithm != CBX_ALLREDUCE_PEER)
-    return fail(CBX_ERR_INVALID, "all-reduce algorithm must be CBX_ALLREDUCE_RCCL or CBX_ALLREDUCE_PEER");
+  if (algorithm != CBX_ALLREDUCE_RCCL && algorithm != CBX_ALLREDUCE_PEER && algorithm != CBX_ALLREDUCE_RSAG)
+    return fail(CBX_ERR_INVALID, "all-reduce algorithm must be CBX_ALLREDUCE_RCCL, _PEER or _RSAG");
+  if (algorithm == CBX_ALLREDUCE_RSAG && (c->G > cbx::kMaxDevices || cbx::kPadFloat4 % c->G != 0))
+    return fail(CBX_ERR_UNSUPPORTED, "the reduce-scatter form needs G dividing %lld (G = %d)",
+                (long long)cbx::kPadFloat4, c->G);
   if (algorithm == CBX_ALLREDUCE_PEER && c->per_rank && c->G > 1)
     return fail(CBX_ERR_UNSUPPORTED, "the peer-read all-reduce needs one process over every device (cbx_init)");
   if (algorithm == CBX_ALLREDUCE_PEER && c->G > cbx::kMaxDevices)

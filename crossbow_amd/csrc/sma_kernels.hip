@@ -256,6 +256,21 @@ __global__ __launch_bounds__(256) void sma_apply_kernel(const SmaArgs a) {
 }
 
 // ---------------------------------------------------------------------------
+// Reduce-scatter form of Phase C (cbx_set_allreduce_algorithm RSAG): on this
+// rank's shard of a bucket, D' = fma(0.9, last, D) into last (sma.c:155-164);
+// the all-gather of last then gives every rank every shard of D', and kernel B
+// (without momentum, D := last) adds it to z.  One float4 per lane, bounds-
+// checked: a shard is 1/G of a padded bucket.
+// ---------------------------------------------------------------------------
+template <int P>
+__global__ __launch_bounds__(256) void sma_shard_momentum_kernel(const SmaArgs a) {
+  const v4f mb = kBaseMomentum;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < a.n4; i += stride)
+    st<P>(a.last + i, vfma(mb, ld<P>(a.last + i), ld<P>(a.D + i)));
+}
+
+// ---------------------------------------------------------------------------
 // Host-staged step through zero-copy (sma_internal.h, StagedArgs).  Same
 // arithmetic, in the same order, as the device-resident kernels above; host
 // memory is read and written with plain loads / stores (PCIe-bound: ~55 GB/s
@@ -968,6 +983,18 @@ hipError_t launch_sma_apply(const SmaArgs &a, bool momentum, const LaunchConfig 
                             Timing t) {
   if (cfg.policy == 1) return momentum ? apply_u<true, 1>(a, cfg, stream, t) : apply_u<false, 1>(a, cfg, stream, t);
   return momentum ? apply_u<true, 0>(a, cfg, stream, t) : apply_u<false, 0>(a, cfg, stream, t);
+}
+
+hipError_t launch_sma_shard_momentum(const SmaArgs &a, const LaunchConfig &cfg0, hipStream_t stream, Timing t) {
+  LaunchConfig cfg = cfg0;
+  cfg.unroll = 1;
+  const dim3 g = grid_for(a.n4, cfg);
+  const unsigned lds = lds_for_occupancy(cfg, 2, 1, g.x);
+  if (cfg.policy == 1)
+    hipExtLaunchKernelGGL((sma_shard_momentum_kernel<1>), g, dim3(cfg.block), lds, stream, t.start, t.stop, 0, a);
+  else
+    hipExtLaunchKernelGGL((sma_shard_momentum_kernel<0>), g, dim3(cfg.block), lds, stream, t.start, t.stop, 0, a);
+  return hipGetLastError();
 }
 
 // Launch `K<..., U>` for the configured unroll (1 or 2) with the occupancy

@@ -14,6 +14,8 @@ from __future__ import annotations
 import os
 from typing import Callable, Optional, Tuple
 
+from ._abi import ALLREDUCE_RCCL, ALLREDUCE_RSAG
+
 
 def env_rank() -> Tuple[int, int, int]:
     """(rank, world_size, local_rank) from the torch.distributed.run environment."""
@@ -95,9 +97,15 @@ def tune_buckets(gpu, n: int, world: int, step: Callable[[], None], candidates=(
     in ``passes`` interleaved passes and each keeps its best pass, so one
     noisy sample (a few percent on one GPU) does not decide.
 
-    Returns (bucket_elements, mode, stride, group, {key: ms_per_step}) with
-    keys "<buckets>/<mode>" for stride 1, "<buckets>/<mode>/s<stride>", and
-    "<key of the winner>/g<group>".
+    Last, the winner's configuration is timed with the reduce-scatter form
+    of the all-reduce (``gpu.set_allreduce_algorithm(ALLREDUCE_RSAG)``:
+    reduce-scatter, base momentum on the rank's shard, all-gather), which
+    moves the same link bytes in two collectives per bucket and saves kernel
+    B's momentum pass on (G-1)/G of the model; it is kept only if faster.
+
+    Returns (bucket_elements, mode, stride, group, algorithm, {key: ms_per_step})
+    with keys "<buckets>/<mode>" for stride 1, "<buckets>/<mode>/s<stride>",
+    "<key of the winner>/g<group>" and "<key of the winner>[/g<group>]/rsag".
     """
     import time
 
@@ -118,6 +126,7 @@ def tune_buckets(gpu, n: int, world: int, step: Callable[[], None], candidates=(
         return max_over_ranks((time.perf_counter() - t0) * 1e3 / steps, world)
 
     gpu.set_allreduce_group(1)
+    gpu.set_allreduce_algorithm(ALLREDUCE_RCCL)
     results = {}
     for _ in range(max(1, passes)):
         for nb in candidates:
@@ -152,7 +161,17 @@ def tune_buckets(gpu, n: int, world: int, step: Callable[[], None], candidates=(
             out[tuning_key(nb, mode, stride) + f"/g{grp}"] = timed[grp]
         group = min(timed, key=lambda g: (timed[g], g))
     gpu.set_allreduce_group(group)
-    return elems, mode, stride, group, out
+    win_key = tuning_key(nb, mode, stride) + (f"/g{group}" if group > 1 else "")
+    win_ms = out.get(win_key, results[best])
+    algorithm = ALLREDUCE_RCCL
+    if world > 1 and world <= 16 and 1024 % world == 0:
+        gpu.set_allreduce_algorithm(ALLREDUCE_RSAG)
+        ms = min(timed_steps() for _ in range(max(1, passes)))
+        out[win_key + "/rsag"] = ms
+        if ms < win_ms:
+            algorithm = ALLREDUCE_RSAG
+        gpu.set_allreduce_algorithm(algorithm)
+    return elems, mode, stride, group, algorithm, out
 
 
 def tuning_key(nb: int, mode: int, stride: int = 1) -> str:

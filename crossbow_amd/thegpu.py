@@ -399,7 +399,8 @@ class TheGPU:
         check(self._L.cbx_set_allreduce_group(self._ctx, group))
 
     def set_allreduce_algorithm(self, algorithm: int) -> None:
-        """ALLREDUCE_RCCL (default) or ALLREDUCE_PEER (one process over every device: peer reads over xGMI)."""
+        """ALLREDUCE_RCCL (default), ALLREDUCE_PEER (one process over every device: peer reads over xGMI)
+        or ALLREDUCE_RSAG (reduce-scatter, momentum on the shard, all-gather)."""
         check(self._L.cbx_set_allreduce_algorithm(self._ctx, algorithm))
 
     def set_staging_mode(self, mode: int) -> None:

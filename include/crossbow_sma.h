@@ -370,9 +370,19 @@ int cbx_set_allreduce_group (cbx_context *ctx, int group);
  *     copies peer buffers, common.c:64-95).  Sums in device order: bit-exact
  *     against the rank-order oracle and identical on every device.  The
  *     host-staged step and S-SGD keep RCCL.
+ *   CBX_ALLREDUCE_RSAG (2): every process form.  Per bucket, RCCL
+ *     reduce-scatter of acc (the control block rides a grouped 64-float
+ *     all-reduce), the base momentum on this rank's shard only
+ *     (last = fma(0.9, last, D)), RCCL all-gather of last, then kernel B
+ *     adds the gathered D' to z.  The all-reduce's link bytes; the momentum
+ *     pass (12 B per element) runs on 1/G of the bucket; every rank ends
+ *     with the same z and last (SURVEY 8(e) variant 1).  G must divide 1024
+ *     (powers of two up to 16).  The host-staged step and S-SGD keep the
+ *     all-reduce.
  * CBX_ERR_UNSUPPORTED for PEER on a one-process-per-GPU context.          */
 #define CBX_ALLREDUCE_RCCL 0
 #define CBX_ALLREDUCE_PEER 1
+#define CBX_ALLREDUCE_RSAG 2
 int cbx_set_allreduce_algorithm (cbx_context *ctx, int algorithm);
 /* How cbx_synchronise_staged moves the model between the pinned host mirror
  * and the device (north_star: the path starts and ends in host memory):

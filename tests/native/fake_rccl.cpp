@@ -12,7 +12,8 @@
 //    communicator, as in NCCL, and run at ncclGroupEnd.  An ungrouped call on
 //    such a communicator is an error (real NCCL would deadlock on it).
 //
-// Each all-reduce synchronises the stream it was given (so every kernel the
+// Calls: ncclAllReduce, ncclReduceScatter and ncclAllGather (fp32; sum).
+// Each collective synchronises the stream it was given (so every kernel the
 // library ordered before it has finished), sums the ranks' send buffers on
 // the host, writes the result to every receive buffer with a blocking copy
 // and returns.  Stream order is thereby preserved: everything the library
@@ -137,7 +138,33 @@ void reduce(const std::vector<const float *> &src, size_t count, bool ring, floa
   }
 }
 
+enum OpKind { kAllReduce = 0, kReduceScatter = 1, kAllGather = 2 };
+
+// Floats of one rank's send buffer / receive buffer for a call with `count`
+// (the NCCL argument: recvcount for reduce-scatter, sendcount for all-gather).
+size_t send_elems(int kind, size_t count, int G) { return kind == kReduceScatter ? count * (size_t)G : count; }
+size_t recv_elems(int kind, size_t count, int G) { return kind == kAllGather ? count * (size_t)G : count; }
+
+// The collective over the ranks' host copies src[0..G-1] of their send
+// buffers: what rank `rank` receives, into out (recv_elems floats).
+//   all-reduce: the sum;  reduce-scatter: rank's slice of the sum (the ring
+//   order, if on, is that of a ring all-reduce's reduce phase);  all-gather:
+//   the concatenation in rank order.
+void collective(int kind, const std::vector<const float *> &src, size_t count, bool ring, int rank, float *out) {
+  const int G = (int)src.size();
+  if (kind == kAllGather) {
+    for (int r = 0; r < G; ++r) std::memcpy(out + (size_t)r * count, src[r], count * sizeof(float));
+    return;
+  }
+  const size_t n = send_elems(kind, count, G);
+  std::vector<float> sum(n);
+  reduce(src, n, ring, sum.data());
+  const size_t off = kind == kReduceScatter ? (size_t)rank * count : 0;
+  std::memcpy(out, sum.data() + off, count * sizeof(float));
+}
+
 struct PendingOp {
+  int kind;
   const void *send;
   void *recv;
   size_t count;
@@ -148,51 +175,54 @@ struct PendingOp {
 thread_local int g_depth = 0;
 thread_local std::vector<PendingOp> g_ops;
 
-// One grouped all-reduce of a single-process clique: ops[r] is rank r's.
+// One grouped collective of a single-process clique: ops[r] is rank r's.
 ncclResult_t run_clique(const std::vector<PendingOp *> &ops) {
   const int G = (int)ops.size();
+  const int kind = ops[0]->kind;
   const size_t count = ops[0]->count;
-  std::vector<std::vector<float>> host(G, std::vector<float>(count));
+  const size_t ns = send_elems(kind, count, G), nr = recv_elems(kind, count, G);
+  std::vector<std::vector<float>> host(G, std::vector<float>(ns));
   std::vector<const float *> src(G);
   for (int r = 0; r < G; ++r) {
-    if (ops[r]->count != count) return ncclInvalidArgument;
+    if (ops[r]->count != count || ops[r]->kind != kind) return ncclInvalidArgument;
     if (hipSetDevice(ops[r]->comm->device) != hipSuccess) return ncclSystemError;
     if (hipStreamSynchronize(ops[r]->stream) != hipSuccess) return ncclSystemError;
-    if (hipMemcpy(host[r].data(), ops[r]->send, count * sizeof(float), hipMemcpyDeviceToHost) != hipSuccess)
+    if (hipMemcpy(host[r].data(), ops[r]->send, ns * sizeof(float), hipMemcpyDeviceToHost) != hipSuccess)
       return ncclSystemError;
     src[r] = host[r].data();
   }
-  std::vector<float> sum(count);
-  reduce(src, count, ops[0]->comm->ring, sum.data());
+  std::vector<float> out(nr);
   for (int r = 0; r < G; ++r) {
+    collective(kind, src, count, ops[0]->comm->ring, r, out.data());
     if (hipSetDevice(ops[r]->comm->device) != hipSuccess) return ncclSystemError;
-    if (hipMemcpy(ops[r]->recv, sum.data(), count * sizeof(float), hipMemcpyHostToDevice) != hipSuccess)
+    if (hipMemcpy(ops[r]->recv, out.data(), nr * sizeof(float), hipMemcpyHostToDevice) != hipSuccess)
       return ncclSystemError;
   }
   return ncclSuccess;
 }
 
-// The per-rank (multi-process) all-reduce through files.
-ncclResult_t run_ranked(const void *send, void *recv, size_t count, ncclComm *c, hipStream_t stream) {
+// The per-rank (multi-process) collective through files.
+ncclResult_t run_ranked(int kind, const void *send, void *recv, size_t count, ncclComm *c, hipStream_t stream) {
   if (hipStreamSynchronize(stream) != hipSuccess) return ncclSystemError;
-  const size_t bytes = count * sizeof(float);
+  const size_t ns = send_elems(kind, count, c->nranks), nr = recv_elems(kind, count, c->nranks);
+  const size_t bytes = ns * sizeof(float);
   std::vector<std::vector<float>> host(c->nranks);
   std::vector<const float *> src(c->nranks);
-  host[c->rank].resize(count);
+  host[c->rank].resize(ns);
   if (hipMemcpy(host[c->rank].data(), send, bytes, hipMemcpyDeviceToHost) != hipSuccess) return ncclSystemError;
   const unsigned long long seq = c->seq++;
   if (c->nranks > 1 && !write_file(path(c, seq, c->rank, "bin"), host[c->rank].data(), bytes)) return ncclSystemError;
   for (int r = 0; r < c->nranks; ++r) {
     if (r != c->rank) {
-      host[r].resize(count);
+      host[r].resize(ns);
       const std::string p = path(c, seq, r, "bin");
       if (!wait_for(p) || !read_file(p, host[r].data(), bytes)) return ncclSystemError;
     }
     src[r] = host[r].data();
   }
-  std::vector<float> sum(count);
-  reduce(src, count, c->ring, sum.data());
-  if (hipMemcpy(recv, sum.data(), bytes, hipMemcpyHostToDevice) != hipSuccess) return ncclSystemError;
+  std::vector<float> out(nr);
+  collective(kind, src, count, c->ring, c->rank, out.data());
+  if (hipMemcpy(recv, out.data(), nr * sizeof(float), hipMemcpyHostToDevice) != hipSuccess) return ncclSystemError;
   if (c->nranks > 1) {
     // Every rank acknowledges; a rank removes its data file once all have read it.
     const char one = 1;
@@ -203,6 +233,17 @@ ncclResult_t run_ranked(const void *send, void *recv, size_t count, ncclComm *c,
     if (seq > 0) std::remove(path(c, seq - 1, c->rank, "ack").c_str());  // every rank is past seq - 1
   }
   return ncclSuccess;
+}
+
+ncclResult_t enqueue(int kind, const void *send, void *recv, size_t count, ncclDataType_t type, ncclComm_t c,
+                     hipStream_t stream) {
+  if (!c || type != ncclFloat) return ncclInvalidArgument;
+  if (c->clique) {
+    if (g_depth == 0) return ncclInvalidUsage;
+    g_ops.push_back(PendingOp{kind, send, recv, count, c, stream});
+    return ncclSuccess;
+  }
+  return run_ranked(kind, send, recv, count, c, stream);
 }
 
 }  // namespace
@@ -304,13 +345,19 @@ const char *ncclGetErrorString(ncclResult_t r) {
 
 ncclResult_t ncclAllReduce(const void *send, void *recv, size_t count, ncclDataType_t type, ncclRedOp_t op,
                            ncclComm_t c, hipStream_t stream) {
-  if (!c || type != ncclFloat || op != ncclSum) return ncclInvalidArgument;
-  if (c->clique) {
-    if (g_depth == 0) return ncclInvalidUsage;
-    g_ops.push_back(PendingOp{send, recv, count, c, stream});
-    return ncclSuccess;
-  }
-  return run_ranked(send, recv, count, c, stream);
+  if (op != ncclSum) return ncclInvalidArgument;
+  return enqueue(kAllReduce, send, recv, count, type, c, stream);
+}
+
+ncclResult_t ncclReduceScatter(const void *send, void *recv, size_t recvcount, ncclDataType_t type, ncclRedOp_t op,
+                               ncclComm_t c, hipStream_t stream) {
+  if (op != ncclSum) return ncclInvalidArgument;
+  return enqueue(kReduceScatter, send, recv, recvcount, type, c, stream);
+}
+
+ncclResult_t ncclAllGather(const void *send, void *recv, size_t sendcount, ncclDataType_t type, ncclComm_t c,
+                           hipStream_t stream) {
+  return enqueue(kAllGather, send, recv, sendcount, type, c, stream);
 }
 
 }  // extern "C"

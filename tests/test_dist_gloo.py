@@ -204,6 +204,10 @@ class _FakeGpu:
 
     def __init__(self, rank, n):
         self.rank, self.n, self.elems, self.mode, self.stride, self.group = rank, n, 0, 0, 1, 1
+        self.algo = 0
+
+    def set_allreduce_algorithm(self, a):
+        self.algo = a
 
     def set_bucket_elements(self, e):
         self.elems = e
@@ -228,6 +232,7 @@ class _FakeGpu:
         cost += 2 if (self.mode >= 1 and self.rank == 1) else 0  # cross-step modes slower on rank 1
         cost += self.stride - 1  # and fewer cross-step waits slower everywhere
         cost += {0: -1, 1: 2}[self.rank] if self.group > 1 else 0  # grouping helps rank 0 only: max says no
+        cost -= 1 if self.algo == 2 else 0  # the reduce-scatter form is faster on both ranks
         time.sleep(cost * 2e-3)
 
 
@@ -241,8 +246,10 @@ def _tune_main(rank, world, port, q):
         D.init(world, rank, backend="gloo")
         g = _FakeGpu(rank, 1000)
         g.group = 3  # a group left over from an earlier setting must not skew the sweep
-        elems, mode, stride, group, res = D.tune_buckets(g, 1000, world, g.step, steps=2, warmup=1)
-        q.put((rank, (elems, g.elems, mode, g.mode, stride, g.stride, group, g.group, sorted(res)), None))
+        g.algo = 2   # nor an algorithm left over: the sweep runs on the all-reduce
+        elems, mode, stride, group, algo, res = D.tune_buckets(g, 1000, world, g.step, steps=2, warmup=1)
+        q.put((rank, (elems, g.elems, mode, g.mode, stride, g.stride, group, g.group, algo, g.algo, sorted(res)),
+               None))
         D.finalize(world)
     except Exception:  # pragma: no cover
         import traceback
@@ -272,8 +279,8 @@ def test_bucket_tuning_agrees_across_ranks():
                 p.kill()
     for rank in range(world):
         assert out[rank][1] is None, out[rank][1]
-    (e0, set0, m0, setm0, s0, sets0, g0, setg0, cands), (e1, set1, m1, setm1, s1, sets1, g1, setg1, _) = \
-        out[0][0], out[1][0]
+    (e0, set0, m0, setm0, s0, sets0, g0, setg0, a0, seta0, cands), \
+        (e1, set1, m1, setm1, s1, sets1, g1, setg1, a1, seta1, _) = out[0][0], out[1][0]
     assert e0 == e1 == set0 == set1 == 250, (out[0][0], out[1][0])
     assert m0 == m1 == setm0 == setm1 == 0
     assert s0 == s1 == sets0 == sets1 == 1
@@ -281,4 +288,6 @@ def test_bucket_tuning_agrees_across_ranks():
     want = ["1/0"] + [f"{nb}/{m}" for nb in (2, 4, 8) for m in (0, 1)]
     want += [f"{nb}/1/s{s}" for nb in (4, 8) for s in (2, 4) if s < nb]
     want += ["4/0/g2"]  # groups 1 < g < buckets, timed for the winner only
+    want += ["4/0/rsag"]  # then the reduce-scatter form of the winner
     assert cands == sorted(want)
+    assert a0 == a1 == seta0 == seta1 == 2  # faster on both ranks: kept

@@ -22,6 +22,12 @@ golden fixtures run through it, are bit for bit against the oracle (device
 order from +0 is the oracle's order).  On one GPU every "peer" is device 0
 itself, so this pins the algorithm, not its xGMI speed.
 
+The reduce-scatter form (cbx_set_allreduce_algorithm RSAG: reduce-scatter,
+base momentum on each device's shard, all-gather) runs here and in the
+one-process-per-GPU tests: bit for bit in rank order (the loopback's
+reduce-scatter sums in rank order), within the tolerance in ring order, and
+through the G > 1 golden fixtures.
+
 The worker runs in a spawned, torch-free process (crossbow_amd/_abi.py), so
 no real RCCL is loaded beside the loopback one.  Shared machinery:
 tests/multidev_common.py.
@@ -57,20 +63,29 @@ CASES = [
     Case("sma-peer-big", 300_007, 3, 0.9, 2, algo=1),
     # switching between the algorithms, and from the cross-step pipeline, between steps
     Case("sma-peer-switch", 300_007, 2, 0.9, 5, bucket=65_536, mode=1, copy={3: 1}, algo_at={1: 1, 2: 0, 4: 1}),
+    # the reduce-scatter form (RSAG: reduce-scatter, momentum on the shard, all-gather)
+    Case("sma-rsag", 50_001, 2, 0.9, 3, copy={1: 3}, held={0: 1}, algo=2),
+    Case("sma-rsag-no-momentum", 20_011, 1, 0.0, 2, bucket=4096, utype=3, algo=2),
+    Case("sma-rsag-buckets-cross", 300_007, 2, 0.9, 5, bucket=65_536, copy={2: 1}, held={3: 0}, mode=1, stride=2,
+         group=2, algo=2),
+    Case("sma-rsag-ring", 300_007, 2, 0.9, 4, bucket=65_536, mode=1, order="ring", algo=2),
+    Case("sma-rsag-switch", 300_007, 2, 0.9, 5, bucket=65_536, mode=1, copy={3: 1}, algo_at={1: 2, 2: 0, 3: 1, 4: 2}),
 ]
 
 
 def _jobs(G):
-    if G == 3:  # a non-power-of-two clique: the plain step in both orders, and the peer path
+    if G == 3:  # a non-power-of-two clique: the plain step in both orders, and the peer path (RSAG is refused)
         names = ("sma", "sma-ring", "sma-peer", "sma-peer-empty-shards")
     elif G == 8:
         names = ("sma-copy-ssp", "sma-buckets-cross", "ssgd-buckets", "sma-ring", "sma-ring-buckets-cross",
-                 "sma-peer", "sma-peer-empty-shards", "sma-peer-switch")
+                 "sma-peer", "sma-peer-empty-shards", "sma-peer-switch", "sma-rsag", "sma-rsag-buckets-cross",
+                 "sma-rsag-ring", "sma-rsag-switch")
     else:
         names = [c.name for c in CASES]
-    jobs = [("case", n) for n in names if G >= 3 or not n.startswith("sma-ring")]
+    jobs = [("case", n) for n in names if G >= 3 or "-ring" not in n]
     jobs += [("golden", gc["name"]) for gc in C.golden_cases(G)]
     jobs += [("golden-peer", gc["name"]) for gc in C.golden_cases(G)]
+    jobs += [("golden-rsag", gc["name"]) for gc in C.golden_cases(G)]
     return jobs + [("bn", "bn"), ("autotune", "autotune")]
 
 
@@ -85,10 +100,13 @@ def _worker(G, jobs, ckdir, q):
             os.environ["FAKE_RCCL_ORDER"] = cases[name].order if kind == "case" else "rank"
             g = C.init_local(L, A, G)
             try:
+                if G == 3:  # the reduce-scatter form needs G dividing the bucket padding
+                    assert L.cbx_set_allreduce_algorithm(g.c, A.ALLREDUCE_RSAG) == A.CBX_ERR_UNSUPPORTED
                 if kind == "case":
                     res = C.run_case(g, G, local, cases[name])
-                elif kind in ("golden", "golden-peer"):
-                    res = {"bad": C.run_golden(g, G, local, goldens[name], algo=1 if kind == "golden-peer" else 0)}
+                elif kind.startswith("golden"):
+                    algo = {"golden": 0, "golden-peer": 1, "golden-rsag": 2}[kind]
+                    res = {"bad": C.run_golden(g, G, local, goldens[name], algo=algo)}
                 elif kind == "bn":
                     res = {"bad": C.run_bn(g, G, local, poison=True)}
                 else:

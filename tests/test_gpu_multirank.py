@@ -51,6 +51,12 @@ CASES = [
     # RCCL's (ring) summation order: the stated tolerance and cross-rank identity
     Case("sma-ring", 50_001, 2, 0.9, 4, copy={2: 1}, order="ring"),
     Case("sma-ring-cross", 300_007, 2, 0.9, 4, bucket=65_536, mode=1, stride=2, order="ring"),
+    # the reduce-scatter form (cbx_set_allreduce_algorithm RSAG)
+    Case("sma-rsag", 50_001, 2, 0.9, 3, copy={1: 3}, held={0: 1}, algo=2),
+    Case("sma-rsag-buckets-cross", 300_007, 2, 0.9, 5, bucket=65_536, copy={2: 1}, held={3: 0}, mode=1, stride=2,
+         group=2, algo=2),
+    Case("sma-rsag-no-momentum", 20_011, 1, 0.0, 2, bucket=4096, utype=3, algo=2),
+    Case("sma-rsag-ring", 300_007, 2, 0.9, 4, bucket=65_536, mode=1, order="ring", algo=2),
 ]
 
 
@@ -59,14 +65,16 @@ def _cases(world):
         return [c for c in CASES if c.order == "rank"]  # a + b is order-free: ring cases add nothing
     if world == 4:
         return [c for c in CASES if c.name in ("sma", "sma-copy-ssp", "sma-5-buckets", "sma-5-buckets-cross",
-                                               "sma-5-buckets-cross-stride", "sma-ring", "sma-ring-cross")]
+                                               "sma-5-buckets-cross-stride", "sma-ring", "sma-ring-cross", "sma-rsag",
+                                               "sma-rsag-buckets-cross", "sma-rsag-ring")]
     return [c for c in CASES if c.name in ("sma-copy-ssp", "sma-5-buckets-cross-stride", "ssgd-buckets",
-                                           "sma-ring")]
+                                           "sma-ring", "sma-rsag-buckets-cross", "sma-rsag-ring")]
 
 
 def _jobs(world):
     jobs = [("case", c.name) for c in _cases(world)]
     jobs += [("golden", gc["name"]) for gc in C.golden_cases(world)]
+    jobs += [("golden-rsag", gc["name"]) for gc in C.golden_cases(world)]
     return jobs + [("bn", "bn"), ("autotune", "autotune")]
 
 
@@ -86,8 +94,8 @@ def _rank_main(rank, world, jobs, uids, fake_dir, q):
                 assert L.cbx_set_allreduce_algorithm(g.c, A.ALLREDUCE_PEER) == A.CBX_ERR_UNSUPPORTED
                 if kind == "case":
                     res = C.run_case(g, world, [rank], case)
-                elif kind == "golden":
-                    res = {"bad": C.run_golden(g, world, [rank], goldens[name])}
+                elif kind.startswith("golden"):
+                    res = {"bad": C.run_golden(g, world, [rank], goldens[name], algo=2 if kind == "golden-rsag" else 0)}
                 elif kind == "bn":
                     res = {"bad": C.run_bn(g, world, [rank], poison=True)}
                 else:

@@ -19,7 +19,7 @@ pytestmark = pytest.mark.gpu
 
 
 def _run(n, R, alpha, momentum, copy_ids=(), first=0, held=(), sync=0, config=None, split=False,
-         bucket=0, steps=1, apply=None):
+         bucket=0, steps=1, apply=None, algo=0):
     st = O.make_state(n, 1, R, alpha, momentum)
     g = make_gpu(n, R, alpha, momentum, sync=sync)
     try:
@@ -30,6 +30,8 @@ def _run(n, R, alpha, momentum, copy_ids=(), first=0, held=(), sync=0, config=No
             g.set_kernel_occupancy(occ)
         if split:
             g.set_force_split(True)
+        if algo:
+            g.set_allreduce_algorithm(algo)
         if apply:
             g.set_apply_kernel_config(*apply)
         if bucket:
@@ -200,6 +202,17 @@ def test_split_apply_launch_shapes_identical(apply):
 
 def test_split_pipeline_buckets_and_copy():
     _run(300_001, 3, 0.1, 0.9, split=True, bucket=65_536, copy_ids=(0,), steps=2)
+
+
+@pytest.mark.parametrize("momentum", [0.0, 0.9])
+@pytest.mark.parametrize("bucket", [0, 65_536, 4096])
+def test_split_pipeline_reduce_scatter_one_rank(momentum, bucket):
+    # cbx_set_allreduce_algorithm(RSAG): reduce-scatter of acc + the control
+    # block's all-reduce, the base momentum on the rank's shard, all-gather,
+    # kernel B without momentum.  One rank: the shard is the whole bucket.
+    from crossbow_amd._lib import ALLREDUCE_RSAG
+    _run(300_001, 3, 0.1, momentum, split=True, bucket=bucket, copy_ids=(1,), steps=3, algo=ALLREDUCE_RSAG)
+    _run(4099, 2, 0.5, momentum, split=True, bucket=bucket, held=(0,), sync=1, steps=2, algo=ALLREDUCE_RSAG)
 
 
 @pytest.mark.parametrize("bucket", [4096, 1_000_000])
@@ -742,7 +755,8 @@ def test_concurrent_task_threads_and_barrier(pipeline):
 @pytest.mark.parametrize("momentum", [0.0, 0.9])
 @pytest.mark.parametrize("bucket", [65_536, 4096])
 @pytest.mark.parametrize("stride,group", [(1, 1), (2, 1), (3, 1), (2, 3), (1, 2), (3, 4)])
-def test_cross_step_pipeline(momentum, bucket, stride, group):
+@pytest.mark.parametrize("algo", [0, 2])  # all-reduce, reduce-scatter + all-gather
+def test_cross_step_pipeline(momentum, bucket, stride, group, algo):
     # cbx_set_pipeline_mode(1): kernels A on their own stream, each waiting
     # only for B of the same bucket in the previous step.  Eight steps with
     # Phase D requests, SSP holds, a host write between two steps (which
@@ -758,6 +772,7 @@ def test_cross_step_pipeline(momentum, bucket, stride, group):
         g.set_pipeline_mode(1)
         g.set_cross_wait_stride(stride)
         g.set_allreduce_group(group)  # all-reduces per comm-stream wait; mode 0 steps use it too
+        g.set_allreduce_algorithm(algo)
         upload(g, st)
         want = st.clone()
         plan = [{}, {"copy": 1}, {"hold": 2}, {}, {"write": 0}, {"mode": 0}, {"mode": 1, "copy": 2, "hold": 0},
@@ -830,6 +845,8 @@ def test_cross_step_pipeline_randomised_long_run():
                 g.set_pipeline_mode(rng.choice([0, 1]))
                 g.set_cross_wait_stride(rng.choice([1, 2, 3, 8]))
                 g.set_allreduce_group(rng.choice([1, 1, 2, 5]))
+            elif u < 0.34:
+                g.set_allreduce_algorithm(rng.choice([0, 2]))  # all-reduce / reduce-scatter + all-gather
             g.lockAny()
             g.synchronise(0, step + 1, 0, False)
             g.unlockAny()

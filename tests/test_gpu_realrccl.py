@@ -66,11 +66,14 @@ def share_uid(L, rank: int, path: str) -> bytes:
 
 def _jobs(world):
     names = {2: ["sma", "sma-copy-ssp", "sma-5-buckets", "sma-5-buckets-cross", "sma-no-momentum", "sma-staged",
-                 "sma-staged-dma", "ssgd", "ssgd-buckets"],
-             4: ["sma", "sma-copy-ssp", "sma-5-buckets", "sma-5-buckets-cross-stride", "sma-staged", "ssgd-buckets"],
-             8: ["sma-copy-ssp", "sma-5-buckets-cross-stride", "ssgd-buckets"]}[world]
+                 "sma-staged-dma", "ssgd", "ssgd-buckets", "sma-rsag", "sma-rsag-buckets-cross",
+                 "sma-rsag-no-momentum"],
+             4: ["sma", "sma-copy-ssp", "sma-5-buckets", "sma-5-buckets-cross-stride", "sma-staged", "ssgd-buckets",
+                 "sma-rsag", "sma-rsag-buckets-cross"],
+             8: ["sma-copy-ssp", "sma-5-buckets-cross-stride", "ssgd-buckets", "sma-rsag-buckets-cross"]}[world]
     jobs = [("case", n) for n in names]
     jobs += [("golden", gc["name"]) for gc in C.golden_cases(world)]
+    jobs += [("golden-rsag", gc["name"]) for gc in C.golden_cases(world)]
     return jobs + [("bn", "bn"), ("autotune", "autotune")]
 
 
@@ -88,8 +91,9 @@ def _rank_main(rank, world, jobs, d, q):
                 if kind == "case":
                     # "ring": the checker's tolerance mode (the loopback order is not used here)
                     res = C.run_case(g, world, [rank], dataclasses.replace(cases[name], order="rank" if exact else "ring"))
-                elif kind == "golden":
-                    res = {"bad": C.run_golden(g, world, [rank], goldens[name], exact=exact)}
+                elif kind.startswith("golden"):
+                    res = {"bad": C.run_golden(g, world, [rank], goldens[name], exact=exact,
+                                               algo=2 if kind == "golden-rsag" else 0)}
                 elif kind == "bn":
                     res = {"bad": C.run_bn(g, world, [rank], poison=True, exact=exact)}
                 else:
@@ -131,7 +135,7 @@ def test_real_rccl_ranks_on_one_gpu_vs_oracle(world):
         assert differs > 0, "RCCL's sums never left the oracle's order"
 
 
-def _full_size_main(rank, world, R, steps, mode, d, q):
+def _full_size_main(rank, world, R, steps, mode, algo, d, q):
     rank_env(rank)
     try:
         L, A = load_real()
@@ -141,6 +145,7 @@ def _full_size_main(rank, world, R, steps, mode, d, q):
             n = N_RESNET50
             C.setup_model(g, A, n, R, 0.9, 7, A.SYNC_BSP, 2 * world * R)
             g("cbx_set_pipeline_mode", mode)
+            g("cbx_set_allreduce_algorithm", algo)
             g("cbx_fill_synthetic", O.SEED)
             size = world * R
             mine = [i for i in range(size) if i % world == rank]
@@ -187,11 +192,12 @@ def _full_size_main(rank, world, R, steps, mode, d, q):
 
 
 @pytest.mark.timeout(300)
-@pytest.mark.parametrize("world,R,mode", [(4, 2, 0),   # C4: 2 replicas/GPU x 4
-                                          (8, 4, 1)])  # C5: 4 replicas/GPU x 8, cross-step pipeline
-def test_real_rccl_resnet50_full_size(world, R, mode):
+@pytest.mark.parametrize("world,R,mode,algo", [(4, 2, 0, 0),   # C4: 2 replicas/GPU x 4
+                                               (8, 4, 1, 0),   # C5: 4 replicas/GPU x 8, cross-step pipeline
+                                               (8, 4, 1, 2)])  # C5 through reduce-scatter / all-gather
+def test_real_rccl_resnet50_full_size(world, R, mode, algo):
     with tempfile.TemporaryDirectory(dir=C.loopback_dir(1 << 30)) as d:
-        res = _spawn(world, _full_size_main, lambda r: (r, world, R, 3, mode, d), timeout=280)
+        res = _spawn(world, _full_size_main, lambda r: (r, world, R, 3, mode, algo, d), timeout=280)
     for r in range(world):
         assert not res[r]["bad"], f"rank {r}: {res[r]['bad']}"
     assert len({res[r]["digest"] for r in range(world)}) == 1, "z / last differ across ranks at full size"
