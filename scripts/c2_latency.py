@@ -11,7 +11,9 @@ dispatch gap between launches is outside the HIP-event span).  If BW is at the
 big kernels' HBM rate, C2 (n = 1,111,946: 62 MB) is latency-bound and its
 0.44 fraction is t0, not a bandwidth problem.
 
-Writes gpurun_out/c2_latency.json; run it under rocprofv3 --kernel-trace to
+Contexts run one at a time (a host wait after each step): each context has
+its own stream, and overlapping launches would share HBM and inflate every
+HIP-event span.  Writes gpurun_out/c2_latency.json; run it under rocprofv3 --kernel-trace to
 see the dispatch gaps as well.
 """
 from __future__ import annotations
@@ -60,6 +62,7 @@ def main():
                 g.lockAny()
                 g.synchronise(0, clock, 0, False)
                 g.unlockAny()
+                g.wait()  # one context at a time: the contexts' streams would otherwise overlap in HBM
         for g in gs:
             g.wait()
         ms = [t for g in gs for t in g.timing_history(_lib.T_KERNEL)[-steps:]]

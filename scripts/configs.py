@@ -47,6 +47,11 @@ def make(model, R, mom, split):
 
 
 def run(gs, steps):
+    """`steps` barrier steps on every context in rotation.  Each context has
+    its own sync stream, so with several contexts each step is waited for
+    before the next context's starts: otherwise two contexts' kernels run at
+    once, share HBM, and each launch's HIP-event span is inflated (the
+    round-1 C2 "rotated" figure, 3.5 TB/s, was that artefact)."""
     clock = 0
     for _ in range(steps):
         for g in gs:
@@ -54,6 +59,8 @@ def run(gs, steps):
             g.lockAny()
             g.synchronise(0, clock, 0, False)
             g.unlockAny()
+            if len(gs) > 1:
+                g.wait()
     for g in gs:
         g.wait()
 
