@@ -62,7 +62,8 @@ def parse():
                    help="G>1: unpipelined steps before warm-up that time kernel A, the all-reduce and kernel B apart")
     p.add_argument("--force-split", action="store_true", help="use kernel A + all-reduce + B even at G=1")
     p.add_argument("--cpu-seconds", type=float, default=10.0)
-    p.add_argument("--cpu-elements", type=int, default=1 << 22)
+    p.add_argument("--cpu-elements", type=int, default=0,
+                   help="elements of the CPU baseline's state (0 = the full workload, n)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-staged", action="store_true")
     p.add_argument("--no-copy-ceiling", action="store_true")
@@ -90,10 +91,10 @@ def cpu_baseline_threads(args, n_full, threads):
     """Same replay with OpenBLAS on `threads` threads (no pinning): the
     'all cores' row of BASELINE.md 3, capped at the GPU box's CPU share."""
     from oracle import oracle as O
-    n = min(args.cpu_elements, n_full)
+    n = min(args.cpu_elements, n_full) if args.cpu_elements > 0 else n_full
     O.blas_open()
     O.blas_set_threads(threads)
-    st = O.make_state(n, 1, args.replicas, args.alpha, args.momentum)
+    st = O.make_state(n, 1, args.replicas, args.alpha, args.momentum, threads=threads)
     try:
         O.sma_step_blas(st)
         steps, t0 = 0, O.now()
@@ -143,10 +144,11 @@ def cpu_baseline(args, n_full):
     momentum, apply) on OpenBLAS, 1 thread bound to core 0 like TheCPU.bind(0)
     (clib-multigpu/CPU.c:39-52, BLAS.c:32), on a bounded sample."""
     from oracle import oracle as O
-    n = min(args.cpu_elements, n_full)
+    n = min(args.cpu_elements, n_full) if args.cpu_elements > 0 else n_full
     lib = O.blas_open()
     O.blas_set_threads(1)
-    st = O.make_state(n, 1, args.replicas, args.alpha, args.momentum)
+    threads = max(1, min(16, len(os.sched_getaffinity(0))))
+    st = O.make_state(n, 1, args.replicas, args.alpha, args.momentum, threads=threads)  # inputs only; timed on 1 thread
     O.bind_core(0)
     try:
         O.sma_step_blas(st)  # warm

@@ -149,9 +149,22 @@ class SmaState:
                         cp(self.s), cp(self.w), self.locked.copy(), self.copy.copy(), self.first)
 
 
-def make_state(n: int, G: int, R: int, alpha: float, momentum: float) -> SmaState:
-    """Synthetic inputs of BASELINE.md 2.3 for ``G`` devices x ``R`` replicas."""
+def make_state(n: int, G: int, R: int, alpha: float, momentum: float, threads: int = 1) -> SmaState:
+    """Synthetic inputs of BASELINE.md 2.3 for ``G`` devices x ``R`` replicas.
+    ``threads`` > 1 fills the buffers on that many threads (the C fill
+    releases the GIL); the values are the same."""
     size = G * R
+    if threads > 1:
+        from concurrent.futures import ThreadPoolExecutor
+        with ThreadPoolExecutor(threads) as ex:
+            zf = ex.submit(fill_normal, n, BUF_Z, 0.05)
+            lf = ex.submit(fill_normal, n, BUF_LAST, 0.001) if momentum > 0 else None
+            z = zf.result()
+            s = list(ex.map(lambda i: fill_normal(n, BUF_S0 + 2 * i, 0.01, z), range(size)))
+            w = list(ex.map(lambda i: fill_normal(n, BUF_W0 + 2 * i, 0.001, s[i]), range(size)))
+            last = lf.result() if lf is not None else None
+        return SmaState(G, size, n, alpha, momentum, [z.copy() for _ in range(G)],
+                        None if last is None else [last.copy() for _ in range(G)], s, w)
     z = fill_normal(n, BUF_Z, 0.05)
     last = fill_normal(n, BUF_LAST, 0.001) if momentum > 0 else None
     s, w = [], []
