@@ -232,6 +232,26 @@ struct Device {
   // this device's shard of D reduced; the other devices' streams wait on them.
   hipEvent_t peer_a = nullptr;
   hipEvent_t peer_r = nullptr;
+  // Stream-order check (cbx_set_order_check): timestamps of the last two
+  // split steps, by step parity, per bucket.  Only dispatch STOP
+  // timestamps are exact (a start event, like an event record after a stream
+  // wait, is a marker that may carry an earlier command's time), so each
+  // point is the end of a kernel: an empty probe dispatch right after each
+  // wait (before kernel A, before the collective, before kernel B), one
+  // right after the collective, and kernels A and B themselves.
+  struct OrderStep {
+    bool valid = false;
+    bool cont = false;  // continued the previous step bucket by bucket (mode 1, no join)
+    int64_t nb = 0;
+    std::vector<hipEvent_t> pa, a1, c0, c1, pb, b1;  // probe<A, A, probe<coll, probe>coll, probe<B, B
+  };
+  OrderStep ord[2];
+  // Owned timing events, 6 per bucket (pa, a1, c0, c1, pb, b1).  While the
+  // check is on, kernel A's and B's dispatches stop these instead of the
+  // reused bucket_acc / bucket_b, and the cross-stream waits use them too,
+  // so the two recorded steps keep their own timestamps.
+  std::vector<hipEvent_t> ord_pool[2];
+  unsigned ord_cur = 0;
   cbx::BnSegment *bn_table = nullptr;  // batch-norm averaging: segment table (device)
   size_t bn_table_bytes = 0;
   float *bn_scratch = nullptr;         // packed statistics, all-reduced
@@ -315,6 +335,11 @@ struct cbx_context {
   int staging_mode = CBX_STAGING_ZEROCOPY;  // cbx_synchronise_staged: zero-copy kernels or DMA copies
   cbx::LaunchConfig staged_cfg = cbx::staged_launch_config();
   bool peer_ready = false;     // hipDeviceEnablePeerAccess done between every pair of devices
+  bool order_check = false;    // record per-bucket timestamps of split steps (cbx_set_order_check)
+  // Fault injection for the order check's own test: $CBX_FAULT_SKIP_COMM_WAIT
+  // at context creation drops the comm stream's wait on kernel A, so the
+  // collective races its input (results are then wrong; tests only).
+  bool fault_skip_comm_wait = std::getenv("CBX_FAULT_SKIP_COMM_WAIT") != nullptr;
   // Bumped by every C-ABI call that may enqueue work on a sync stream other
   // than the barrier path itself: a cross-step pipelined step then joins the
   // whole sync stream instead of waiting bucket by bucket.
@@ -508,6 +533,8 @@ void close_device(Device &d) {
   if (d.a_stream) (void)hipStreamSynchronize(d.a_stream);
   for (hipEvent_t e : d.bucket_b) (void)hipEventDestroy(e);
   if (d.cross_entry) (void)hipEventDestroy(d.cross_entry);
+  for (auto &pool : d.ord_pool)
+    for (hipEvent_t e : pool) (void)hipEventDestroy(e);
   if (d.peer_a) (void)hipEventDestroy(d.peer_a);
   if (d.peer_r) (void)hipEventDestroy(d.peer_r);
   if (d.decision) (void)hipFree(d.decision);
@@ -831,6 +858,29 @@ int sma_step(cbx_context *c, int first) {
         }
       }
     }
+    // Stream-order check: a fresh set of per-bucket timestamps for this step.
+    const bool ocheck = c->order_check && c->timing;
+    for (size_t k = 0; ocheck && k < c->devs.size(); ++k) {
+      Device &d = c->devs[k];
+      HIP_TRY(hipSetDevice(d.hip_id));
+      d.ord_cur ^= 1u;
+      std::vector<hipEvent_t> &pool = d.ord_pool[d.ord_cur];
+      while ((int64_t)pool.size() < 6 * nb) {
+        hipEvent_t e;
+        HIP_TRY(hipEventCreate(&e));
+        pool.push_back(e);
+      }
+      Device::OrderStep &o = d.ord[d.ord_cur];
+      o.valid = true;
+      o.cont = cross && !join[k];
+      o.nb = nb;
+      o.pa.assign(pool.begin(), pool.begin() + nb);
+      o.c0.assign(pool.begin() + nb, pool.begin() + 2 * nb);
+      o.c1.assign(pool.begin() + 2 * nb, pool.begin() + 3 * nb);
+      o.pb.assign(pool.begin() + 3 * nb, pool.begin() + 4 * nb);
+      o.b1.assign(pool.begin() + 4 * nb, pool.begin() + 5 * nb);
+      o.a1.assign(pool.begin() + 5 * nb, pool.begin() + 6 * nb);
+    }
     // `wait_acc`: the comm stream first waits for kernel A of that bucket
     // (-1: no wait; an earlier all-reduce of the same group already waited
     // on a later bucket, which implies this one: A runs in order).
@@ -839,12 +889,17 @@ int sma_step(cbx_context *c, int first) {
       const int64_t len = std::min(b4, c->n4 - start);
       // common.c:14-54: grouped all-reduce, fp32 sum.  Bucket 0 also carries
       // the control block that sits right in front of the data.
-      if (on_comm && wait_acc >= 0) {
+      if (on_comm && wait_acc >= 0 && !c->fault_skip_comm_wait) {
         for (size_t k = 0; k < c->devs.size(); ++k) {
           Device &d = c->devs[k];
           HIP_TRY(hipSetDevice(d.hip_id));
-          HIP_TRY(hipStreamWaitEvent(d.comm_stream, d.bucket_acc[wait_acc], 0));
+          HIP_TRY(hipStreamWaitEvent(d.comm_stream, ocheck ? d.ord[d.ord_cur].a1[wait_acc] : d.bucket_acc[wait_acc], 0));
         }
+      }
+      for (size_t k = 0; ocheck && k < c->devs.size(); ++k) {
+        Device &d = c->devs[k];
+        HIP_TRY(hipSetDevice(d.hip_id));
+        HIP_TRY(cbx::launch_order_probe(on_comm ? d.comm_stream : d.stream, {nullptr, d.ord[d.ord_cur].c0[b]}));
       }
       if (rsag) {
         // Reduce-scatter form: shard g of the bucket (len / G float4s) is
@@ -902,6 +957,11 @@ int sma_step(cbx_context *c, int first) {
         }
         NCCL_TRY(ncclGroupEnd());
       }
+      for (size_t k = 0; ocheck && k < c->devs.size(); ++k) {
+        Device &d = c->devs[k];
+        HIP_TRY(hipSetDevice(d.hip_id));
+        HIP_TRY(cbx::launch_order_probe(on_comm ? d.comm_stream : d.stream, {nullptr, d.ord[d.ord_cur].c1[b]}));
+      }
       if (on_comm) {
         for (size_t k = 0; k < c->devs.size(); ++k) {
           Device &d = c->devs[k];
@@ -923,9 +983,16 @@ int sma_step(cbx_context *c, int first) {
         if (b == 0) t.start = ring_event(c, d, EV_START);
         if (!pipelined) t.stop = ring_event(c, d, EV_A);
         hipStream_t st = cross ? d.a_stream : d.stream;
-        if (cross && !join[k] && b % wait_stride == 0)  // B(b .. b+stride-1) of the last step
-          HIP_TRY(hipStreamWaitEvent(st, d.bucket_b[std::min<int64_t>(b + wait_stride - 1, nb - 1)], 0));
-        if (pipelined) t.stop = d.bucket_acc[b];
+        if (cross && !join[k] && b % wait_stride == 0) {  // B(b .. b+stride-1) of the last step
+          const int64_t w = std::min<int64_t>(b + wait_stride - 1, nb - 1);
+          HIP_TRY(hipStreamWaitEvent(st, ocheck ? d.ord[d.ord_cur ^ 1u].b1[w] : d.bucket_b[w], 0));
+        }
+        if (pipelined) t.stop = ocheck ? d.ord[d.ord_cur].a1[b] : d.bucket_acc[b];
+        if (ocheck) {
+          Device::OrderStep &o = d.ord[d.ord_cur];
+          HIP_TRY(cbx::launch_order_probe(st, {nullptr, o.pa[b]}));
+          o.a1[b] = t.stop;  // with timing on, A always carries a stop event (the pool's or the ring's)
+        }
         HIP_TRY(cbx::launch_sma_accumulate(offset_args(args[k], start, len), b == 0, cfg, st, t));
       }
       return CBX_OK;
@@ -951,7 +1018,13 @@ int sma_step(cbx_context *c, int first) {
           a.decision = d.decision + (d.cross_parity & 1u);
         }
         const bool in_dispatch = cross && !t.stop;
-        if (in_dispatch) t.stop = d.bucket_b[b];
+        if (in_dispatch) t.stop = ocheck ? d.ord[d.ord_cur].b1[b] : d.bucket_b[b];
+        if (ocheck) {
+          Device::OrderStep &o = d.ord[d.ord_cur];
+          HIP_TRY(cbx::launch_order_probe(d.stream, {nullptr, o.pb[b]}));
+          if (!t.stop) t.stop = o.b1[b];
+          o.b1[b] = t.stop;
+        }
         HIP_TRY(cbx::launch_sma_apply(a, mom && !rsag, cfg, d.stream, t));
         if (cross && !in_dispatch) HIP_TRY(hipEventRecord(d.bucket_b[b], d.stream));
       }
@@ -1501,6 +1574,64 @@ int load_buffer(float *dev, size_t bytes, const std::string &path, std::vector<c
   tmp.resize(bytes);
   TRY(read_file(path, tmp.data(), bytes));
   HIP_TRY(hipMemcpy(dev, tmp.data(), bytes, hipMemcpyHostToDevice));
+  return CBX_OK;
+}
+
+// ---------------------------------------------------------------------------
+// Stream-order check (cbx_set_order_check / cbx_check_order).  From the
+// timestamps a split step recorded, per bucket k on every device:
+//   the collective of k started after kernel A(k) ended;
+//   kernel B(k) started after the collective of k ended, and after B(k-1);
+// and between two consecutive split steps: kernel A(k) of the later step
+// started after B(k) of the earlier one (continued bucket by bucket), or
+// A(0) after the earlier step's last B (joined).  "Started after X ended"
+// is checked as "the probe dispatched right after the wait ended after X
+// ended": both are exact dispatch-completion timestamps, and the probe
+// cannot run before its stream's wait is satisfied (slack: kOrderSlackMs).
+// ---------------------------------------------------------------------------
+constexpr float kOrderSlackMs = 0.0005f;
+
+int order_fail(int64_t k, const char *what, float gap_ms) {
+  return fail(CBX_ERR_STATE, "stream order violated at bucket %lld: %s (%.2f us early)", (long long)k, what,
+              -gap_ms * 1e3f);
+}
+
+int check_order_step(const Device::OrderStep &o) {
+  HIP_TRY(hipEventSynchronize(o.b1[o.nb - 1]));
+  auto at = [&](hipEvent_t e, float *ms) { return hipEventElapsedTime(ms, o.pa[0], e); };
+  float prev_b1 = -1e30f;
+  for (int64_t k = 0; k < o.nb; ++k) {
+    float a1, c0, c1, pb, b1;
+    HIP_TRY(at(o.a1[k], &a1));
+    HIP_TRY(at(o.c0[k], &c0));
+    HIP_TRY(at(o.c1[k], &c1));
+    HIP_TRY(at(o.pb[k], &pb));
+    HIP_TRY(at(o.b1[k], &b1));
+    if (c0 - a1 < -kOrderSlackMs) return order_fail(k, "the collective started before kernel A ended", c0 - a1);
+    if (pb - c1 < -kOrderSlackMs) return order_fail(k, "kernel B started before its collective ended", pb - c1);
+    if (pb - prev_b1 < -kOrderSlackMs) return order_fail(k, "kernel B started before the previous B ended", pb - prev_b1);
+    prev_b1 = b1;
+  }
+  return CBX_OK;
+}
+
+int check_order_pair(const Device::OrderStep &p, const Device::OrderStep &q) {
+  HIP_TRY(hipEventSynchronize(q.b1[q.nb - 1]));
+  auto at = [&](hipEvent_t e, float *ms) { return hipEventElapsedTime(ms, p.pa[0], e); };
+  if (q.cont && q.nb == p.nb) {
+    for (int64_t k = 0; k < q.nb; ++k) {
+      float pa, b1;
+      HIP_TRY(at(q.pa[k], &pa));
+      HIP_TRY(at(p.b1[k], &b1));
+      if (pa - b1 < -kOrderSlackMs)
+        return order_fail(k, "kernel A of the next step started before this step's kernel B ended", pa - b1);
+    }
+    return CBX_OK;
+  }
+  float pa, b1;
+  HIP_TRY(at(q.pa[0], &pa));
+  HIP_TRY(at(p.b1[p.nb - 1], &b1));
+  if (pa - b1 < -kOrderSlackMs) return order_fail(0, "the next step started before this step ended", pa - b1);
   return CBX_OK;
 }
 
@@ -2791,6 +2922,36 @@ int cbx_set_timing(cbx_context *c, int enable) {
     }
   }
   return CBX_OK;
+}
+
+int cbx_set_order_check(cbx_context *c, int enable) {
+  // check_ctx counts a foreign op: the next step joins the whole stream, so
+  // no cross-step wait spans a change of the events the waits use.
+  TRY(check_ctx(c));
+  if (enable && !c->timing) TRY(cbx_set_timing(c, 1));
+  c->order_check = enable != 0;
+  for (Device &d : c->devs)
+    for (Device::OrderStep &o : d.ord) o.valid = false;
+  return CBX_OK;
+}
+
+int cbx_check_order(cbx_context *c) {
+  TRY(check_ctx_q(c));
+  if (!c->order_check) return fail(CBX_ERR_STATE, "stream-order checking is off (cbx_set_order_check)");
+  int checked = 0;
+  for (Device &d : c->devs) {
+    HIP_TRY(hipSetDevice(d.hip_id));
+    Device::OrderStep &q = d.ord[d.ord_cur];      // the latest split step
+    Device::OrderStep &p = d.ord[d.ord_cur ^ 1];  // the one before it
+    for (Device::OrderStep *o : {&p, &q})
+      if (o->valid) {
+        TRY(check_order_step(*o));
+        ++checked;
+      }
+    if (p.valid && q.valid) TRY(check_order_pair(p, q));
+    p.valid = q.valid = false;
+  }
+  return checked;
 }
 
 int cbx_last_timing(cbx_context *c, int local, float *ms) {

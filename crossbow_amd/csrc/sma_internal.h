@@ -184,6 +184,9 @@ hipError_t launch_sma_apply(const SmaArgs &a, bool momentum,
 // Reduce-scatter form (cbx_set_allreduce_algorithm RSAG), on this rank's
 // shard of a bucket (a.n4 float4s, any count): last = fma(0.9, last, D).
 hipError_t launch_sma_shard_momentum(const SmaArgs &a, const LaunchConfig &cfg, hipStream_t stream, Timing t = {});
+// An empty dispatch whose own timestamps mark a point on `stream` (the
+// stream-order check, cbx_set_order_check).
+hipError_t launch_order_probe(hipStream_t stream, Timing t);
 // Host-staged step through zero-copy (cbx_synchronise_staged, staging mode
 // CBX_STAGING_ZEROCOPY): the kernels read their inputs straight from the
 // pinned host mirror over PCIe and write their outputs to the host mirror AND

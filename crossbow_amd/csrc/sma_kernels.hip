@@ -985,6 +985,17 @@ hipError_t launch_sma_apply(const SmaArgs &a, bool momentum, const LaunchConfig 
   return momentum ? apply_u<true, 0>(a, cfg, stream, t) : apply_u<false, 0>(a, cfg, stream, t);
 }
 
+// An empty one-wave kernel whose dispatch timestamps mark a point on a stream
+// (the stream-order check's collective start / end, cbx_set_order_check):
+// unlike an event record, a dispatch after a stream wait is timestamped when
+// it really runs.
+__global__ void order_probe_kernel() {}
+
+hipError_t launch_order_probe(hipStream_t stream, Timing t) {
+  hipExtLaunchKernelGGL(order_probe_kernel, dim3(1), dim3(64), 0, stream, t.start, t.stop, 0);
+  return hipGetLastError();
+}
+
 hipError_t launch_sma_shard_momentum(const SmaArgs &a, const LaunchConfig &cfg0, hipStream_t stream, Timing t) {
   LaunchConfig cfg = cfg0;
   cfg.unroll = 1;

@@ -398,6 +398,14 @@ class TheGPU:
         """Split path: buckets all-reduced behind one wait on the group's last kernel A."""
         check(self._L.cbx_set_allreduce_group(self._ctx, group))
 
+    def set_order_check(self, enable: bool) -> None:
+        """Record per-bucket timestamps of split steps (turns timing on); see check_order."""
+        check(self._L.cbx_set_order_check(self._ctx, 1 if enable else 0))
+
+    def check_order(self) -> int:
+        """Verify the stream order of the last two split steps; returns the steps checked."""
+        return check(self._L.cbx_check_order(self._ctx))
+
     def set_allreduce_algorithm(self, algorithm: int) -> None:
         """ALLREDUCE_RCCL (default), ALLREDUCE_PEER (one process over every device: peer reads over xGMI)
         or ALLREDUCE_RSAG (reduce-scatter, momentum on the shard, all-gather)."""

@@ -302,6 +302,20 @@ int cbx_step_event (cbx_context *ctx, int local, void **event);
 #define CBX_T_COUNT     6
 /* When enabled, HIP events bracket each launch on the sync stream.       */
 int cbx_set_timing (cbx_context *ctx, int enable);
+/* Stream-order check, a debug aid (event-ordering assertions).
+ * When on (it turns timing on too), every split step -- kernel A /
+ * collective / kernel B per bucket, G > 1 or forced -- records per-bucket
+ * timestamps of its last two steps.  cbx_check_order then blocks on them
+ * and verifies, per device, that each bucket's collective started after
+ * its kernel A ended, that kernel B started after its collective and after
+ * the previous B, and that the later step's kernel A(k) started after the
+ * earlier step's B(k) (or its last B, when the later step joined the whole
+ * stream).  Returns the number of steps checked (0..2 per device), or
+ * CBX_ERR_STATE naming the first violation.  Checked steps are consumed; to
+ * check cross-step overlap, run two steps back to back between checks.
+ * The peer-read and host-staged steps are not recorded.                   */
+int cbx_set_order_check (cbx_context *ctx, int enable);
+int cbx_check_order (cbx_context *ctx);
 /* Milliseconds of the last step on local device `local`, CBX_T_COUNT floats
  * (blocks on the recorded events); -1 for a span the step did not have.   */
 int cbx_last_timing (cbx_context *ctx, int local, float *ms);

@@ -860,3 +860,64 @@ def test_cross_step_pipeline_randomised_long_run():
         compare_states(download(g, st), want)
     finally:
         g.free()
+
+
+@pytest.mark.parametrize("mode,stride,group,algo", [(0, 1, 1, 0), (1, 1, 1, 0), (1, 2, 2, 0), (0, 1, 3, 2),
+                                                    (1, 2, 1, 2)])
+def test_stream_order_check(mode, stride, group, algo):
+    # cbx_set_order_check: every split step records per-bucket timestamps
+    # (kernel A, the collective, kernel B); cbx_check_order after every two
+    # back-to-back steps verifies the bucket pipeline's ordering and, in
+    # mode 1, that each A(k) of the second step began after B(k) of the first.
+    n, R = 300_001, 3
+    st = O.make_state(n, 1, R, 0.1, 0.9)
+    g = make_gpu(n, R, 0.1, 0.9)
+    try:
+        g.set_force_split(True)
+        g.set_bucket_elements(65_536)
+        g.set_pipeline_mode(mode)
+        g.set_cross_wait_stride(stride)
+        g.set_allreduce_group(group)
+        g.set_allreduce_algorithm(algo)
+        g.set_order_check(True)
+        upload(g, st)
+        want = st.clone()
+        for step in range(8):
+            want.locked[:] = 1
+            g.lockAny()
+            g.synchronise(0, step + 1, 0, False)
+            g.unlockAny()
+            O.sma_step(want)
+            if step % 2 == 1:
+                assert g.check_order() == 2
+        g.wait()
+        compare_states(download(g, st), want)
+        assert g.check_order() == 0  # nothing new since the last check
+    finally:
+        g.free()
+
+
+def test_stream_order_check_detects_a_race(monkeypatch):
+    # Fault injection ($CBX_FAULT_SKIP_COMM_WAIT at context creation): the
+    # comm stream no longer waits for kernel A, so each bucket's collective
+    # reads acc while kernel A is still writing it.  The order check must
+    # name that race.
+    from crossbow_amd import CbxError
+    monkeypatch.setenv("CBX_FAULT_SKIP_COMM_WAIT", "1")
+    n = 25_557_032
+    g = make_gpu(n, 8, 0.1, 0.9)
+    monkeypatch.delenv("CBX_FAULT_SKIP_COMM_WAIT")
+    try:
+        g.set_force_split(True)
+        g.set_bucket_elements(-(-n // 4))
+        g.fill_synthetic(7)
+        g.set_order_check(True)
+        for step in range(2):
+            g.lockAny()
+            g.synchronise(0, step + 1, 0, False)
+            g.unlockAny()
+        with pytest.raises(CbxError, match="the collective started before kernel A ended"):
+            g.check_order()
+        g.wait()
+    finally:
+        g.free()

@@ -11,6 +11,8 @@ the loopback tests (test_gpu_multirank.py) only stand in for:
 * RCCL's own ncclAllReduce with nranks > 1: its kernels run asynchronously
   on the comm stream beside kernels A and B, with its proxy threads, and sum
   in its own order, not rank order;
+* the stream-order check (cbx_check_order) of the bucketed pipeline while
+  RCCL's kernels run beside kernels A and B;
 * so the G > 1 tolerance (rtol 1e-5 / atol 1e-6) is checked
   against the oracle wherever RCCL's order differs from it (G >= 3), z and
   last must come out bitwise identical on every rank (sma.c:168-174), and at
@@ -74,7 +76,35 @@ def _jobs(world):
     jobs = [("case", n) for n in names]
     jobs += [("golden", gc["name"]) for gc in C.golden_cases(world)]
     jobs += [("golden-rsag", gc["name"]) for gc in C.golden_cases(world)]
+    jobs += [("order", "order-all-reduce"), ("order", "order-rsag")]
     return jobs + [("bn", "bn"), ("autotune", "autotune")]
+
+
+def run_order(g, world, algo):
+    """The stream-order check (cbx_set_order_check) under real RCCL, whose
+    collective runs asynchronously beside kernels A and B: bucketed, cross-step
+    pipeline with wait stride 2 and all-reduce groups of 2, checked after every
+    two back-to-back steps."""
+    A = g.A
+    C.setup_model(g, A, 300_007, 2, 0.9, 7, A.SYNC_BSP, 4 * world)
+    g("cbx_set_bucket_elements", ctypes.c_longlong(65_536))
+    g("cbx_set_pipeline_mode", 1)
+    g("cbx_set_cross_wait_stride", 2)
+    g("cbx_set_allreduce_group", 2)
+    g("cbx_set_allreduce_algorithm", algo)
+    g("cbx_fill_synthetic", 5)
+    g("cbx_set_order_check", 1)
+    bad = []
+    for step in range(6):
+        g("cbx_lock_any")
+        g("cbx_synchronise", 0, step + 1, 0, 0)
+        g("cbx_unlock_any")
+        if step % 2 == 1:
+            n = g("cbx_check_order")
+            if n != 2:
+                bad.append(f"order check after step {step} covered {n} steps, not 2")
+    g("cbx_wait")
+    return bad
 
 
 def _rank_main(rank, world, jobs, d, q):
@@ -94,6 +124,8 @@ def _rank_main(rank, world, jobs, d, q):
                 elif kind.startswith("golden"):
                     res = {"bad": C.run_golden(g, world, [rank], goldens[name], exact=exact,
                                                algo=2 if kind == "golden-rsag" else 0)}
+                elif kind == "order":
+                    res = {"bad": run_order(g, world, 2 if name == "order-rsag" else 0)}
                 elif kind == "bn":
                     res = {"bad": C.run_bn(g, world, [rank], poison=True, exact=exact)}
                 else:
