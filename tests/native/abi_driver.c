@@ -243,13 +243,20 @@ int main (void) {
 	EXPECT (cbx_set_pipeline_mode (c, 2) == CBX_ERR_INVALID);
 	EXPECT (cbx_set_pipeline_mode (c, -1) == CBX_ERR_INVALID);
 	EXPECT (cbx_set_cross_wait_stride (c, 0) == CBX_ERR_INVALID);
-	for (int clock = 3; clock < 9; ++clock) {
+	EXPECT (cbx_check_order (c) == CBX_ERR_STATE);  /* not enabled */
+	EXPECT (cbx_set_allreduce_algorithm (c, 3) == CBX_ERR_INVALID);
+	for (int clock = 3; clock < 13; ++clock) {
 		if (clock == 5) CHECK (cbx_replica_set_copy (c, 1, 1));
 		if (clock == 6) CHECK (cbx_set_pipeline_mode (c, 0));  /* back to within-step buckets */
 		if (clock == 7) CHECK (cbx_set_cross_wait_stride (c, 3));
+		if (clock == 8) CHECK (cbx_set_order_check (c, 1));
+		if (clock == 9) CHECK (cbx_set_pipeline_mode (c, 1));
+		if (clock == 10) CHECK (cbx_set_allreduce_algorithm (c, CBX_ALLREDUCE_RSAG));
+		if (clock == 12) CHECK (cbx_set_order_check (c, 0));
 		CHECK (cbx_lock_any (c));
 		CHECK (cbx_synchronise (c, 0, clock, 0, 0));
 		CHECK (cbx_unlock_any (c));
+		if (clock == 9 || clock == 11) EXPECT (cbx_check_order (c) == 2);
 	}
 	CHECK (cbx_wait (c));
 	CHECK (cbx_free (c));
