@@ -280,6 +280,9 @@ struct Device {
   static constexpr int kRing = 1024;
   std::vector<hipEvent_t> ring;
   std::vector<char> ring_split;
+  // 1: this slot recorded no START; its step queued right behind the previous
+  // slot's fused step, whose stop event stands in as its start (ring_start).
+  std::vector<char> ring_from_prev;
   int ring_pos = 0;
   int ring_count = 0;
 };
@@ -559,6 +562,37 @@ hipEvent_t ring_event(cbx_context *c, Device &d, int ev) {
   return d.ring[(size_t)d.ring_pos * 4 + ev];
 }
 
+// The START event for a fused step's dispatch (kind 0).  A dispatch start
+// event is a marker packet that costs the stream ~4.5 us per launch, while a
+// stop event costs nothing (scripts/event_ts_probe.hip: 20.8 vs 16.4 us per
+// back-to-back launch).  When the previous slot is a fused step whose stop
+// has not completed yet, this dispatch queues right behind it on the same
+// stream, so that stop stands in as this step's start and no marker is
+// added; otherwise (an idle GPU, another kind of step) START is recorded.
+hipEvent_t fused_start_event(cbx_context *c, Device &d) {
+  if (!c->timing || d.ring.empty()) return nullptr;
+  const int slot = d.ring_pos;
+  d.ring_from_prev[slot] = 0;
+  if (d.ring_count > 0) {
+    const int prev = (slot + Device::kRing - 1) % Device::kRing;
+    if (d.ring_split[prev] == 0 && hipEventQuery(d.ring[(size_t)prev * 4 + EV_A]) == hipErrorNotReady) {
+      (void)hipGetLastError();  // hipEventQuery leaves NotReady as the thread's last error
+      d.ring_from_prev[slot] = 1;
+      return nullptr;
+    }
+    (void)hipGetLastError();
+  }
+  return d.ring[(size_t)slot * 4 + EV_START];
+}
+
+// The event that opens ring slot `slot`: its START, or the previous slot's
+// stop when the step was enqueued behind it (fused_start_event).
+hipEvent_t ring_start(Device &d, int slot) {
+  if (!d.ring_from_prev.empty() && d.ring_from_prev[slot])
+    return d.ring[(size_t)((slot + Device::kRing - 1) % Device::kRing) * 4 + EV_A];
+  return d.ring[(size_t)slot * 4 + EV_START];
+}
+
 // Record a timing marker when timing is enabled.  Step events (START..B) go
 // to the current ring slot, staging events to the fixed ones.
 int mark(cbx_context *c, Device &d, int ev) {
@@ -577,6 +611,7 @@ int mark(cbx_context *c, Device &d, int ev) {
 void ring_advance(cbx_context *c, Device &d, int kind) {
   if (!c->timing || d.ring.empty()) return;
   d.ring_split[d.ring_pos] = (char)kind;
+  if (kind != 0) d.ring_from_prev[d.ring_pos] = 0;
   d.ring_pos = (d.ring_pos + 1) % Device::kRing;
   if (d.ring_count < Device::kRing) d.ring_count++;
 }
@@ -585,7 +620,8 @@ void ring_advance(cbx_context *c, Device &d, int kind) {
 int ring_span(Device &d, int slot, int a, int b, float *out) {
   *out = -1.0f;
   HIP_TRY(hipEventSynchronize(d.ring[(size_t)slot * 4 + b]));
-  HIP_TRY(hipEventElapsedTime(out, d.ring[(size_t)slot * 4 + a], d.ring[(size_t)slot * 4 + b]));
+  hipEvent_t from = a == EV_START ? ring_start(d, slot) : d.ring[(size_t)slot * 4 + a];
+  HIP_TRY(hipEventElapsedTime(out, from, d.ring[(size_t)slot * 4 + b]));
   return CBX_OK;
 }
 
@@ -785,7 +821,7 @@ int sma_step(cbx_context *c, int first) {
     // The dispatch timestamps its own (start, stop) ring events: no marker
     // packets between steps (each costs ~3 us of stream time, membench v4).
     HIP_TRY(cbx::launch_sma_fused(args[0], mom, copies_total > 0, cfg, d.stream,
-                                  {ring_event(c, d, EV_START), step_stop_event(c, d, EV_A)}));
+                                  {fused_start_event(c, d), step_stop_event(c, d, EV_A)}));
     ring_advance(c, d, 0);
     d.cross_valid = false;
     c->last_step_split = false;
@@ -2417,7 +2453,7 @@ static int default_step(cbx_context *c, int first) {
   cbx::LaunchConfig cfg = c->broadcast_cfg;
   cfg.num_cus = d.num_cus;
   cfg.blocks_per_cu = 0;
-  HIP_TRY(cbx::launch_broadcast(a, cfg, d.stream, {ring_event(c, d, EV_START), step_stop_event(c, d, EV_A)}));
+  HIP_TRY(cbx::launch_broadcast(a, cfg, d.stream, {fused_start_event(c, d), step_stop_event(c, d, EV_A)}));
   ring_advance(c, d, 0);
   c->last_step_split = false;
   return finish_step(c);
@@ -2918,6 +2954,7 @@ int cbx_set_timing(cbx_context *c, int enable) {
       HIP_TRY(hipSetDevice(d.hip_id));
       d.ring.resize((size_t)Device::kRing * 4, nullptr);
       d.ring_split.assign(Device::kRing, 0);
+      d.ring_from_prev.assign(Device::kRing, 0);
       for (hipEvent_t &e : d.ring) HIP_TRY(hipEventCreate(&e));
     }
   }

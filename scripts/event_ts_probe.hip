@@ -9,6 +9,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
+#include <vector>
 
 #define CK(x)                                                                   \
   do {                                                                          \
@@ -54,6 +55,41 @@ int main() {
     CK(hipEventElapsedTime(&r, ref, er));
     std::printf("{\"round\":%d,\"K_stop_dispatch_ms\":%.4f,\"K_stop_record_ms\":%.4f,\"probe_stop_dispatch_ms\":%.4f,"
                 "\"probe_then_record_ms\":%.4f}\n", round, k, k2, p, r);
+  }
+  // Start events: exact, or a marker carrying the previous command's end?
+  // And what does a per-launch (start, stop) pair cost back to back?
+  hipEvent_t e1, es2, e2, t0, t1;
+  CK(hipEventCreate(&e1));
+  CK(hipEventCreate(&es2));
+  CK(hipEventCreate(&e2));
+  CK(hipEventCreate(&t0));
+  CK(hipEventCreate(&t1));
+  for (int round = 0; round < 3; ++round) {
+    hipExtLaunchKernelGGL(stream_kernel, dim3(1024), dim3(256), 0, s1, nullptr, e1, 0, b, a, n);
+    hipExtLaunchKernelGGL(stream_kernel, dim3(1024), dim3(256), 0, s1, es2, e2, 0, a, b, n);
+    CK(hipDeviceSynchronize());
+    float gap, dur;
+    CK(hipEventElapsedTime(&gap, e1, es2));
+    CK(hipEventElapsedTime(&dur, es2, e2));
+    std::printf("{\"round\":%d,\"start_after_prev_stop_us\":%.2f,\"k2_start_to_stop_ms\":%.4f}\n", round, gap * 1e3,
+                dur);
+  }
+  std::vector<hipEvent_t> ev(100);
+  for (auto &e : ev) CK(hipEventCreate(&e));
+  const long m = 1L << 22;  // 64 MiB per buffer: ~20 us kernels, so per-launch costs show
+  for (int round = 0; round < 3; ++round) {
+    for (int mode = 0; mode < 3; ++mode) {  // 0 no events, 1 stop only, 2 start + stop
+      CK(hipEventRecord(t0, s1));
+      for (int i = 0; i < 50; ++i)
+        hipExtLaunchKernelGGL(stream_kernel, dim3(1024), dim3(256), 0, s1, mode == 2 ? ev[2 * i] : nullptr,
+                              mode >= 1 ? ev[2 * i + 1] : nullptr, 0, b, a, m);
+      CK(hipEventRecord(t1, s1));
+      CK(hipDeviceSynchronize());
+      float ms;
+      CK(hipEventElapsedTime(&ms, t0, t1));
+      std::printf("{\"round\":%d,\"events\":\"%s\",\"us_per_launch\":%.2f}\n", round,
+                  mode == 0 ? "none" : mode == 1 ? "stop" : "start+stop", ms * 1e3 / 50);
+    }
   }
   return 0;
 }
