@@ -233,12 +233,11 @@ struct Device {
   hipEvent_t peer_a = nullptr;
   hipEvent_t peer_r = nullptr;
   // Stream-order check (cbx_set_order_check): timestamps of the last two
-  // split steps, by step parity, per bucket.  Only dispatch STOP
-  // timestamps are exact (a start event, like an event record after a stream
-  // wait, is a marker that may carry an earlier command's time), so each
-  // point is the end of a kernel: an empty probe dispatch right after each
-  // wait (before kernel A, before the collective, before kernel B), one
-  // right after the collective, and kernels A and B themselves.
+  // split steps, by step parity, per bucket.  Every point is the stop
+  // timestamp of a dispatch (a start event is a marker packet of its own):
+  // an empty probe dispatch right after each wait (before kernel A, before
+  // the collective, before kernel B), one right after the collective, and
+  // kernels A and B themselves.
   struct OrderStep {
     bool valid = false;
     bool cont = false;  // continued the previous step bucket by bucket (mode 1, no join)
