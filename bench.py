@@ -200,6 +200,13 @@ def bench_optimiser(gpu, torch, n, args, rounds=10):
 
 def main():
     args = parse()
+    # stdout carries the ONE JSON line and nothing else: native libraries
+    # print banners there (RCCL's "RCCL version : ..." at communicator init),
+    # so fd 1 is pointed at stderr for the run and the result goes to a
+    # duplicate of the original stdout.
+    sys.stdout.flush()
+    result_out = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
     from crossbow_amd import dist as D
     rank, world, local_rank = D.env_rank()
     if args.rehearse_one_gpu:
@@ -436,7 +443,7 @@ def main():
 
     gpu.free()
     if rank == 0:
-        print(json.dumps(result), flush=True)
+        print(json.dumps(result), file=result_out, flush=True)
     D.finalize(world)
 
 

@@ -282,6 +282,7 @@ struct Device {
   // 1: this slot recorded no START; its step queued right behind the previous
   // slot's fused step, whose stop event stands in as its start (ring_start).
   std::vector<char> ring_from_prev;
+  bool start_chosen = false;  // step_start_event decided this slot's ring_from_prev
   int ring_pos = 0;
   int ring_count = 0;
 };
@@ -561,34 +562,45 @@ hipEvent_t ring_event(cbx_context *c, Device &d, int ev) {
   return d.ring[(size_t)d.ring_pos * 4 + ev];
 }
 
-// The START event for a fused step's dispatch (kind 0).  A dispatch start
-// event is a marker packet that costs the stream ~4.5 us per launch, while a
-// stop event costs nothing (scripts/event_ts_probe.hip: 20.8 vs 16.4 us per
-// back-to-back launch).  When the previous slot is a fused step whose stop
-// has not completed yet, this dispatch queues right behind it on the same
-// stream, so that stop stands in as this step's start and no marker is
-// added; otherwise (an idle GPU, another kind of step) START is recorded.
-hipEvent_t fused_start_event(cbx_context *c, Device &d) {
+// The stop event of ring slot `slot`'s step: EV_A for a fused step (kind 0),
+// EV_B for a split one.
+hipEvent_t ring_stop(Device &d, int slot) {
+  return d.ring[(size_t)slot * 4 + (d.ring_split[slot] == 0 ? EV_A : EV_B)];
+}
+
+// The START event for the first dispatch of a fused (kind 0) or pipelined
+// split (kind 2) step.  A dispatch start event is a marker packet that costs
+// the stream ~4.5 us per launch, while a stop event costs nothing
+// (scripts/event_ts_probe.hip: 20.8 vs 16.4 us per back-to-back launch).
+// When the previous slot is a step of the same kind whose stop has not
+// completed yet, this step is enqueued behind a busy GPU: that stop stands in
+// as this step's start (a fused step queues right behind it on the same
+// stream; a pipelined step's span becomes its stop-to-stop share of the
+// pipeline) and no marker is added.  Otherwise (an idle GPU, another kind of
+// step) START is recorded.
+hipEvent_t step_start_event(cbx_context *c, Device &d, int kind) {
   if (!c->timing || d.ring.empty()) return nullptr;
   const int slot = d.ring_pos;
   d.ring_from_prev[slot] = 0;
   if (d.ring_count > 0) {
     const int prev = (slot + Device::kRing - 1) % Device::kRing;
-    if (d.ring_split[prev] == 0 && hipEventQuery(d.ring[(size_t)prev * 4 + EV_A]) == hipErrorNotReady) {
-      (void)hipGetLastError();  // hipEventQuery leaves NotReady as the thread's last error
+    const bool busy = d.ring_split[prev] == kind && hipEventQuery(ring_stop(d, prev)) == hipErrorNotReady;
+    (void)hipGetLastError();  // hipEventQuery leaves NotReady as the thread's last error
+    if (busy) {
       d.ring_from_prev[slot] = 1;
+      d.start_chosen = true;
       return nullptr;
     }
-    (void)hipGetLastError();
   }
+  d.start_chosen = true;
   return d.ring[(size_t)slot * 4 + EV_START];
 }
 
 // The event that opens ring slot `slot`: its START, or the previous slot's
-// stop when the step was enqueued behind it (fused_start_event).
+// stop when the step was enqueued behind it (step_start_event).
 hipEvent_t ring_start(Device &d, int slot) {
   if (!d.ring_from_prev.empty() && d.ring_from_prev[slot])
-    return d.ring[(size_t)((slot + Device::kRing - 1) % Device::kRing) * 4 + EV_A];
+    return ring_stop(d, (slot + Device::kRing - 1) % Device::kRing);
   return d.ring[(size_t)slot * 4 + EV_START];
 }
 
@@ -610,7 +622,8 @@ int mark(cbx_context *c, Device &d, int ev) {
 void ring_advance(cbx_context *c, Device &d, int kind) {
   if (!c->timing || d.ring.empty()) return;
   d.ring_split[d.ring_pos] = (char)kind;
-  if (kind != 0) d.ring_from_prev[d.ring_pos] = 0;
+  if (!d.start_chosen) d.ring_from_prev[d.ring_pos] = 0;  // a path that records START itself
+  d.start_chosen = false;
   d.ring_pos = (d.ring_pos + 1) % Device::kRing;
   if (d.ring_count < Device::kRing) d.ring_count++;
 }
@@ -820,7 +833,7 @@ int sma_step(cbx_context *c, int first) {
     // The dispatch timestamps its own (start, stop) ring events: no marker
     // packets between steps (each costs ~3 us of stream time, membench v4).
     HIP_TRY(cbx::launch_sma_fused(args[0], mom, copies_total > 0, cfg, d.stream,
-                                  {fused_start_event(c, d), step_stop_event(c, d, EV_A)}));
+                                  {step_start_event(c, d, 0), step_stop_event(c, d, EV_A)}));
     ring_advance(c, d, 0);
     d.cross_valid = false;
     c->last_step_split = false;
@@ -1015,7 +1028,7 @@ int sma_step(cbx_context *c, int first) {
         cbx::LaunchConfig cfg = c->cfg;
         cfg.num_cus = d.num_cus;
         cbx::Timing t;
-        if (b == 0) t.start = ring_event(c, d, EV_START);
+        if (b == 0) t.start = pipelined ? step_start_event(c, d, 2) : ring_event(c, d, EV_START);
         if (!pipelined) t.stop = ring_event(c, d, EV_A);
         hipStream_t st = cross ? d.a_stream : d.stream;
         if (cross && !join[k] && b % wait_stride == 0) {  // B(b .. b+stride-1) of the last step
@@ -2452,7 +2465,7 @@ static int default_step(cbx_context *c, int first) {
   cbx::LaunchConfig cfg = c->broadcast_cfg;
   cfg.num_cus = d.num_cus;
   cfg.blocks_per_cu = 0;
-  HIP_TRY(cbx::launch_broadcast(a, cfg, d.stream, {fused_start_event(c, d), step_stop_event(c, d, EV_A)}));
+  HIP_TRY(cbx::launch_broadcast(a, cfg, d.stream, {step_start_event(c, d, 0), step_stop_event(c, d, EV_A)}));
   ring_advance(c, d, 0);
   c->last_step_split = false;
   return finish_step(c);
