@@ -1,7 +1,7 @@
 """Build the native pieces of crossbow_amd in-tree.
 
 * ``crossbow_amd/libcrossbow_sma.so``  -- the C-ABI library (hipcc, gfx950):
-  csrc/context.hip + csrc/sma_kernels.hip, linked against RCCL.
+  csrc/context.hip + csrc/sync_steps.hip + csrc/sma_kernels.hip, linked against RCCL.
 * ``crossbow_amd/libGPU.so``           -- the JNI shim exporting Crossbow's
   ``TheGPU`` model-path natives; built only where ``jni.h`` exists (there is
   no JDK in this image).
@@ -31,13 +31,17 @@ def _hipcc() -> str:
     raise RuntimeError("hipcc not found: the MI355X library needs ROCm's hipcc")
 
 
+SOURCES = ("context.hip", "sync_steps.hip", "sma_kernels.hip")
+HEADERS = ("context_internal.h", "sma_internal.h")
+
+
 def _sources():
-    return [os.path.join(CSRC, "context.hip"), os.path.join(CSRC, "sma_kernels.hip")]
+    return [os.path.join(CSRC, f) for f in SOURCES]
 
 
 def _deps():
-    return _sources() + [os.path.join(CSRC, "sma_internal.h"), os.path.join(ROOT, "include", "crossbow_sma.h"),
-                         os.path.abspath(__file__)]
+    return _sources() + [os.path.join(CSRC, f) for f in HEADERS] + [os.path.join(ROOT, "include", "crossbow_sma.h"),
+                                                                   os.path.abspath(__file__)]
 
 
 def _stale(target: str, deps) -> bool:

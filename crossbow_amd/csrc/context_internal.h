@@ -1,0 +1,651 @@
+// context_internal.h -- the execution context's types and helpers, shared by
+// context.hip (the C-ABI, the model manager, checkpoints) and sync_steps.hip
+// (the barrier steps: SMA, host-staged SMA, S-SGD, the stream-order check).
+// Internal to libcrossbow_sma; the C-ABI is include/crossbow_sma.h.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+#include <rocprofiler-sdk-roctx/roctx.h>
+
+#include <pthread.h>
+#include <sched.h>
+#include <sys/stat.h>
+#include <sys/types.h>
+#include <fcntl.h>
+#include <unistd.h>
+#include <errno.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "../../include/crossbow_sma.h"
+#include "sma_internal.h"
+
+namespace cbx::host {
+
+inline thread_local std::string g_last_error;
+
+inline int fail(int code, const char *fmt, ...) {
+  char buf[1024];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  g_last_error = buf;
+  return code;
+}
+
+#define HIP_TRY(call)                                                                              \
+  do {                                                                                             \
+    hipError_t e_ = (call);                                                                        \
+    if (e_ != hipSuccess)                                                                          \
+      return fail(CBX_ERR_HIP, "%s:%d %s: %s", __FILE__, __LINE__, #call, hipGetErrorString(e_)); \
+  } while (0)
+
+#define NCCL_TRY(call)                                                                             \
+  do {                                                                                             \
+    ncclResult_t r_ = (call);                                                                      \
+    if (r_ != ncclSuccess)                                                                         \
+      return fail(CBX_ERR_RCCL, "%s:%d %s: %s", __FILE__, __LINE__, #call, ncclGetErrorString(r_)); \
+  } while (0)
+
+// ROCTx range over one C-ABI call (tracing): rocprofv3
+// --marker-trace shows each barrier step, staging pass, checkpoint and task
+// step as a host range beside its kernels.  Without a tool attached a push /
+// pop is a call through an empty dispatch table.
+struct TraceRange {
+  explicit TraceRange(const char *name) { roctxRangePushA(name); }
+  ~TraceRange() { roctxRangePop(); }
+  TraceRange(const TraceRange &) = delete;
+  TraceRange &operator=(const TraceRange &) = delete;
+};
+
+#define TRY(expr)            \
+  do {                       \
+    int rc_ = (expr);        \
+    if (rc_ < 0) return rc_; \
+  } while (0)
+
+// ---------------------------------------------------------------------------
+// Solver configuration, clib-multigpu/solverconfiguration.{h,c}
+// ---------------------------------------------------------------------------
+enum LrPolicy { LR_FIXED = 0, LR_INV, LR_STEP, LR_MULTISTEP, LR_EXP, LR_CLR, LR_LSR };
+
+struct SolverConf {
+  float alpha = 0.5f;  // solverconfiguration.c:17
+  int tau = 1;
+  LrPolicy policy = LR_FIXED;
+  float learningRate = 0.0f;
+  double gamma = 0.0;
+  double power = 0.0;
+  int size = 0;
+  std::vector<int> steps;
+  int step = 0;
+  int warmuptasks = 0;
+  float momentum = 0.0f;
+  int momentumMethod = 0;
+  float weightDecay = 0.0f;
+  float baseModelMomentum = 0.0f;
+  unsigned copy = 0;  // `_copy`, solverconfiguration.h:41-52
+  int irregular = 0;  // variables with a learning-rate multiplier != 1 (executioncontext.c:1602)
+  float circularLearningRate[3] = {0, 0, 0};  // CLR (executioncontext.c:1701-1718)
+  float circularMomentum[3] = {0, 0, 0};
+  int superConvergence = 0;
+
+  // crossbowSolverConfGetLearningRate, solverconfiguration.c:116-162.
+  int learning_rate(int task, float *out) {
+    float rate = 0.0f;
+    switch (policy) {
+      case LR_FIXED: rate = learningRate; break;
+      case LR_INV: rate = learningRate * (float)std::pow(1.0 + gamma * (double)(task + 1), -power); break;
+      case LR_STEP:
+        if (size <= 0) return fail(CBX_ERR_STATE, "step learning-rate policy with size 0");
+        rate = learningRate * (float)std::pow(gamma, std::floor((double)((task + 1) / size)));
+        break;
+      case LR_MULTISTEP:
+        if (step < (int)steps.size() && (task + 1) >= steps[step]) {
+          step++;
+          copy = 1;  // signal Phase D (solverconfiguration.c:133)
+        }
+        rate = learningRate * (float)std::pow(gamma, (double)step);
+        break;
+      case LR_LSR:
+        if (warmuptasks <= 0) return fail(CBX_ERR_STATE, "LSR policy without warm-up tasks");
+        if (task < warmuptasks) {
+          rate = (learningRate * (float)task) / (float)warmuptasks;
+        } else {
+          if (step < (int)steps.size() && (task + 1) >= steps[step]) {
+            step++;
+            copy = 1;  // solverconfiguration.c:147
+          }
+          rate = learningRate * (float)std::pow(gamma, (double)step);
+        }
+        break;
+      case LR_EXP: rate = learningRate * (float)std::pow(gamma, (double)(task + 1)); break;
+      case LR_CLR: return fail(CBX_ERR_UNSUPPORTED, "circular learning rate is unsupported");  // :155-157
+      default: return fail(CBX_ERR_UNSUPPORTED, "learning-rate policy %d unsupported", (int)policy);
+    }
+    *out = rate;
+    return CBX_OK;
+  }
+};
+
+// ---------------------------------------------------------------------------
+// Model definition (theModel before the manager exists), model.c:8-200
+// ---------------------------------------------------------------------------
+struct Variable {
+  int64_t offset_bytes;
+  int64_t bytes;
+  int64_t elements;
+  float lr_multiplier = 1.0f;  // variable.c; read only by per-variable optimisers, not by SMA's
+};
+
+struct ModelDef {
+  bool defined = false;
+  int ops = 0;
+  int64_t bytes = 0;       // setModel size (sum of capacities)
+  int64_t offset = 0;      // model.c:151 running offset
+  int64_t elements = 0;    // model.c:153
+  int wpc = 0;
+  int type = 0;            // update model type
+  SolverConf conf;
+  std::map<std::pair<int, int>, Variable> vars;  // (op id, order) -> variable
+  std::vector<int> count_per_op;
+  std::vector<float> host;  // initial values (PIN host buffer of theModel->data)
+};
+
+// The model manager's theta queue (thetaqueue.c, modelmanager.c:121-132): one
+// cache-line slot per replica id.  FREE; BUSY = reserved by a task from
+// acquireAccess until its release; SKIP = disabled.
+enum ThetaState { kThetaFree = 0, kThetaBusy = 1, kThetaSkip = 2 };  // thetaqueue.c:6-8
+struct alignas(64) ThetaSlot {
+  std::atomic<int> state{kThetaFree};
+};
+
+struct Replica {
+  int id = 0;
+  int g = 0;          // global device index (id % G)
+  int local = -1;     // local device slot, -1 if in another process
+  int slot = 0;       // replica slot within its device
+  int clock = 0;
+  int updates = 0;
+  SolverConf conf;
+  pthread_mutex_t lock;
+  hipEvent_t client = nullptr;  // end of the last optimiser step on a task stream (sma.cu:79)
+};
+
+enum TimingEv { EV_START = 0, EV_A, EV_AR, EV_B, EV_H2D0, EV_H2D1, EV_D2H0, EV_D2H1, EV_COUNT };
+
+struct Device {
+  int hip_id = 0;
+  int g = 0;  // global device index
+  // The device number in checkpoint file names, `model->dev` in the
+  // reference (modelmanager.c:285,324,337): the selected HIP device id, or
+  // the rank in the one-process-per-GPU form.
+  int file_id = 0;
+  hipStream_t stream = nullptr;       // model synchronisation stream (kernels)
+  hipStream_t comm_stream = nullptr;  // RCCL all-reduce of the bucketed pipeline (G > 1)
+  // Pipelined host-staged step (cbx_synchronise_staged): pinned H2D and D2H
+  // run on their own streams (separate DMA engines, both PCIe directions at
+  // once) beside the kernels on `stream`.  Created on first use.
+  hipStream_t h2d_stream = nullptr;
+  hipStream_t d2h_stream = nullptr;
+  hipEvent_t stage_entry = nullptr;       // sync stream -> h2d stream at entry
+  hipEvent_t stage_done = nullptr;        // d2h stream -> sync stream at exit
+  std::vector<hipEvent_t> stage_h2d;      // per bucket: inputs landed
+  std::vector<hipEvent_t> stage_k;        // per bucket: outputs computed
+  std::vector<hipEvent_t> bucket_acc;  // per bucket: kernel A done (stream -> comm_stream)
+  std::vector<hipEvent_t> bucket_red;  // per bucket: all-reduce done (comm_stream -> stream)
+  // Cross-step pipeline (cbx_set_pipeline_mode 1): kernels A run on a_stream,
+  // kernels B stay on `stream`; bucket_b[k] marks B(k) done, which A(k) of
+  // the next step waits for instead of the whole previous step.
+  hipStream_t a_stream = nullptr;
+  std::vector<hipEvent_t> bucket_b;
+  hipEvent_t cross_entry = nullptr;
+  float *decision = nullptr;           // 2 floats: the Phase-D decision, by step parity
+  bool cross_valid = false;            // the last step was cross-pipelined ...
+  int64_t cross_nb = 0;                // ... over this many buckets ...
+  unsigned long long cross_foreign = 0;  // ... and nothing else was enqueued since
+  unsigned cross_parity = 0;
+  ncclComm_t comm = nullptr;
+  // Peer-read all-reduce (cbx_set_allreduce_algorithm PEER): kernel A done /
+  // this device's shard of D reduced; the other devices' streams wait on them.
+  hipEvent_t peer_a = nullptr;
+  hipEvent_t peer_r = nullptr;
+  // Stream-order check (cbx_set_order_check): timestamps of the last two
+  // split steps, by step parity, per bucket.  Every point is the stop
+  // timestamp of a dispatch (a start event is a marker packet of its own):
+  // an empty probe dispatch right after each wait (before kernel A, before
+  // the collective, before kernel B), one right after the collective, and
+  // kernels A and B themselves.
+  struct OrderStep {
+    bool valid = false;
+    bool cont = false;  // continued the previous step bucket by bucket (mode 1, no join)
+    int64_t nb = 0;
+    std::vector<hipEvent_t> pa, a1, c0, c1, pb, b1;  // probe<A, A, probe<coll, probe>coll, probe<B, B
+  };
+  OrderStep ord[2];
+  // Owned timing events, 6 per bucket (pa, a1, c0, c1, pb, b1).  While the
+  // check is on, kernel A's and B's dispatches stop these instead of the
+  // reused bucket_acc / bucket_b, and the cross-stream waits use them too,
+  // so the two recorded steps keep their own timestamps.
+  std::vector<hipEvent_t> ord_pool[2];
+  unsigned ord_cur = 0;
+  cbx::BnSegment *bn_table = nullptr;  // batch-norm averaging: segment table (device)
+  size_t bn_table_bytes = 0;
+  float *bn_scratch = nullptr;         // packed statistics, all-reduced
+  size_t bn_scratch_bytes = 0;
+  int num_cus = 256;
+  // Arena: [base data][base gradient(ctrl+acc)][base diff(ctrl+D)][base last]
+  //        then per replica [data][diff][last][gradient].
+  char *arena = nullptr;
+  char *host = nullptr;  // pinned mirror, same layout (lazy)
+  size_t arena_bytes = 0;
+  size_t stride = 0;  // bytes per buffer slot
+  int base_slots = 0;  // replica slots inside the arena (replicas per device at creation)
+  // Replica slots added by autotune (modelmanager.c:362-470) beyond the arena:
+  // one block of kReplicaSlots buffers each, so existing pointers stay valid.
+  std::vector<char *> extra;
+  std::vector<char *> extra_host;
+  std::vector<int> replicas;  // global ids, increasing
+  hipEvent_t synched = nullptr;     // end-of-step event when timing is off
+  bool synched_by_dispatch = false;  // the step's last dispatch completes `synched` itself
+  hipEvent_t step_event = nullptr;  // end of the last step (cbx_step_event)
+  hipEvent_t ev[EV_COUNT] = {};
+  bool ev_valid[EV_COUNT] = {};
+  // Per-step timing ring: events {START, A, AR, B} of the last kRing steps,
+  // so a benchmark reads every launch of its timed region afterwards without
+  // a host synchronisation between steps.
+  static constexpr int kRing = 1024;
+  std::vector<hipEvent_t> ring;
+  std::vector<char> ring_split;
+  // 1: this slot recorded no START; its step queued right behind the previous
+  // slot's fused step, whose stop event stands in as its start (ring_start).
+  std::vector<char> ring_from_prev;
+  bool start_chosen = false;  // step_start_event decided this slot's ring_from_prev
+  int ring_pos = 0;
+  int ring_count = 0;
+};
+
+}  // namespace cbx::host
+
+struct cbx_context {
+  using Device = cbx::host::Device;
+  using ModelDef = cbx::host::ModelDef;
+  using Replica = cbx::host::Replica;
+  using ThetaSlot = cbx::host::ThetaSlot;
+  std::vector<Device> devs;
+  int G = 1;           // global device count (ranks)
+  bool per_rank = false;
+  ModelDef model;
+  bool manager = false;
+  int R = 0;           // replicas per device
+  // R * G.  Task threads read it (the theta queue) while the barrier thread
+  // may add or delete replicas (autotune), hence atomic.
+  std::atomic<int> size{0};
+  int sync_type = CBX_SYNC_BSP;
+  std::vector<Replica *> replicas;  // global id -> replica (all ids; remote ones have local = -1)
+  // Replicas removed by cbx_del_model.  A task thread may still be spinning
+  // on one's clock or blocked on its lock (cbx_get_next_or_wait), so the
+  // objects live until cbx_free instead of being deleted at once.
+  std::vector<Replica *> retired;
+  std::vector<int> locked;
+  std::unique_ptr<ThetaSlot[]> theta;  // kMaxReplicas * G slots, index = replica id
+  std::atomic<unsigned> theta_iter{0};  // round-robin cursor (thetaqueue.c:95-104)
+  int64_t n = 0;       // model elements
+  int64_t n4 = 0;      // padded float4 count
+  bool has_last = false;
+  unsigned long long version = 0;
+  // BN operators whose running statistics travel with the checkpoint
+  // (executioncontext.c:2352-2364): op id -> per-local-device buffers.
+  struct BnStats {
+    int elements = 0;
+    std::vector<float *> mean, variance;
+  };
+  std::map<int, BnStats> bn_stats;
+  bool timing = false;
+  cbx::LaunchConfig cfg;
+  // Optimiser step and S-SGD kernels (one float4 stream per buffer, few reads).
+  cbx::LaunchConfig aux_cfg = cbx::aux_launch_config();
+  // Write-heavy barrier kernels of DEFAULT and S-SGD (scripts/barrier_sweep.py).
+  cbx::LaunchConfig broadcast_cfg = cbx::broadcast_launch_config();
+  cbx::LaunchConfig ssgd_apply_cfg = cbx::ssgd_apply_launch_config();
+  // Kernel B of the split SMA path (scripts/apply_sweep.py).
+  cbx::LaunchConfig apply_cfg = cbx::sma_apply_launch_config();
+  int64_t bucket_elems = 0;
+  bool force_split = false;
+  bool last_step_split = false;
+  int pipeline_mode = 0;  // 0 bucketed within a step, 1 across steps (G > 1 split path)
+  int cross_wait_stride = 1;  // mode 1: buckets per cross-step wait
+  int allreduce_group = 1;     // pipelined split path: buckets per comm-stream wait
+  int allreduce_algo = CBX_ALLREDUCE_RCCL;
+  int staging_mode = CBX_STAGING_ZEROCOPY;  // cbx_synchronise_staged: zero-copy kernels or DMA copies
+  cbx::LaunchConfig staged_cfg = cbx::staged_launch_config();
+  bool peer_ready = false;     // hipDeviceEnablePeerAccess done between every pair of devices
+  bool order_check = false;    // record per-bucket timestamps of split steps (cbx_set_order_check)
+  // Fault injection for the order check's own test: $CBX_FAULT_SKIP_COMM_WAIT
+  // at context creation drops the comm stream's wait on kernel A, so the
+  // collective races its input (results are then wrong; tests only).
+  bool fault_skip_comm_wait = std::getenv("CBX_FAULT_SKIP_COMM_WAIT") != nullptr;
+  // Bumped by every C-ABI call that may enqueue work on a sync stream other
+  // than the barrier path itself: a cross-step pipelined step then joins the
+  // whole sync stream instead of waiting bucket by bucket.
+  std::atomic<unsigned long long> foreign_ops{0};
+};
+
+namespace cbx::host {
+
+// ---------------------------------------------------------------------------
+// Arena layout helpers
+// ---------------------------------------------------------------------------
+constexpr int kBaseSlots = 4;     // data, gradient, diff, last
+constexpr int kReplicaSlots = 4;  // data, diff, last, gradient
+constexpr size_t kAlign = 2u << 20;
+// Extra bytes between consecutive buffer slots, so the 2R+2 streams of one
+// element index do not all start on the same 2 MiB boundary (measured +1-2 %
+// on the fused kernel, scripts/membench.hip, profiles/r01).
+constexpr size_t kSlotStagger = 4096;
+// Buckets of the G > 1 pipeline when cbx_set_bucket_elements was not called.
+constexpr int64_t kDefaultBuckets = 8;
+
+inline size_t slot_index_base(int kind) {
+  switch (kind) {
+    case CBX_BUF_DATA: return 0;
+    case CBX_BUF_GRADIENT: return 1;
+    case CBX_BUF_DIFF: return 2;
+    default: return 3;
+  }
+}
+
+inline size_t slot_index_replica(int slot, int kind) {
+  size_t k;
+  switch (kind) {
+    case CBX_BUF_DATA: k = 0; break;
+    case CBX_BUF_DIFF: k = 1; break;
+    case CBX_BUF_LAST: k = 2; break;
+    default: k = 3; break;
+  }
+  return kBaseSlots + (size_t)slot * kReplicaSlots + k;
+}
+
+// Byte offset of the model data inside a slot: acc and D carry a 256-byte
+// control block in front (sma_internal.h).
+inline size_t data_offset(bool ctrl) { return ctrl ? (size_t)cbx::kCtrlFloats * sizeof(float) : 0; }
+
+inline float *slot_ptr(char *arena, const Device &d, size_t slot, bool ctrl) {
+  return reinterpret_cast<float *>(arena + slot * d.stride + data_offset(ctrl));
+}
+
+inline bool base_has(const cbx_context *c, int kind) { return kind != CBX_BUF_LAST || c->has_last; }
+
+inline float *base_dev(const cbx_context *c, const Device &d, int kind) {
+  const bool ctrl = (kind == CBX_BUF_GRADIENT || kind == CBX_BUF_DIFF);
+  return slot_ptr(d.arena, d, slot_index_base(kind), ctrl);
+}
+
+inline float *base_ctrl(const Device &d, int kind) {
+  return reinterpret_cast<float *>(d.arena + slot_index_base(kind) * d.stride);
+}
+
+inline size_t replica_kind_index(int kind) { return slot_index_replica(0, kind) - kBaseSlots; }
+
+inline float *replica_dev(const Device &d, const Replica &r, int kind) {
+  if (r.slot >= d.base_slots)
+    return reinterpret_cast<float *>(d.extra[r.slot - d.base_slots] + replica_kind_index(kind) * d.stride);
+  return slot_ptr(d.arena, d, slot_index_replica(r.slot, kind), false);
+}
+
+inline float *base_host(const Device &d, int kind) {
+  const bool ctrl = (kind == CBX_BUF_GRADIENT || kind == CBX_BUF_DIFF);
+  return slot_ptr(d.host, d, slot_index_base(kind), ctrl);
+}
+
+inline float *replica_host(const Device &d, const Replica &r, int kind) {
+  if (r.slot >= d.base_slots)
+    return reinterpret_cast<float *>(d.extra_host[r.slot - d.base_slots] + replica_kind_index(kind) * d.stride);
+  return slot_ptr(d.host, d, slot_index_replica(r.slot, kind), false);
+}
+
+// The *_q checks are for calls that enqueue no device work (the barrier path,
+// replica locks, queries); the others also count a possible foreign op.
+inline int check_ctx_q(cbx_context *c) {
+  if (!c) return fail(CBX_ERR_INVALID, "null context");
+  return CBX_OK;
+}
+
+inline int check_ctx(cbx_context *c) {
+  TRY(check_ctx_q(c));
+  c->foreign_ops.fetch_add(1, std::memory_order_relaxed);
+  return CBX_OK;
+}
+
+inline int check_manager_q(cbx_context *c) {
+  TRY(check_ctx_q(c));
+  if (!c->manager) return fail(CBX_ERR_STATE, "model manager not created (call cbx_set_model_manager)");
+  return CBX_OK;
+}
+
+inline int check_manager(cbx_context *c) {
+  TRY(check_manager_q(c));
+  c->foreign_ops.fetch_add(1, std::memory_order_relaxed);
+  return CBX_OK;
+}
+
+inline int check_replica_q(cbx_context *c, int id, bool need_local) {
+  TRY(check_manager_q(c));
+  if (id < 0 || id >= c->size) return fail(CBX_ERR_INVALID, "replica id %d out of range [0, %d)", id, c->size.load());
+  if (need_local && c->replicas[id]->local < 0)
+    return fail(CBX_ERR_INVALID, "replica %d lives in another process (device %d)", id, c->replicas[id]->g);
+  return CBX_OK;
+}
+
+inline int check_replica(cbx_context *c, int id, bool need_local) {
+  TRY(check_manager(c));
+  if (id < 0 || id >= c->size) return fail(CBX_ERR_INVALID, "replica id %d out of range [0, %d)", id, c->size.load());
+  if (need_local && c->replicas[id]->local < 0)
+    return fail(CBX_ERR_INVALID, "replica %d lives in another process (device %d)", id, c->replicas[id]->g);
+  return CBX_OK;
+}
+
+inline int local_of(cbx_context *c, int g) {
+  for (size_t k = 0; k < c->devs.size(); ++k)
+    if (c->devs[k].g == g) return (int)k;
+  return -1;
+}
+
+inline int gfx950_device_count(int *count) {
+  int n = 0;
+  *count = 0;
+  hipError_t e = hipGetDeviceCount(&n);
+  if (e != hipSuccess || n <= 0) {
+    (void)hipGetLastError();
+    return CBX_OK;
+  }
+  int k = 0;
+  for (int i = 0; i < n; ++i) {
+    hipDeviceProp_t p;
+    if (hipGetDeviceProperties(&p, i) != hipSuccess) continue;
+    if (std::strncmp(p.gcnArchName, "gfx950", 6) == 0) ++k;
+  }
+  *count = k;
+  return CBX_OK;
+}
+
+inline int open_device(Device &d, int hip_id, int g) {
+  int total = 0;
+  hipError_t ce = hipGetDeviceCount(&total);
+  if (ce != hipSuccess) {
+    (void)hipGetLastError();
+    return fail(CBX_ERR_NO_DEVICE, "no MI355X visible: %s", hipGetErrorString(ce));
+  }
+  if (hip_id < 0 || hip_id >= total) return fail(CBX_ERR_NO_DEVICE, "device %d not visible (%d devices)", hip_id, total);
+  hipDeviceProp_t p;
+  HIP_TRY(hipGetDeviceProperties(&p, hip_id));
+  if (std::strncmp(p.gcnArchName, "gfx950", 6) != 0)
+    return fail(CBX_ERR_NO_DEVICE, "device %d is %s, this library is built for gfx950 (MI355X) only", hip_id,
+                p.gcnArchName);
+  d.hip_id = hip_id;
+  d.g = g;
+  d.file_id = g;
+  d.num_cus = p.multiProcessorCount;
+  HIP_TRY(hipSetDevice(hip_id));
+  // executioncontext.c:324: one non-blocking model-synchronisation stream.
+  HIP_TRY(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
+  HIP_TRY(hipStreamCreateWithFlags(&d.comm_stream, hipStreamNonBlocking));
+  HIP_TRY(hipEventCreateWithFlags(&d.synched, hipEventDisableTiming));
+  for (int k = 0; k < EV_COUNT; ++k) HIP_TRY(hipEventCreate(&d.ev[k]));
+  return CBX_OK;
+}
+
+inline void close_device(Device &d) {
+  if (d.stream == nullptr && d.arena == nullptr) return;
+  (void)hipSetDevice(d.hip_id);
+  if (d.stream) (void)hipStreamSynchronize(d.stream);
+  if (d.comm_stream) (void)hipStreamSynchronize(d.comm_stream);
+  if (d.comm) (void)ncclCommDestroy(d.comm);
+  if (d.arena) (void)hipFree(d.arena);
+  for (char *p : d.extra)
+    if (p) (void)hipFree(p);
+  for (char *p : d.extra_host)
+    if (p) (void)hipHostFree(p);
+  if (d.bn_table) (void)hipFree(d.bn_table);
+  if (d.bn_scratch) (void)hipFree(d.bn_scratch);
+  if (d.host) (void)hipHostFree(d.host);
+  if (d.synched) (void)hipEventDestroy(d.synched);
+  for (int k = 0; k < EV_COUNT; ++k)
+    if (d.ev[k]) (void)hipEventDestroy(d.ev[k]);
+  for (hipEvent_t e : d.ring) (void)hipEventDestroy(e);
+  for (hipEvent_t e : d.bucket_acc) (void)hipEventDestroy(e);
+  for (hipEvent_t e : d.bucket_red) (void)hipEventDestroy(e);
+  if (d.a_stream) (void)hipStreamSynchronize(d.a_stream);
+  for (hipEvent_t e : d.bucket_b) (void)hipEventDestroy(e);
+  if (d.cross_entry) (void)hipEventDestroy(d.cross_entry);
+  for (auto &pool : d.ord_pool)
+    for (hipEvent_t e : pool) (void)hipEventDestroy(e);
+  if (d.peer_a) (void)hipEventDestroy(d.peer_a);
+  if (d.peer_r) (void)hipEventDestroy(d.peer_r);
+  if (d.decision) (void)hipFree(d.decision);
+  if (d.a_stream) (void)hipStreamDestroy(d.a_stream);
+  for (hipStream_t st : {d.h2d_stream, d.d2h_stream})
+    if (st) (void)hipStreamSynchronize(st);
+  for (hipEvent_t e : d.stage_h2d) (void)hipEventDestroy(e);
+  for (hipEvent_t e : d.stage_k) (void)hipEventDestroy(e);
+  if (d.stage_entry) (void)hipEventDestroy(d.stage_entry);
+  if (d.stage_done) (void)hipEventDestroy(d.stage_done);
+  if (d.h2d_stream) (void)hipStreamDestroy(d.h2d_stream);
+  if (d.d2h_stream) (void)hipStreamDestroy(d.d2h_stream);
+  if (d.stream) (void)hipStreamDestroy(d.stream);
+  if (d.comm_stream) (void)hipStreamDestroy(d.comm_stream);
+  d = Device();
+}
+
+// The current ring slot's event `ev` (START..B) when timing is enabled, for
+// a dispatch to timestamp itself (hipExtLaunchKernelGGL); else nullptr.
+inline hipEvent_t ring_event(cbx_context *c, Device &d, int ev) {
+  if (!c->timing || d.ring.empty()) return nullptr;
+  return d.ring[(size_t)d.ring_pos * 4 + ev];
+}
+
+// The stop event of ring slot `slot`'s step: EV_A for a fused step (kind 0),
+// EV_B for a split one.
+inline hipEvent_t ring_stop(Device &d, int slot) {
+  return d.ring[(size_t)slot * 4 + (d.ring_split[slot] == 0 ? EV_A : EV_B)];
+}
+
+// The START event for the first dispatch of a fused (kind 0) or pipelined
+// split (kind 2) step.  A dispatch start event is a marker packet that costs
+// the stream ~4.5 us per launch, while a stop event costs nothing
+// (scripts/event_ts_probe.hip: 20.8 vs 16.4 us per back-to-back launch).
+// When the previous slot is a step of the same kind whose stop has not
+// completed yet, this step is enqueued behind a busy GPU: that stop stands in
+// as this step's start (a fused step queues right behind it on the same
+// stream; a pipelined step's span becomes its stop-to-stop share of the
+// pipeline) and no marker is added.  Otherwise (an idle GPU, another kind of
+// step) START is recorded.
+inline hipEvent_t step_start_event(cbx_context *c, Device &d, int kind) {
+  if (!c->timing || d.ring.empty()) return nullptr;
+  const int slot = d.ring_pos;
+  d.ring_from_prev[slot] = 0;
+  if (d.ring_count > 0) {
+    const int prev = (slot + Device::kRing - 1) % Device::kRing;
+    const bool busy = d.ring_split[prev] == kind && hipEventQuery(ring_stop(d, prev)) == hipErrorNotReady;
+    (void)hipGetLastError();  // hipEventQuery leaves NotReady as the thread's last error
+    if (busy) {
+      d.ring_from_prev[slot] = 1;
+      d.start_chosen = true;
+      return nullptr;
+    }
+  }
+  d.start_chosen = true;
+  return d.ring[(size_t)slot * 4 + EV_START];
+}
+
+// The event that opens ring slot `slot`: its START, or the previous slot's
+// stop when the step was enqueued behind it (step_start_event).
+inline hipEvent_t ring_start(Device &d, int slot) {
+  if (!d.ring_from_prev.empty() && d.ring_from_prev[slot])
+    return ring_stop(d, (slot + Device::kRing - 1) % Device::kRing);
+  return d.ring[(size_t)slot * 4 + EV_START];
+}
+
+// Record a timing marker when timing is enabled.  Step events (START..B) go
+// to the current ring slot, staging events to the fixed ones.
+inline int mark(cbx_context *c, Device &d, int ev) {
+  if (!c->timing) return CBX_OK;
+  if (ev <= EV_B && !d.ring.empty()) {
+    HIP_TRY(hipEventRecord(d.ring[(size_t)d.ring_pos * 4 + ev], d.stream));
+    return CBX_OK;
+  }
+  HIP_TRY(hipEventRecord(d.ev[ev], d.stream));
+  d.ev_valid[ev] = true;
+  return CBX_OK;
+}
+
+// kind: 0 fused (START, A=B), 1 split in order (START, A, AR, B),
+// 2 split pipelined (START, B only: per-kernel spans are not separable).
+inline void ring_advance(cbx_context *c, Device &d, int kind) {
+  if (!c->timing || d.ring.empty()) return;
+  d.ring_split[d.ring_pos] = (char)kind;
+  if (!d.start_chosen) d.ring_from_prev[d.ring_pos] = 0;  // a path that records START itself
+  d.start_chosen = false;
+  d.ring_pos = (d.ring_pos + 1) % Device::kRing;
+  if (d.ring_count < Device::kRing) d.ring_count++;
+}
+
+// Elapsed ms between events a and b of ring slot `slot` (-1 if absent).
+inline int ring_span(Device &d, int slot, int a, int b, float *out) {
+  *out = -1.0f;
+  HIP_TRY(hipEventSynchronize(d.ring[(size_t)slot * 4 + b]));
+  hipEvent_t from = a == EV_START ? ring_start(d, slot) : d.ring[(size_t)slot * 4 + a];
+  HIP_TRY(hipEventElapsedTime(out, from, d.ring[(size_t)slot * 4 + b]));
+  return CBX_OK;
+}
+
+// ---- the barrier steps (sync_steps.hip) ------------------------------------
+// SMA (synch/sma.c:13-231): fused at G = 1; kernel A / collective / kernel B
+// per bucket at G > 1 (or forced); the peer-read form.
+int sma_step(cbx_context *c, int first);
+// The same step from and to the pinned host mirror (cbx_synchronise_staged).
+int sma_step_staged(cbx_context *c, int first, int buckets);
+// Synchronous SGD, update model WORKER (synch/synchronoussgd.c:13-106).
+int ssgd_step(cbx_context *c, int first);
+// The step event of every device (cbx_step_event), after a step's last dispatch.
+int finish_step(cbx_context *c);
+// The stop event for a step's LAST dispatch (see sync_steps.hip).
+hipEvent_t step_stop_event(cbx_context *c, Device &d, int ev);
+int alloc_host_mirror(cbx_context *c);
+// Stream-order check of one recorded step, and of two consecutive ones.
+int check_order_step(const Device::OrderStep &o);
+int check_order_pair(const Device::OrderStep &p, const Device::OrderStep &q);
+
+}  // namespace cbx::host
