@@ -75,7 +75,7 @@ def _rank_main(rank, world, port, q):
             s = [mine.s[i] for i in ids]
             w = [mine.w[i] for i in ids]
             acc, copies = O.sma_accumulate(alpha, z, s, w, [int(mine.copy[i]) for i in ids])
-            # control slot in front of acc, summed with it (context.hip, sma_internal.h)
+            # control slot in front of acc, summed with it (sync_steps.hip, sma_internal.h)
             buf = torch.from_numpy(np.concatenate([np.array([copies], np.float32), acc]))
             dist.all_reduce(buf, op=dist.ReduceOp.SUM)
             ctrl, Dsum = float(buf[0]), buf[1:].numpy().copy()

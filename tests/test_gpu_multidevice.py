@@ -3,7 +3,7 @@
 Crossbow runs one JVM over all selected GPUs: ncclCommInitAll over the G
 devices (clib-multigpu/executioncontext.c:185-201) and, per step, grouped
 ncclAllReduce calls issued from one thread (synch/common.c:14-54).  The JNI
-drop-in reaches it through cbx_init(devices, G) (TheGPU_jni.c -> context.hip).
+drop-in reaches it through cbx_init(devices, G) (TheGPU_jni.c -> context.hip, sync_steps.hip).
 
 Here cbx_init gets G copies of device 0 and the library build linked
 against the loopback collective (tests/native/fake_rccl.cpp), whose
