@@ -77,7 +77,79 @@ def _jobs(world):
     jobs += [("golden", gc["name"]) for gc in C.golden_cases(world)]
     jobs += [("golden-rsag", gc["name"]) for gc in C.golden_cases(world)]
     jobs += [("order", "order-all-reduce"), ("order", "order-rsag")]
+    if world == 4:
+        jobs += [("random", "random-long-run")]
     return jobs + [("bn", "bn"), ("autotune", "autotune")]
+
+
+def run_random(g, world, rank, steps=40):
+    """A long randomised run under real RCCL: every few steps the bucket size,
+    pipeline mode, wait stride, all-reduce group or the collective's form
+    changes (the same choice on every rank, from a shared seed), replicas
+    ask for Phase D, are held by a task (SSP) or are rewritten by the host,
+    and the stream order is checked every two steps.  Against the oracle
+    within the G > 1 tolerance at the end; returns (bad, digest, differs)."""
+    import random
+    O = C.oracle()
+    A = g.A
+    n, R = 200_003, 2
+    C.setup_model(g, A, n, R, 0.9, 7, A.SYNC_SSP, 4 * world)
+    g("cbx_set_order_check", 1)
+    size = world * R
+    mine = [i for i in range(size) if i % world == rank]
+    st = O.make_state(n, world, R, 0.1, 0.9)
+    g.write("cbx_base_write", rank, A.BUF_DATA, st.z[rank])
+    g.write("cbx_base_write", rank, A.BUF_LAST, st.last[rank])
+    for i in mine:
+        g.write("cbx_replica_write", i, A.BUF_DIFF, st.s[i])
+        g.write("cbx_replica_write", i, A.BUF_DATA, st.w[i])
+    rng = random.Random(9001)  # the same sequence on every rank: collective choices must match
+    bad = []
+    for step in range(steps):
+        st.locked[:] = 1
+        u = rng.random()
+        hold = None
+        if u < 0.1:
+            i = rng.randrange(size)
+            st.copy[i] = 1
+            if i in mine:
+                g("cbx_replica_set_copy", i, 1)
+        elif u < 0.2:
+            hold = rng.randrange(size)
+            st.locked[hold] = 0
+            if hold in mine:
+                g("cbx_replica_lock", hold)
+        elif u < 0.3:
+            g("cbx_set_bucket_elements", ctypes.c_longlong(rng.choice([16_384, 65_536, 1 << 40])))
+        elif u < 0.4:
+            g("cbx_set_pipeline_mode", rng.choice([0, 1]))
+            g("cbx_set_cross_wait_stride", rng.choice([1, 2, 3]))
+            g("cbx_set_allreduce_group", rng.choice([1, 2, 4]))
+        elif u < 0.5:
+            g("cbx_set_allreduce_algorithm", rng.choice([0, 2]))
+        elif u < 0.55:
+            i = rng.randrange(size)
+            new = O.fill_normal(n, 7000 + step, 0.05)
+            st.w[i] = new.copy()
+            if i in mine:
+                g.write("cbx_replica_write", i, A.BUF_DATA, new)
+        g("cbx_lock_any")
+        g("cbx_synchronise", 0, step + 1, 0, 0)
+        g("cbx_unlock_any")
+        if hold is not None and hold in mine:
+            g("cbx_replica_unlock", hold)
+        O.sma_step(st)
+        if step % 2 == 1:
+            g("cbx_check_order")  # raises on a violation
+    g("cbx_wait")
+    check = C.Checker(exact=world < 3)
+    z = g.read("cbx_base_read", rank, A.BUF_DATA, n)
+    last = g.read("cbx_base_read", rank, A.BUF_LAST, n)
+    check(f"z[{rank}]", z, st.z[rank])
+    check(f"last[{rank}]", last, st.last[rank])
+    for i in mine:
+        check(f"w[{i}]", g.read("cbx_replica_read", i, A.BUF_DATA, n), st.w[i])
+    return bad + check.bad, C.digest(z, last), check.differs
 
 
 def run_order(g, world, algo):
@@ -126,6 +198,9 @@ def _rank_main(rank, world, jobs, d, q):
                                                algo=2 if kind == "golden-rsag" else 0)}
                 elif kind == "order":
                     res = {"bad": run_order(g, world, 2 if name == "order-rsag" else 0)}
+                elif kind == "random":
+                    bad, dig, differs = run_random(g, world, rank)
+                    res = {"bad": bad, "digest": {rank: dig}, "differs": differs}
                 elif kind == "bn":
                     res = {"bad": C.run_bn(g, world, [rank], poison=True, exact=exact)}
                 else:
@@ -156,7 +231,7 @@ def test_real_rccl_ranks_on_one_gpu_vs_oracle(world):
         assert not failures, f"rank {rank}: {failures}"
     differs = 0
     for j, (kind, name) in enumerate(jobs):
-        if kind != "case":
+        if kind not in ("case", "random"):
             continue
         # every rank applied the same D: z and last bitwise identical across ranks (sma.c:168-174)
         digests = {res[r][j][1]["digest"][r] for r in range(world)}
