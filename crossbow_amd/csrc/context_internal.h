@@ -273,6 +273,7 @@ struct Device {
   // slot's fused step, whose stop event stands in as its start (ring_start).
   std::vector<char> ring_from_prev;
   bool start_chosen = false;  // step_start_event decided this slot's ring_from_prev
+  unsigned long long start_foreign = ~0ull;  // foreign_ops at the last step_start_event
   int ring_pos = 0;
   int ring_count = 0;
 };
@@ -567,7 +568,8 @@ inline hipEvent_t ring_stop(Device &d, int slot) {
 // the stream ~4.5 us per launch, while a stop event costs nothing
 // (scripts/event_ts_probe.hip: 20.8 vs 16.4 us per back-to-back launch).
 // When the previous slot is a step of the same kind whose stop has not
-// completed yet, this step is enqueued behind a busy GPU: that stop stands in
+// completed yet, and no other C-ABI call enqueued work since, this step is
+// enqueued behind a busy GPU: that stop stands in
 // as this step's start (a fused step queues right behind it on the same
 // stream; a pipelined step's span becomes its stop-to-stop share of the
 // pipeline) and no marker is added.  Otherwise (an idle GPU, another kind of
@@ -576,7 +578,13 @@ inline hipEvent_t step_start_event(cbx_context *c, Device &d, int kind) {
   if (!c->timing || d.ring.empty()) return nullptr;
   const int slot = d.ring_pos;
   d.ring_from_prev[slot] = 0;
-  if (d.ring_count > 0) {
+  // Nothing else may have been enqueued since the previous step (a task's
+  // optimiser step on the sync stream, a host write): the dispatch must queue
+  // directly behind that step's stop.
+  const unsigned long long foreign = c->foreign_ops.load(std::memory_order_acquire);
+  const bool nothing_between = d.start_foreign == foreign;
+  d.start_foreign = foreign;
+  if (d.ring_count > 0 && nothing_between) {
     const int prev = (slot + Device::kRing - 1) % Device::kRing;
     const bool busy = d.ring_split[prev] == kind && hipEventQuery(ring_stop(d, prev)) == hipErrorNotReady;
     (void)hipGetLastError();  // hipEventQuery leaves NotReady as the thread's last error

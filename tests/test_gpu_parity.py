@@ -921,3 +921,42 @@ def test_stream_order_check_detects_a_race(monkeypatch):
         g.wait()
     finally:
         g.free()
+
+
+def test_fused_timing_excludes_work_enqueued_between_steps():
+    # Back-to-back fused steps reuse the previous step's stop event as their
+    # start (no start marker).  When a task's optimiser step was enqueued on
+    # the sync stream in between, the next step records its own start, so
+    # its kernel span never includes the optimiser kernels.
+    import statistics
+
+    from crossbow_amd import _lib
+    n, R = 4_000_003, 4
+    g = make_gpu(n, R, 0.1, 0.9)
+    try:
+        g.setLearningRateDecayPolicyFixed(0.01)
+        g.fill_synthetic(3)
+        g.set_timing(True)
+        clock = 0
+
+        def step():
+            nonlocal clock
+            clock += 1
+            g.lockAny()
+            g.synchronise(0, clock, 0, False)
+            g.unlockAny()
+
+        for _ in range(12):
+            step()
+        g.wait()
+        plain = g.timing_history(_lib.T_KERNEL)[-10:]
+        for _ in range(6):
+            for i in range(R):
+                g.replica_optimise(i, clock, None)  # on the sync stream
+            step()
+        g.wait()
+        mixed = g.timing_history(_lib.T_KERNEL)[-6:]
+        assert min(plain) > 0 and min(mixed) > 0
+        assert statistics.median(mixed) < 1.3 * statistics.median(plain), (plain, mixed)
+    finally:
+        g.free()
