@@ -72,15 +72,15 @@ def max_over_ranks(value: float, world: int) -> float:
 def tune_buckets(gpu, n: int, world: int, step: Callable[[], None], candidates=(1, 2, 4, 8),
                  steps: int = 10, warmup: int = 2, modes=(0, 1), strides=(1, 2, 4), passes: int = 2,
                  group_candidates=(2, 4)):
-    """Pick the bucket count of the G > 1 pipeline (kernel A / RCCL
-    all-reduce / kernel B per bucket) by timing each candidate on the live
-    communicator, the way a runtime tunes itself in its warm-up.
+    """Pick the configuration of the G > 1 pipeline (kernel A / collective /
+    kernel B per bucket) by timing each candidate on the live communicator,
+    the way a runtime tunes itself in its warm-up.
 
-    More buckets hide more of the all-reduce behind kernel A, but each bucket
+    More buckets hide more of the collective behind kernel A, but each bucket
     costs fixed time (cross-queue waits, a shorter launch's ramp and drain:
     ~7 us per bucket on one MI355X with the bucket events on the kernel
     dispatches, profiles/r01/bench_force_split_tuned.json), so the best count
-    depends on how long the all-reduce is, i.e. on G and the xGMI links.
+    depends on how long the collective is, i.e. on G and the xGMI links.
     Every rank times every candidate, the times are max-reduced over ranks,
     and all ranks take the same argmin, so the RCCL call sequence stays
     identical on every rank.  ``step()`` runs one barrier step.
@@ -90,22 +90,21 @@ def tune_buckets(gpu, n: int, world: int, step: Callable[[], None], candidates=(
     profiles/r01/bench_force_split_tuned.json), pipeline mode 0 (within a
     step) and 1 (across steps, ``gpu.set_pipeline_mode``), mode 1 at each
     cross-step wait stride below the bucket count (``gpu.set_cross_wait_stride``,
-    3-6 % at 8 buckets, profiles/r01/cross_wait_stride_ab.json), then the
-    all-reduce grouping of the winner (``gpu.set_allreduce_group``, 4-9 % in
-    mode 0, profiles/r01/allreduce_group_ab.json).  The group is reset to 1
-    first, so an earlier setting never skews the sweep.  Candidates are timed
-    in ``passes`` interleaved passes and each keeps its best pass, so one
-    noisy sample (a few percent on one GPU) does not decide.
-
-    Last, the winner's configuration is timed with the reduce-scatter form
-    of the all-reduce (``gpu.set_allreduce_algorithm(ALLREDUCE_RSAG)``:
-    reduce-scatter, base momentum on the rank's shard, all-gather), which
-    moves the same link bytes in two collectives per bucket and saves kernel
-    B's momentum pass on (G-1)/G of the model; it is kept only if faster.
+    3-6 % at 8 buckets, profiles/r01/cross_wait_stride_ab.json), and the
+    collective's form (``gpu.set_allreduce_algorithm``): one all-reduce, or,
+    where G divides 1024, reduce-scatter + base momentum on the rank's shard
+    + all-gather, which moves the same link bytes in two collectives per
+    bucket and saves kernel B's momentum pass on (G-1)/G of the model.  Then
+    the all-reduce grouping of the winner (``gpu.set_allreduce_group``, 4-9 %
+    in mode 0, profiles/r01/allreduce_group_ab.json).  The group and the
+    form are reset first, so an earlier setting never skews the sweep.
+    Candidates are timed in ``passes`` interleaved passes and each keeps its
+    best pass, so one noisy sample (a few percent on one GPU) does not decide.
 
     Returns (bucket_elements, mode, stride, group, algorithm, {key: ms_per_step})
     with keys "<buckets>/<mode>" for stride 1, "<buckets>/<mode>/s<stride>",
-    "<key of the winner>/g<group>" and "<key of the winner>[/g<group>]/rsag".
+    the same with "/rsag" for the reduce-scatter form, and "<key of the
+    winner>/g<group>".
     """
     import time
 
@@ -125,28 +124,34 @@ def tune_buckets(gpu, n: int, world: int, step: Callable[[], None], candidates=(
         gpu.wait()
         return max_over_ranks((time.perf_counter() - t0) * 1e3 / steps, world)
 
+    def elems_of(nb):
+        return (1 << 62) if nb <= 1 else max(1, -(-n // nb))
+
+    algos = [ALLREDUCE_RCCL]
+    if 1 < world <= 16 and 1024 % world == 0:
+        algos.append(ALLREDUCE_RSAG)
     gpu.set_allreduce_group(1)
-    gpu.set_allreduce_algorithm(ALLREDUCE_RCCL)
     results = {}
     for _ in range(max(1, passes)):
-        for nb in candidates:
-            elems = (1 << 62) if nb <= 1 else max(1, -(-n // nb))
-            for mode, stride in combos(nb):
-                gpu.set_bucket_elements(elems)
-                gpu.set_pipeline_mode(mode)
-                gpu.set_cross_wait_stride(stride)
-                ms = timed_steps()
-                key = (nb, mode, stride)
-                results[key] = min(ms, results.get(key, ms))
+        for algo in algos:
+            gpu.set_allreduce_algorithm(algo)
+            for nb in candidates:
+                for mode, stride in combos(nb):
+                    gpu.set_bucket_elements(elems_of(nb))
+                    gpu.set_pipeline_mode(mode)
+                    gpu.set_cross_wait_stride(stride)
+                    ms = timed_steps()
+                    key = (nb, mode, stride, algo)
+                    results[key] = min(ms, results.get(key, ms))
     best = min(results, key=lambda k: (results[k], k))
-    nb, mode, stride = best
-    elems = (1 << 62) if nb <= 1 else max(1, -(-n // nb))
-    gpu.set_bucket_elements(elems)
+    nb, mode, stride, algorithm = best
+    gpu.set_allreduce_algorithm(algorithm)
+    gpu.set_bucket_elements(elems_of(nb))
     gpu.set_pipeline_mode(mode)
     gpu.set_cross_wait_stride(stride)
     out = {tuning_key(*k): v for k, v in results.items()}
     # Then the all-reduce grouping of the winner: fewer comm-stream waits,
-    # later all-reduce starts.  Over xGMI the later start may cost more than
+    # later collective starts.  Over xGMI the later start may cost more than
     # the waits save, so it is timed, not assumed.
     group = 1
     groups = [grp for grp in group_candidates if 1 < grp < nb]
@@ -158,24 +163,15 @@ def tune_buckets(gpu, n: int, world: int, step: Callable[[], None], candidates=(
                 ms = timed_steps()
                 timed[grp] = min(ms, timed.get(grp, ms))
         for grp in groups:
-            out[tuning_key(nb, mode, stride) + f"/g{grp}"] = timed[grp]
+            out[tuning_key(*best) + f"/g{grp}"] = timed[grp]
         group = min(timed, key=lambda g: (timed[g], g))
     gpu.set_allreduce_group(group)
-    win_key = tuning_key(nb, mode, stride) + (f"/g{group}" if group > 1 else "")
-    win_ms = out.get(win_key, results[best])
-    algorithm = ALLREDUCE_RCCL
-    if world > 1 and world <= 16 and 1024 % world == 0:
-        gpu.set_allreduce_algorithm(ALLREDUCE_RSAG)
-        ms = min(timed_steps() for _ in range(max(1, passes)))
-        out[win_key + "/rsag"] = ms
-        if ms < win_ms:
-            algorithm = ALLREDUCE_RSAG
-        gpu.set_allreduce_algorithm(algorithm)
-    return elems, mode, stride, group, algorithm, out
+    return elems_of(nb), mode, stride, group, algorithm, out
 
 
-def tuning_key(nb: int, mode: int, stride: int = 1) -> str:
-    return f"{nb}/{mode}" if stride == 1 else f"{nb}/{mode}/s{stride}"
+def tuning_key(nb: int, mode: int, stride: int = 1, algo: int = ALLREDUCE_RCCL) -> str:
+    key = f"{nb}/{mode}" if stride == 1 else f"{nb}/{mode}/s{stride}"
+    return key + ("/rsag" if algo == ALLREDUCE_RSAG else "")
 
 
 def local_replicas(size: int, world: int, rank: int):

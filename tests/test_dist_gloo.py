@@ -287,7 +287,7 @@ def test_bucket_tuning_agrees_across_ranks():
     assert g0 == g1 == setg0 == setg1 == 1  # the all-reduce group of the winner, by the max over ranks
     want = ["1/0"] + [f"{nb}/{m}" for nb in (2, 4, 8) for m in (0, 1)]
     want += [f"{nb}/1/s{s}" for nb in (4, 8) for s in (2, 4) if s < nb]
-    want += ["4/0/g2"]  # groups 1 < g < buckets, timed for the winner only
-    want += ["4/0/rsag"]  # then the reduce-scatter form of the winner
+    want += [k + "/rsag" for k in want]  # every candidate in the reduce-scatter form too
+    want += ["4/0/rsag/g2"]  # groups 1 < g < buckets, timed for the winner only
     assert cands == sorted(want)
-    assert a0 == a1 == seta0 == seta1 == 2  # faster on both ranks: kept
+    assert a0 == a1 == seta0 == seta1 == 2  # faster on both ranks: chosen
