@@ -180,73 +180,65 @@ int sma_step_peer(cbx_context *c, std::vector<cbx::SmaArgs> &args, bool mom) {
   return CBX_OK;
 }
 
-int sma_step(cbx_context *c, int first) {
-  const bool mom = c->has_last && c->model.conf.momentum > 0;  // sma.c:150 (base conf)
-  std::vector<cbx::SmaArgs> args(c->devs.size());
-  int copies_total = 0;
-  for (size_t k = 0; k < c->devs.size(); ++k) {
-    int cp = 0;
-    TRY(build_args(c, c->devs[k], first, args[k], &cp));
-    copies_total += cp;
-  }
+// ---------------------------------------------------------------------------
+// The split SMA step (G > 1, or forced at G = 1): kernel A, the collective of
+// acc (+ control block), kernel B.  With one bucket everything runs in order
+// on the sync stream.  With nb > 1 buckets the collective runs on a second
+// stream:
+//   stream      : A(0) A(1) [wait red(0)] B(0) A(2) [wait red(1)] B(1) ...
+//   comm_stream :      [wait acc(0)] AR(0) [wait acc(1)] AR(1) ...
+// so kernel A of bucket k+1 overlaps the xGMI collective of bucket k.
+// Cross-step mode (cbx_set_pipeline_mode 1): kernels A on a_stream, B on the
+// sync stream.  A(k) waits only for B(k) of the previous step, so the next
+// step's first buckets run while this step's last collectives are still on
+// the link:
+//   a_stream    : [wait b(0)'] A(0) [wait b(1)'] A(1) ...
+//   comm_stream : [wait acc(0)] AR(0) [wait acc(1)] AR(1) ...
+//   stream      : [wait red(0)] B(0) [wait red(1)] B(1) ...
+// A step joins the whole sync stream instead when anything else was enqueued
+// since the last cross-pipelined step (foreign_ops).
+// Per-bucket events ride on the kernels' own dispatch packets (stop event)
+// instead of a separate hipEventRecord marker, which left a ~10 us gap on the
+// sync stream per bucket: -2 to -8 % per step (scripts/dispatch_event_ab.py,
+// profiles/r01/dispatch_event_ab.json).  Mode 1: A(k) waits for
+// B(k + stride - 1) of the last step once per `stride` buckets (it implies
+// B(k..): same stream).  Each satisfied cross-queue wait still costs the
+// waiting queue ~10 us; fewer waits trade that for less cross-step overlap
+// (cbx_set_cross_wait_stride).
+// ---------------------------------------------------------------------------
+struct SplitStep {
+  cbx_context *c;
+  std::vector<cbx::SmaArgs> &args;
+  bool mom;
+  int64_t b4 = 0, nb = 0, wait_stride = 1;
+  bool pipelined = false, cross = false, rsag = false, ocheck = false;
+  unsigned long long foreign = 0;
+  std::vector<char> join;
 
-  TRY(ensure_one_rank_comm(c));
-  if (c->allreduce_algo == CBX_ALLREDUCE_PEER && c->G > 1) {
-    TRY(sma_step_peer(c, args, mom));
-  } else if (c->G == 1 && !c->force_split) {
-    // Single GPU: Phase B is the identity, so A + C (+ D) fuse into one pass.
-    // (sma.c:63 waits on base->updated; every producer of z is this stream,
-    // so stream order already gives that dependency.)
-    Device &d = c->devs[0];
-    HIP_TRY(hipSetDevice(d.hip_id));
-    cbx::LaunchConfig cfg = c->cfg;
-    cfg.num_cus = d.num_cus;
-    // The dispatch timestamps its own (start, stop) ring events: no marker
-    // packets between steps (each costs ~3 us of stream time, membench v4).
-    HIP_TRY(cbx::launch_sma_fused(args[0], mom, copies_total > 0, cfg, d.stream,
-                                  {step_start_event(c, d, 0), step_stop_event(c, d, EV_A)}));
-    ring_advance(c, d, 0);
-    d.cross_valid = false;
-    c->last_step_split = false;
-  } else {
-    // G > 1: kernel A, grouped RCCL all-reduce of acc (+ control block),
-    // kernel B.  With one bucket everything runs in order on the sync
-    // stream.  With nb > 1 buckets the all-reduce runs on a second stream:
-    //   stream      : A(0) A(1) [wait red(0)] B(0) A(2) [wait red(1)] B(1) ...
-    //   comm_stream :      [wait acc(0)] AR(0) [wait acc(1)] AR(1) ...
-    // so kernel A of bucket k+1 overlaps the xGMI all-reduce of bucket k.
+  SplitStep(cbx_context *ctx, std::vector<cbx::SmaArgs> &a, bool momentum) : c(ctx), args(a), mom(momentum) {}
+
+  int64_t start_of(int64_t b) const { return b * b4; }
+  int64_t len_of(int64_t b) const { return std::min(b4, c->n4 - b * b4); }
+
+  // Bucket geometry, per-bucket events, the cross-step join decision, and a
+  // fresh set of stream-order timestamps when the check is on.
+  int prepare() {
     const int64_t pad = cbx::kPadFloat4;
-    int64_t b4 = c->n4;
+    b4 = c->n4;
     if (c->bucket_elems > 0) {
       b4 = ((c->bucket_elems / 4 + pad - 1) / pad) * pad;
     } else if (c->G > 1) {
       b4 = ((c->n4 / kDefaultBuckets + pad - 1) / pad) * pad;  // auto: kDefaultBuckets buckets
     }
     if (b4 <= 0 || b4 > c->n4) b4 = c->n4;
-    const int64_t nb = (c->n4 + b4 - 1) / b4;
-    const bool pipelined = nb > 1;
-    // Cross-step mode (cbx_set_pipeline_mode 1): kernels A on a_stream, B on
-    // the sync stream.  A(k) waits only for B(k) of the previous step, so the
-    // next step's first buckets run while this step's last all-reduces are
-    // still on the link:
-    //   a_stream    : [wait b(0)'] A(0) [wait b(1)'] A(1) ...
-    //   comm_stream : [wait acc(0)] AR(0) [wait acc(1)] AR(1) ...
-    //   stream      : [wait red(0)] B(0) [wait red(1)] B(1) ...
-    // A step joins the whole sync stream instead when anything else was
-    // enqueued since the last cross-pipelined step (foreign_ops).
-    const bool cross = pipelined && c->pipeline_mode == 1;
-    const bool rsag = c->allreduce_algo == CBX_ALLREDUCE_RSAG;
-    // Per-bucket events ride on the kernels' own dispatch packets (stop
-    // event) instead of a separate hipEventRecord marker, which left a
-    // ~10 us gap on the sync stream per bucket: -2 to -8 % per step
-    // (scripts/dispatch_event_ab.py, profiles/r01/dispatch_event_ab.json).
-    // Mode 1: A(k) waits for B(k + stride - 1) of the last step once per
-    // `stride` buckets (it implies B(k..): same stream).  Each satisfied
-    // cross-queue wait still costs the waiting queue ~10 us; fewer waits
-    // trade that for less cross-step overlap (cbx_set_cross_wait_stride).
-    const int64_t wait_stride = std::max(1, c->cross_wait_stride);
-    const unsigned long long foreign = c->foreign_ops.load(std::memory_order_acquire);
-    std::vector<char> join(c->devs.size(), 1);
+    nb = (c->n4 + b4 - 1) / b4;
+    pipelined = nb > 1;
+    cross = pipelined && c->pipeline_mode == 1;
+    rsag = c->allreduce_algo == CBX_ALLREDUCE_RSAG;
+    ocheck = c->order_check && c->timing;
+    wait_stride = std::max(1, c->cross_wait_stride);
+    foreign = c->foreign_ops.load(std::memory_order_acquire);
+    join.assign(c->devs.size(), 1);
     for (size_t k = 0; k < c->devs.size(); ++k) {
       Device &d = c->devs[k];
       HIP_TRY(hipSetDevice(d.hip_id));
@@ -276,206 +268,206 @@ int sma_step(cbx_context *c, int first) {
           HIP_TRY(hipStreamWaitEvent(d.a_stream, d.cross_entry, 0));
         }
       }
+      if (ocheck) {
+        d.ord_cur ^= 1u;
+        std::vector<hipEvent_t> &pool = d.ord_pool[d.ord_cur];
+        while ((int64_t)pool.size() < 6 * nb) {
+          hipEvent_t e;
+          HIP_TRY(hipEventCreate(&e));
+          pool.push_back(e);
+        }
+        Device::OrderStep &o = d.ord[d.ord_cur];
+        o.valid = true;
+        o.cont = cross && !join[k];
+        o.nb = nb;
+        o.pa.assign(pool.begin(), pool.begin() + nb);
+        o.c0.assign(pool.begin() + nb, pool.begin() + 2 * nb);
+        o.c1.assign(pool.begin() + 2 * nb, pool.begin() + 3 * nb);
+        o.pb.assign(pool.begin() + 3 * nb, pool.begin() + 4 * nb);
+        o.b1.assign(pool.begin() + 4 * nb, pool.begin() + 5 * nb);
+        o.a1.assign(pool.begin() + 5 * nb, pool.begin() + 6 * nb);
+      }
     }
-    // Stream-order check: a fresh set of per-bucket timestamps for this step.
-    const bool ocheck = c->order_check && c->timing;
+    return CBX_OK;
+  }
+
+  // Kernel A (Phase A) of bucket b on every device.
+  int accumulate(int64_t b) {
+    for (size_t k = 0; k < c->devs.size(); ++k) {
+      Device &d = c->devs[k];
+      HIP_TRY(hipSetDevice(d.hip_id));
+      cbx::LaunchConfig cfg = c->cfg;
+      cfg.num_cus = d.num_cus;
+      cbx::Timing t;
+      if (b == 0) t.start = pipelined ? step_start_event(c, d, 2) : ring_event(c, d, EV_START);
+      if (!pipelined) t.stop = ring_event(c, d, EV_A);
+      hipStream_t st = cross ? d.a_stream : d.stream;
+      if (cross && !join[k] && b % wait_stride == 0) {  // B(b .. b+stride-1) of the last step
+        const int64_t w = std::min<int64_t>(b + wait_stride - 1, nb - 1);
+        HIP_TRY(hipStreamWaitEvent(st, ocheck ? d.ord[d.ord_cur ^ 1u].b1[w] : d.bucket_b[w], 0));
+      }
+      if (pipelined) t.stop = ocheck ? d.ord[d.ord_cur].a1[b] : d.bucket_acc[b];
+      if (ocheck) {
+        Device::OrderStep &o = d.ord[d.ord_cur];
+        HIP_TRY(cbx::launch_order_probe(st, {nullptr, o.pa[b]}));
+        o.a1[b] = t.stop;  // with timing on, A always carries a stop event (the pool's or the ring's)
+      }
+      HIP_TRY(cbx::launch_sma_accumulate(offset_args(args[k], start_of(b), len_of(b)), b == 0, cfg, st, t));
+    }
+    return CBX_OK;
+  }
+
+  // The collective of bucket b (common.c:14-54: grouped, fp32 sum; bucket 0
+  // also carries the control block right in front of the data).  `wait_acc`:
+  // the comm stream first waits for kernel A of that bucket (-1: no wait; an
+  // earlier collective of the same group already waited on a later bucket,
+  // which implies this one: A runs in order).
+  int collective(int64_t b, bool on_comm, int64_t wait_acc) {
+    const int64_t start = start_of(b), len = len_of(b);
+    if (on_comm && wait_acc >= 0 && !c->fault_skip_comm_wait) {
+      for (size_t k = 0; k < c->devs.size(); ++k) {
+        Device &d = c->devs[k];
+        HIP_TRY(hipSetDevice(d.hip_id));
+        HIP_TRY(hipStreamWaitEvent(d.comm_stream, ocheck ? d.ord[d.ord_cur].a1[wait_acc] : d.bucket_acc[wait_acc], 0));
+      }
+    }
     for (size_t k = 0; ocheck && k < c->devs.size(); ++k) {
       Device &d = c->devs[k];
       HIP_TRY(hipSetDevice(d.hip_id));
-      d.ord_cur ^= 1u;
-      std::vector<hipEvent_t> &pool = d.ord_pool[d.ord_cur];
-      while ((int64_t)pool.size() < 6 * nb) {
-        hipEvent_t e;
-        HIP_TRY(hipEventCreate(&e));
-        pool.push_back(e);
-      }
-      Device::OrderStep &o = d.ord[d.ord_cur];
-      o.valid = true;
-      o.cont = cross && !join[k];
-      o.nb = nb;
-      o.pa.assign(pool.begin(), pool.begin() + nb);
-      o.c0.assign(pool.begin() + nb, pool.begin() + 2 * nb);
-      o.c1.assign(pool.begin() + 2 * nb, pool.begin() + 3 * nb);
-      o.pb.assign(pool.begin() + 3 * nb, pool.begin() + 4 * nb);
-      o.b1.assign(pool.begin() + 4 * nb, pool.begin() + 5 * nb);
-      o.a1.assign(pool.begin() + 5 * nb, pool.begin() + 6 * nb);
+      HIP_TRY(cbx::launch_order_probe(on_comm ? d.comm_stream : d.stream, {nullptr, d.ord[d.ord_cur].c0[b]}));
     }
-    // `wait_acc`: the comm stream first waits for kernel A of that bucket
-    // (-1: no wait; an earlier all-reduce of the same group already waited
-    // on a later bucket, which implies this one: A runs in order).
-    auto allreduce = [&](int64_t b, bool on_comm, int64_t wait_acc) -> int {
-      const int64_t start = b * b4;
-      const int64_t len = std::min(b4, c->n4 - start);
-      // common.c:14-54: grouped all-reduce, fp32 sum.  Bucket 0 also carries
-      // the control block that sits right in front of the data.
-      if (on_comm && wait_acc >= 0 && !c->fault_skip_comm_wait) {
-        for (size_t k = 0; k < c->devs.size(); ++k) {
-          Device &d = c->devs[k];
-          HIP_TRY(hipSetDevice(d.hip_id));
-          HIP_TRY(hipStreamWaitEvent(d.comm_stream, ocheck ? d.ord[d.ord_cur].a1[wait_acc] : d.bucket_acc[wait_acc], 0));
-        }
-      }
-      for (size_t k = 0; ocheck && k < c->devs.size(); ++k) {
+    if (rsag) {
+      // Reduce-scatter form: shard g of the bucket (len / G float4s) is
+      // reduced on rank g, which applies the base momentum to its shard of
+      // last; the all-gather of last (or of D without momentum) then hands
+      // every rank the whole bucket of D' for kernel B.  The control block
+      // rides a 64-float all-reduce grouped with bucket 0's reduce-scatter.
+      const int64_t sh4 = len / c->G;
+      NCCL_TRY(ncclGroupStart());
+      for (size_t k = 0; k < c->devs.size(); ++k) {
         Device &d = c->devs[k];
         HIP_TRY(hipSetDevice(d.hip_id));
-        HIP_TRY(cbx::launch_order_probe(on_comm ? d.comm_stream : d.stream, {nullptr, d.ord[d.ord_cur].c0[b]}));
-      }
-      if (rsag) {
-        // Reduce-scatter form: shard g of the bucket (len / G float4s) is
-        // reduced on rank g, which applies the base momentum to its shard of
-        // last; the all-gather of last (or of D without momentum) then hands
-        // every rank the whole bucket of D' for kernel B.  The control block
-        // rides a 64-float all-reduce grouped with bucket 0's reduce-scatter.
-        const int64_t sh4 = len / c->G;
-        NCCL_TRY(ncclGroupStart());
-        for (size_t k = 0; k < c->devs.size(); ++k) {
-          Device &d = c->devs[k];
-          HIP_TRY(hipSetDevice(d.hip_id));
-          hipStream_t st = on_comm ? d.comm_stream : d.stream;
-          if (b == 0)
-            NCCL_TRY(ncclAllReduce(base_ctrl(d, CBX_BUF_GRADIENT), base_ctrl(d, CBX_BUF_DIFF), cbx::kCtrlFloats,
+        hipStream_t st = on_comm ? d.comm_stream : d.stream;
+        if (b == 0)
+          NCCL_TRY(ncclAllReduce(base_ctrl(d, CBX_BUF_GRADIENT), base_ctrl(d, CBX_BUF_DIFF), cbx::kCtrlFloats,
+                                 ncclFloat, ncclSum, d.comm, st));
+        NCCL_TRY(ncclReduceScatter(base_dev(c, d, CBX_BUF_GRADIENT) + start * 4,
+                                   base_dev(c, d, CBX_BUF_DIFF) + (start + d.g * sh4) * 4, (size_t)sh4 * 4,
                                    ncclFloat, ncclSum, d.comm, st));
-          NCCL_TRY(ncclReduceScatter(base_dev(c, d, CBX_BUF_GRADIENT) + start * 4,
-                                     base_dev(c, d, CBX_BUF_DIFF) + (start + d.g * sh4) * 4, (size_t)sh4 * 4,
-                                     ncclFloat, ncclSum, d.comm, st));
-        }
-        NCCL_TRY(ncclGroupEnd());
-        const int gather = mom ? CBX_BUF_LAST : CBX_BUF_DIFF;
-        for (size_t k = 0; k < c->devs.size(); ++k) {
-          if (!mom) break;
-          Device &d = c->devs[k];
-          HIP_TRY(hipSetDevice(d.hip_id));
-          cbx::SmaArgs a = offset_args(args[k], start + d.g * sh4, sh4);
-          cbx::LaunchConfig cfg = c->apply_cfg;
-          cfg.num_cus = d.num_cus;
-          HIP_TRY(cbx::launch_sma_shard_momentum(a, cfg, on_comm ? d.comm_stream : d.stream));
-        }
-        NCCL_TRY(ncclGroupStart());
-        for (size_t k = 0; k < c->devs.size(); ++k) {
-          Device &d = c->devs[k];
-          HIP_TRY(hipSetDevice(d.hip_id));
-          float *buf = base_dev(c, d, gather) + start * 4;
-          NCCL_TRY(ncclAllGather(buf + d.g * sh4 * 4, buf, (size_t)sh4 * 4, ncclFloat, d.comm,
-                                 on_comm ? d.comm_stream : d.stream));
-        }
-        NCCL_TRY(ncclGroupEnd());
-      } else {
-        NCCL_TRY(ncclGroupStart());
-        for (size_t k = 0; k < c->devs.size(); ++k) {
-          Device &d = c->devs[k];
-          HIP_TRY(hipSetDevice(d.hip_id));
-          const float *src = base_dev(c, d, CBX_BUF_GRADIENT) + start * 4;
-          float *dst = base_dev(c, d, CBX_BUF_DIFF) + start * 4;
-          size_t count = (size_t)len * 4;
-          if (b == 0) {
-            src -= cbx::kCtrlFloats;
-            dst -= cbx::kCtrlFloats;
-            count += cbx::kCtrlFloats;
-          }
-          NCCL_TRY(ncclAllReduce(src, dst, count, ncclFloat, ncclSum, d.comm, on_comm ? d.comm_stream : d.stream));
-        }
-        NCCL_TRY(ncclGroupEnd());
       }
-      for (size_t k = 0; ocheck && k < c->devs.size(); ++k) {
+      NCCL_TRY(ncclGroupEnd());
+      const int gather = mom ? CBX_BUF_LAST : CBX_BUF_DIFF;
+      for (size_t k = 0; mom && k < c->devs.size(); ++k) {
         Device &d = c->devs[k];
         HIP_TRY(hipSetDevice(d.hip_id));
-        HIP_TRY(cbx::launch_order_probe(on_comm ? d.comm_stream : d.stream, {nullptr, d.ord[d.ord_cur].c1[b]}));
-      }
-      if (on_comm) {
-        for (size_t k = 0; k < c->devs.size(); ++k) {
-          Device &d = c->devs[k];
-          HIP_TRY(hipSetDevice(d.hip_id));
-          HIP_TRY(hipEventRecord(d.bucket_red[b], d.comm_stream));
-        }
-      }
-      return CBX_OK;
-    };
-    auto accumulate = [&](int64_t b) -> int {
-      const int64_t start = b * b4;
-      const int64_t len = std::min(b4, c->n4 - start);
-      for (size_t k = 0; k < c->devs.size(); ++k) {
-        Device &d = c->devs[k];
-        HIP_TRY(hipSetDevice(d.hip_id));
-        cbx::LaunchConfig cfg = c->cfg;
-        cfg.num_cus = d.num_cus;
-        cbx::Timing t;
-        if (b == 0) t.start = pipelined ? step_start_event(c, d, 2) : ring_event(c, d, EV_START);
-        if (!pipelined) t.stop = ring_event(c, d, EV_A);
-        hipStream_t st = cross ? d.a_stream : d.stream;
-        if (cross && !join[k] && b % wait_stride == 0) {  // B(b .. b+stride-1) of the last step
-          const int64_t w = std::min<int64_t>(b + wait_stride - 1, nb - 1);
-          HIP_TRY(hipStreamWaitEvent(st, ocheck ? d.ord[d.ord_cur ^ 1u].b1[w] : d.bucket_b[w], 0));
-        }
-        if (pipelined) t.stop = ocheck ? d.ord[d.ord_cur].a1[b] : d.bucket_acc[b];
-        if (ocheck) {
-          Device::OrderStep &o = d.ord[d.ord_cur];
-          HIP_TRY(cbx::launch_order_probe(st, {nullptr, o.pa[b]}));
-          o.a1[b] = t.stop;  // with timing on, A always carries a stop event (the pool's or the ring's)
-        }
-        HIP_TRY(cbx::launch_sma_accumulate(offset_args(args[k], start, len), b == 0, cfg, st, t));
-      }
-      return CBX_OK;
-    };
-    auto apply = [&](int64_t b) -> int {
-      const int64_t start = b * b4;
-      const int64_t len = std::min(b4, c->n4 - start);
-      for (size_t k = 0; k < c->devs.size(); ++k) {
-        Device &d = c->devs[k];
-        HIP_TRY(hipSetDevice(d.hip_id));
-        if (pipelined) HIP_TRY(hipStreamWaitEvent(d.stream, d.bucket_red[b], 0));
+        cbx::SmaArgs a = offset_args(args[k], start + d.g * sh4, sh4);
         cbx::LaunchConfig cfg = c->apply_cfg;
         cfg.num_cus = d.num_cus;
-        cbx::Timing t;
-        if (b == nb - 1) t.stop = step_stop_event(c, d, EV_B);
-        cbx::SmaArgs a = offset_args(args[k], start, len);
-        if (rsag && mom) a.D = a.last;  // the gathered D' (kernel B then adds it without momentum)
-        if (cross) {
-          // The next step's AR(0) may overwrite D's control block before this
-          // step's later buckets run: B(0) publishes the Phase-D decision to a
-          // per-parity slot that B(1..) read.
-          a.decision_mode = b == 0 ? 1 : 2;
-          a.decision = d.decision + (d.cross_parity & 1u);
-        }
-        const bool in_dispatch = cross && !t.stop;
-        if (in_dispatch) t.stop = ocheck ? d.ord[d.ord_cur].b1[b] : d.bucket_b[b];
-        if (ocheck) {
-          Device::OrderStep &o = d.ord[d.ord_cur];
-          HIP_TRY(cbx::launch_order_probe(d.stream, {nullptr, o.pb[b]}));
-          if (!t.stop) t.stop = o.b1[b];
-          o.b1[b] = t.stop;
-        }
-        HIP_TRY(cbx::launch_sma_apply(a, mom && !rsag, cfg, d.stream, t));
-        if (cross && !in_dispatch) HIP_TRY(hipEventRecord(d.bucket_b[b], d.stream));
+        HIP_TRY(cbx::launch_sma_shard_momentum(a, cfg, on_comm ? d.comm_stream : d.stream));
       }
-      return CBX_OK;
-    };
+      NCCL_TRY(ncclGroupStart());
+      for (size_t k = 0; k < c->devs.size(); ++k) {
+        Device &d = c->devs[k];
+        HIP_TRY(hipSetDevice(d.hip_id));
+        float *buf = base_dev(c, d, gather) + start * 4;
+        NCCL_TRY(ncclAllGather(buf + d.g * sh4 * 4, buf, (size_t)sh4 * 4, ncclFloat, d.comm,
+                               on_comm ? d.comm_stream : d.stream));
+      }
+      NCCL_TRY(ncclGroupEnd());
+    } else {
+      NCCL_TRY(ncclGroupStart());
+      for (size_t k = 0; k < c->devs.size(); ++k) {
+        Device &d = c->devs[k];
+        HIP_TRY(hipSetDevice(d.hip_id));
+        const float *src = base_dev(c, d, CBX_BUF_GRADIENT) + start * 4;
+        float *dst = base_dev(c, d, CBX_BUF_DIFF) + start * 4;
+        size_t count = (size_t)len * 4;
+        if (b == 0) {
+          src -= cbx::kCtrlFloats;
+          dst -= cbx::kCtrlFloats;
+          count += cbx::kCtrlFloats;
+        }
+        NCCL_TRY(ncclAllReduce(src, dst, count, ncclFloat, ncclSum, d.comm, on_comm ? d.comm_stream : d.stream));
+      }
+      NCCL_TRY(ncclGroupEnd());
+    }
+    for (size_t k = 0; ocheck && k < c->devs.size(); ++k) {
+      Device &d = c->devs[k];
+      HIP_TRY(hipSetDevice(d.hip_id));
+      HIP_TRY(cbx::launch_order_probe(on_comm ? d.comm_stream : d.stream, {nullptr, d.ord[d.ord_cur].c1[b]}));
+    }
+    if (on_comm) {
+      for (size_t k = 0; k < c->devs.size(); ++k) {
+        Device &d = c->devs[k];
+        HIP_TRY(hipSetDevice(d.hip_id));
+        HIP_TRY(hipEventRecord(d.bucket_red[b], d.comm_stream));
+      }
+    }
+    return CBX_OK;
+  }
+
+  // Kernel B (Phase C, + D on copy) of bucket b on every device.
+  int apply(int64_t b) {
+    for (size_t k = 0; k < c->devs.size(); ++k) {
+      Device &d = c->devs[k];
+      HIP_TRY(hipSetDevice(d.hip_id));
+      if (pipelined) HIP_TRY(hipStreamWaitEvent(d.stream, d.bucket_red[b], 0));
+      cbx::LaunchConfig cfg = c->apply_cfg;
+      cfg.num_cus = d.num_cus;
+      cbx::Timing t;
+      if (b == nb - 1) t.stop = step_stop_event(c, d, EV_B);
+      cbx::SmaArgs a = offset_args(args[k], start_of(b), len_of(b));
+      if (rsag && mom) a.D = a.last;  // the gathered D' (kernel B then adds it without momentum)
+      if (cross) {
+        // The next step's AR(0) may overwrite D's control block before this
+        // step's later buckets run: B(0) publishes the Phase-D decision to a
+        // per-parity slot that B(1..) read.
+        a.decision_mode = b == 0 ? 1 : 2;
+        a.decision = d.decision + (d.cross_parity & 1u);
+      }
+      const bool in_dispatch = cross && !t.stop;
+      if (in_dispatch) t.stop = ocheck ? d.ord[d.ord_cur].b1[b] : d.bucket_b[b];
+      if (ocheck) {
+        Device::OrderStep &o = d.ord[d.ord_cur];
+        HIP_TRY(cbx::launch_order_probe(d.stream, {nullptr, o.pb[b]}));
+        if (!t.stop) t.stop = o.b1[b];
+        o.b1[b] = t.stop;
+      }
+      HIP_TRY(cbx::launch_sma_apply(a, mom && !rsag, cfg, d.stream, t));
+      if (cross && !in_dispatch) HIP_TRY(hipEventRecord(d.bucket_b[b], d.stream));
+    }
+    return CBX_OK;
+  }
+
+  int run() {
+    TRY(prepare());
     if (!pipelined) {
       TRY(accumulate(0));
-      TRY(allreduce(0, false, -1));
+      TRY(collective(0, false, -1));
       for (Device &d : c->devs) {
         HIP_TRY(hipSetDevice(d.hip_id));
         TRY(mark(c, d, EV_AR));
       }
       TRY(apply(0));
     } else {
-      // All-reduces go out in groups of `ar_group` buckets behind a single
+      // Collectives go out in groups of `ar_group` buckets behind a single
       // comm-stream wait on the group's last kernel A (cbx_set_allreduce_group).
       // Every event is recorded before the wait on it is enqueued: a group's
-      // all-reduces follow its last A, and B(j) follows AR(j).  Mode 0 applies
+      // collectives follow its last A, and B(j) follows AR(j).  Mode 0 applies
       // the previous group while this one is on the link; mode 1 applies a
-      // group right behind its all-reduces.  ar_group 1 is the per-bucket order
-      // A(b) AR(b) B(b-1) (mode 0) / A(b) AR(b) B(b) (mode 1).
+      // group right behind its collectives.  ar_group 1 is the per-bucket
+      // order A(b) AR(b) B(b-1) (mode 0) / A(b) AR(b) B(b) (mode 1).
       const int64_t ar_group = std::max(1, c->allreduce_group);
       int64_t applied = 0;
       for (int64_t b = 0; b < nb; ++b) {
         TRY(accumulate(b));
         if ((b + 1) % ar_group != 0 && b != nb - 1) continue;
         const int64_t g0 = b - b % ar_group;
-        for (int64_t j = g0; j <= b; ++j) TRY(allreduce(j, true, j == g0 ? b : -1));
+        for (int64_t j = g0; j <= b; ++j) TRY(collective(j, true, j == g0 ? b : -1));
         const int64_t upto = cross ? b + 1 : g0;
         for (; applied < upto; ++applied) TRY(apply(applied));
       }
-      // The wait inside apply(nb-1) also joins every earlier all-reduce
+      // The wait inside apply(nb-1) also joins every earlier collective
       // (comm_stream is in order) back into the sync stream.
       for (; applied < nb; ++applied) TRY(apply(applied));
     }
@@ -489,6 +481,41 @@ int sma_step(cbx_context *c, int first) {
       }
     }
     c->last_step_split = true;
+    return CBX_OK;
+  }
+};
+
+int sma_step(cbx_context *c, int first) {
+  const bool mom = c->has_last && c->model.conf.momentum > 0;  // sma.c:150 (base conf)
+  std::vector<cbx::SmaArgs> args(c->devs.size());
+  int copies_total = 0;
+  for (size_t k = 0; k < c->devs.size(); ++k) {
+    int cp = 0;
+    TRY(build_args(c, c->devs[k], first, args[k], &cp));
+    copies_total += cp;
+  }
+
+  TRY(ensure_one_rank_comm(c));
+  if (c->allreduce_algo == CBX_ALLREDUCE_PEER && c->G > 1) {
+    TRY(sma_step_peer(c, args, mom));
+  } else if (c->G == 1 && !c->force_split) {
+    // Single GPU: Phase B is the identity, so A + C (+ D) fuse into one pass.
+    // (sma.c:63 waits on base->updated; every producer of z is this stream,
+    // so stream order already gives that dependency.)
+    Device &d = c->devs[0];
+    HIP_TRY(hipSetDevice(d.hip_id));
+    cbx::LaunchConfig cfg = c->cfg;
+    cfg.num_cus = d.num_cus;
+    // The dispatch timestamps its own stop (and, on an idle GPU, start) ring
+    // events: no marker packets between back-to-back steps.
+    HIP_TRY(cbx::launch_sma_fused(args[0], mom, copies_total > 0, cfg, d.stream,
+                                  {step_start_event(c, d, 0), step_stop_event(c, d, EV_A)}));
+    ring_advance(c, d, 0);
+    d.cross_valid = false;
+    c->last_step_split = false;
+  } else {
+    SplitStep split(c, args, mom);
+    TRY(split.run());
   }
 
   TRY(finish_step(c));
