@@ -199,7 +199,7 @@ int sma_step_peer(cbx_context *c, std::vector<cbx::SmaArgs> &args, bool mom) {
 // since the last cross-pipelined step (foreign_ops).
 // Per-bucket events ride on the kernels' own dispatch packets (stop event)
 // instead of a separate hipEventRecord marker, which left a ~10 us gap on the
-// sync stream per bucket: -2 to -8 % per step (scripts/dispatch_event_ab.py,
+// sync stream per bucket: -2 to -8 % per step (round 1, dispatch_event_ab:
 // profiles/r01/dispatch_event_ab.json).  Mode 1: A(k) waits for
 // B(k + stride - 1) of the last step once per `stride` buckets (it implies
 // B(k..): same stream).  Each satisfied cross-queue wait still costs the
