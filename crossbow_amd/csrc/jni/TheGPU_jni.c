@@ -12,6 +12,7 @@
 
 #include <stdio.h>
 #include <stdlib.h>
+#include <string.h>
 
 #include "crossbow_sma.h"
 
@@ -37,6 +38,63 @@ static jint fatal_or (int rc) {
 
 #define NATIVE(ret, name) JNIEXPORT ret JNICALL Java_uk_ac_imperial_lsds_crossbow_device_TheGPU_##name
 
+/* The Java side has no natives for this library's G > 1 pipeline settings
+ * (Crossbow's own step is one grouped all-reduce), so a deployment chooses
+ * them through the environment, read once at init (values as the C-ABI
+ * takes them; an unparsable or refused value is fatal, like every error):
+ *   CBX_ALLREDUCE          rccl | rsag | peer   (cbx_set_allreduce_algorithm)
+ *   CBX_BUCKET_ELEMENTS    floats per bucket    (cbx_set_bucket_elements)
+ *   CBX_PIPELINE_MODE      0 | 1                (cbx_set_pipeline_mode)
+ *   CBX_CROSS_WAIT_STRIDE  1..4096              (cbx_set_cross_wait_stride)
+ *   CBX_ALLREDUCE_GROUP    1..4096              (cbx_set_allreduce_group)
+ *   CBX_STAGING            zerocopy | dma       (cbx_set_staging_mode)
+ * bench.py's warm-up tuner (crossbow_amd/dist.py) prints the values it
+ * chose for a node in its JSON config. */
+static long long env_int (const char *name, int *present) {
+	const char *v = getenv (name);
+	*present = v != NULL && *v != '\0';
+	if (!*present)
+		return 0;
+	char *end = NULL;
+	long long x = strtoll (v, &end, 10);
+	if (end == v || *end != '\0') {
+		fprintf (stderr, "error: %s=%s is not an integer\n", name, v);
+		exit (1);
+	}
+	return x;
+}
+
+static void configure_from_env (void) {
+	const char *algo = getenv ("CBX_ALLREDUCE");
+	if (algo && *algo) {
+		int a = !strcmp (algo, "rccl") ? CBX_ALLREDUCE_RCCL : !strcmp (algo, "rsag") ? CBX_ALLREDUCE_RSAG
+			: !strcmp (algo, "peer") ? CBX_ALLREDUCE_PEER : -1;
+		if (a < 0) {
+			fprintf (stderr, "error: CBX_ALLREDUCE=%s (rccl, rsag or peer)\n", algo);
+			exit (1);
+		}
+		fatal_or (cbx_set_allreduce_algorithm (theGPU, a));
+	}
+	const char *staging = getenv ("CBX_STAGING");
+	if (staging && *staging) {
+		int m = !strcmp (staging, "zerocopy") ? CBX_STAGING_ZEROCOPY : !strcmp (staging, "dma") ? CBX_STAGING_DMA : -1;
+		if (m < 0) {
+			fprintf (stderr, "error: CBX_STAGING=%s (zerocopy or dma)\n", staging);
+			exit (1);
+		}
+		fatal_or (cbx_set_staging_mode (theGPU, m));
+	}
+	int on;
+	long long v = env_int ("CBX_BUCKET_ELEMENTS", &on);
+	if (on) fatal_or (cbx_set_bucket_elements (theGPU, v));
+	v = env_int ("CBX_PIPELINE_MODE", &on);
+	if (on) fatal_or (cbx_set_pipeline_mode (theGPU, (int) v));
+	v = env_int ("CBX_CROSS_WAIT_STRIDE", &on);
+	if (on) fatal_or (cbx_set_cross_wait_stride (theGPU, (int) v));
+	v = env_int ("CBX_ALLREDUCE_GROUP", &on);
+	if (on) fatal_or (cbx_set_allreduce_group (theGPU, (int) v));
+}
+
 /* GPU.c:21-63.  Thread-count / core-offset arguments configure the reference's
  * task and callback handler threads, which are not on this path. */
 NATIVE(jint, init) (JNIEnv *env, jobject obj, jintArray devices, jint streams, jint callbacks,
@@ -50,7 +108,9 @@ NATIVE(jint, init) (JNIEnv *env, jobject obj, jintArray devices, jint streams, j
 	jint *argv = (*env)->GetIntArrayElements (env, devices, 0);
 	int rc = cbx_init (&theGPU, (const int *) argv, (int) argc);
 	(*env)->ReleaseIntArrayElements (env, devices, argv, JNI_ABORT);
-	return fatal_or (rc);
+	fatal_or (rc);
+	configure_from_env ();
+	return 0;
 }
 
 NATIVE(jint, free) (JNIEnv *env, jobject obj) {

@@ -39,9 +39,25 @@ def test_jni_natives_end_to_end():
     assert "jni_driver: ok" in r.stdout
 
 
-@pytest.mark.parametrize("G", [2, 4, 8])
-def test_jni_natives_single_process_multi_device(G):
+@pytest.mark.parametrize("G,env", [(2, {}), (4, {}), (8, {}),
+                                   # the pipeline settings a deployment picks through the environment
+                                   (4, {"CBX_ALLREDUCE": "rsag", "CBX_BUCKET_ELEMENTS": "4096",
+                                        "CBX_PIPELINE_MODE": "1", "CBX_CROSS_WAIT_STRIDE": "2"}),
+                                   (4, {"CBX_ALLREDUCE": "peer"}),
+                                   (2, {"CBX_BUCKET_ELEMENTS": "8192", "CBX_ALLREDUCE_GROUP": "2",
+                                        "CBX_STAGING": "dma"})])
+def test_jni_natives_single_process_multi_device(G, env):
     assert os.path.exists(EXE_LOOPBACK), "run scripts/build_fake_rccl.sh (or __graft_entry__.build()) first"
-    r = subprocess.run([EXE_LOOPBACK, str(G)], capture_output=True, text=True, timeout=110)
+    r = subprocess.run([EXE_LOOPBACK, str(G)], capture_output=True, text=True, timeout=110,
+                       env=dict(os.environ, **env))
     assert r.returncode == 0, (r.stdout + r.stderr)[-4000:]
     assert f"jni_driver: ok (G={G})" in r.stdout
+
+
+def test_jni_environment_settings_are_checked():
+    # a refused setting is fatal at init, as every error of the shim is
+    assert os.path.exists(EXE_LOOPBACK)
+    for env in ({"CBX_ALLREDUCE": "ring"}, {"CBX_PIPELINE_MODE": "7"}, {"CBX_BUCKET_ELEMENTS": "12x"}):
+        r = subprocess.run([EXE_LOOPBACK, "2"], capture_output=True, text=True, timeout=110,
+                           env=dict(os.environ, **env))
+        assert r.returncode != 0 and "error:" in r.stderr, (env, r.stderr[-2000:])
