@@ -316,7 +316,13 @@ def main():
             "replicas_per_gpu": args.replicas,
             "alpha": args.alpha,
             "momentum": args.momentum,
+            # SURVEY 8(d)'s per-GPU bytes of the step, the unit `value` counts in
+            # whichever collective form runs; the reduce-scatter form moves fewer
+            # (kernel B without momentum plus the momentum pass on 1/G), shown apart
             "bytes_per_step_per_gpu": step_bytes,
+            "hbm_bytes_moved_per_step_per_gpu": (
+                step_bytes if not (split and ar_algo == 2) else
+                (12 * args.replicas + 8) * n + 12 * n + (12 * n // G if args.momentum > 0 else 0)),
             "parallelism": f"sma-dp{G}",
             "pipeline": "fused" if not split else "accumulate+rccl-allreduce+apply, bucketed on two streams",
             "buckets": (None if not split else int(min(tuning, key=lambda k: tuning[k]).split("/")[0]) if tuning
