@@ -76,6 +76,8 @@ CASES = [
 def _jobs(G):
     if G == 3:  # a non-power-of-two clique: the plain step in both orders, and the peer path (RSAG is refused)
         names = ("sma", "sma-ring", "sma-peer", "sma-peer-empty-shards")
+    elif G == 16:  # the most devices one process takes (kMaxDevices): plain, ring order, peer, reduce-scatter
+        names = ("sma-copy-ssp", "sma-ring", "sma-peer", "sma-peer-empty-shards", "sma-rsag", "sma-rsag-ring")
     elif G == 8:
         names = ("sma-copy-ssp", "sma-buckets-cross", "ssgd-buckets", "sma-ring", "sma-ring-buckets-cross",
                  "sma-peer", "sma-peer-empty-shards", "sma-peer-switch", "sma-rsag", "sma-rsag-buckets-cross",
@@ -121,7 +123,7 @@ def _worker(G, jobs, ckdir, q):
 
 
 @pytest.mark.skipif(not os.path.exists(C.VARIANT), reason="run scripts/build_fake_rccl.sh first")
-@pytest.mark.parametrize("G", [2, 3, 4, 8])
+@pytest.mark.parametrize("G", [2, 3, 4, 8, 16])
 def test_one_process_many_devices_vs_oracle(G):
     import multiprocessing as mp
     jobs = _jobs(G)
