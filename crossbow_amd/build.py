@@ -55,11 +55,27 @@ def build_lib(force: bool = False, verbose: bool = False) -> str:
     if not force and not _stale(LIB, _deps()):
         return LIB
     tmp = LIB + ".tmp"
-    cmd = [_hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wall",
-           # fp32 results must equal the reference's cuBLAS op order bit for bit: every
-           # fma is written explicitly, nothing may be contracted behind our back.
-           "-ffp-contract=off",
-           "-I", os.path.join(ROOT, "include"), "-o", tmp] + _sources() + ["-lrccl", "-lrocprofiler-sdk-roctx", "-lpthread"]
+    objdir = os.path.join(PKG, "build")
+    os.makedirs(objdir, exist_ok=True)
+    objs = []
+    for src in _sources():
+        stem = os.path.splitext(os.path.basename(src))[0]
+        obj = os.path.join(objdir, stem + ".o")
+        cmd = [_hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall",
+               # A fixed compilation-unit id per source instead of one hashed from
+               # its path: the device code (and code_object_digest) is then the
+               # same wherever the tree is built.
+               f"-cuid=crossbow_{stem}",
+               # fp32 results must equal the reference's cuBLAS op order bit for bit: every
+               # fma is written explicitly, nothing may be contracted behind our back.
+               "-ffp-contract=off",
+               "-I", os.path.join(ROOT, "include"), "-c", "-o", obj, src]
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        subprocess.run(cmd, check=True)
+        objs.append(obj)
+    cmd = [_hipcc(), f"--offload-arch={ARCH}", "-shared", "-o", tmp] + objs + \
+        ["-lrccl", "-lrocprofiler-sdk-roctx", "-lpthread"]
     if verbose:
         print(" ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)
