@@ -139,6 +139,18 @@ def cpu_c1(seconds=3.0):
             "sample": f"C1 LeNet n={n}, 2 replicas, mu 0, full size, {steps} steps in {el:.1f} s"}
 
 
+def cpu_model() -> str:
+    """The host CPU's model name (/proc/cpuinfo), for the baseline's record."""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def cpu_baseline(args, n_full):
     """The reference's call sequence (memset, memcpy + 3 saxpy per replica,
     momentum, apply) on OpenBLAS, 1 thread bound to core 0 like TheCPU.bind(0)
@@ -442,6 +454,7 @@ def main():
             threads = max(1, min(16, len(os.sched_getaffinity(0))))
             mt = cpu_baseline_threads(args, n, threads)
             result["cpu_baseline"] = cpu_baseline(args, n)
+            result["cpu_baseline"]["cpu_model"] = mt["cpu_model"] = cpu_model()
             result["cpu_baseline_multithread"] = mt
             result["cpu_c1_lenet"] = cpu_c1()
         else:
