@@ -87,12 +87,13 @@ static void configure_from_env (void) {
 	int on;
 	long long v = env_int ("CBX_BUCKET_ELEMENTS", &on);
 	if (on) fatal_or (cbx_set_bucket_elements (theGPU, v));
+	/* the int settings: out-of-range values go to the setter as -1 (refused) */
 	v = env_int ("CBX_PIPELINE_MODE", &on);
-	if (on) fatal_or (cbx_set_pipeline_mode (theGPU, (int) v));
+	if (on) fatal_or (cbx_set_pipeline_mode (theGPU, v < 0 || v > 4096 ? -1 : (int) v));
 	v = env_int ("CBX_CROSS_WAIT_STRIDE", &on);
-	if (on) fatal_or (cbx_set_cross_wait_stride (theGPU, (int) v));
+	if (on) fatal_or (cbx_set_cross_wait_stride (theGPU, v < 0 || v > 4096 ? -1 : (int) v));
 	v = env_int ("CBX_ALLREDUCE_GROUP", &on);
-	if (on) fatal_or (cbx_set_allreduce_group (theGPU, (int) v));
+	if (on) fatal_or (cbx_set_allreduce_group (theGPU, v < 0 || v > 4096 ? -1 : (int) v));
 }
 
 /* GPU.c:21-63.  Thread-count / core-offset arguments configure the reference's

@@ -57,7 +57,8 @@ def test_jni_natives_single_process_multi_device(G, env):
 def test_jni_environment_settings_are_checked():
     # a refused setting is fatal at init, as every error of the shim is
     assert os.path.exists(EXE_LOOPBACK)
-    for env in ({"CBX_ALLREDUCE": "ring"}, {"CBX_PIPELINE_MODE": "7"}, {"CBX_BUCKET_ELEMENTS": "12x"}):
+    for env in ({"CBX_ALLREDUCE": "ring"}, {"CBX_PIPELINE_MODE": "7"}, {"CBX_BUCKET_ELEMENTS": "12x"},
+                {"CBX_PIPELINE_MODE": "4294967297"}, {"CBX_ALLREDUCE_GROUP": "0"}):
         r = subprocess.run([EXE_LOOPBACK, "2"], capture_output=True, text=True, timeout=110,
                            env=dict(os.environ, **env))
         assert r.returncode != 0 and "error:" in r.stderr, (env, r.stderr[-2000:])
