@@ -1,7 +1,8 @@
 """Build the native pieces of crossbow_amd in-tree.
 
 * ``crossbow_amd/libcrossbow_sma.so``  -- the C-ABI library (hipcc, gfx950):
-  csrc/context.hip + csrc/sync_steps.hip + csrc/sma_kernels.hip, linked against RCCL.
+  csrc/context.hip + csrc/sync_steps.hip + csrc/sma_kernels.hip + csrc/sma_seam.hip,
+  linked against RCCL.
 * ``crossbow_amd/libGPU.so``           -- the JNI shim exporting Crossbow's
   ``TheGPU`` model-path natives; built only where ``jni.h`` exists (there is
   no JDK in this image).
@@ -31,7 +32,7 @@ def _hipcc() -> str:
     raise RuntimeError("hipcc not found: the MI355X library needs ROCm's hipcc")
 
 
-SOURCES = ("context.hip", "sync_steps.hip", "sma_kernels.hip")
+SOURCES = ("context.hip", "sync_steps.hip", "sma_kernels.hip", "sma_seam.hip")
 HEADERS = ("context_internal.h", "sma_internal.h")
 
 

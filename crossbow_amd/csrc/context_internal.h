@@ -482,7 +482,9 @@ inline int gfx950_device_count(int *count) {
   return CBX_OK;
 }
 
-inline int open_device(Device &d, int hip_id, int g) {
+// A visible gfx950 device: its CU count, and it becomes the current device.
+// Anything else fails loudly (no CPU fallback).
+inline int probe_device(int hip_id, int *num_cus) {
   int total = 0;
   hipError_t ce = hipGetDeviceCount(&total);
   if (ce != hipSuccess) {
@@ -495,11 +497,16 @@ inline int open_device(Device &d, int hip_id, int g) {
   if (std::strncmp(p.gcnArchName, "gfx950", 6) != 0)
     return fail(CBX_ERR_NO_DEVICE, "device %d is %s, this library is built for gfx950 (MI355X) only", hip_id,
                 p.gcnArchName);
+  *num_cus = p.multiProcessorCount;
+  HIP_TRY(hipSetDevice(hip_id));
+  return CBX_OK;
+}
+
+inline int open_device(Device &d, int hip_id, int g) {
+  TRY(probe_device(hip_id, &d.num_cus));
   d.hip_id = hip_id;
   d.g = g;
   d.file_id = g;
-  d.num_cus = p.multiProcessorCount;
-  HIP_TRY(hipSetDevice(hip_id));
   // executioncontext.c:324: one non-blocking model-synchronisation stream.
   HIP_TRY(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
   HIP_TRY(hipStreamCreateWithFlags(&d.comm_stream, hipStreamNonBlocking));

@@ -1,0 +1,391 @@
+// sma_seam.hip -- the SMA step and the replica optimiser step over buffers the
+// CALLER owns: the seam at crossbowSynchronisationSMA (clib-multigpu/synch/
+// sma.c:233-248 -> :13-231) and at crossbowKernelOptimiserSMA
+// (kernels/optimisers/sma.cu:3-100) for a Crossbow build that keeps its own
+// model manager, model buffers and task side (modelmanager.c, model.c,
+// executioncontext.c) and replaces only those two function bodies.
+//
+// The context API (context.hip) owns an arena whose buffers are padded to
+// whole kernel trips; the reference's buffers hold exactly `elements` floats.
+// So every step here is the bulk of the buffers through the same float4
+// kernels (n4b float4s, a multiple of kPadFloat4) plus a scalar tail kernel
+// over the last < 4 * kPadFloat4 + 3 elements, with the same fma sequence per
+// element: the results equal the context path's and the oracle's bit for bit.
+//
+// The plan owns what the step needs beyond the caller's buffers: the
+// accumulator and the all-reduced difference (base->gradient and base->diff
+// in the reference, sma.c:66,82) with the 256-byte control block that carries
+// the Phase-D request count through the all-reduce, and -- unless the caller
+// hands over its own (executioncontext.c:185-201) -- the RCCL communicators.
+#include "context_internal.h"
+
+using namespace cbx::host;
+
+namespace {
+
+// Elements [lo, hi) outside the float4 kernels' trips.  phase 0: the fused
+// one-GPU step; 1: kernel A (Phase A into acc); 2: kernel B (Phase C, and
+// Phase D when the reduced control block counts a request).
+struct TailArgs {
+  const float *s[cbx::kMaxReplicas];
+  float *w[cbx::kMaxReplicas];
+  float *z;
+  float *last;  // null without base momentum
+  float *acc;
+  const float *D;
+  float *ctrl_out;       // phase 1: write this device's control block (when the bulk launch does not)
+  const float *ctrl_in;  // phase 2: the reduced control block
+  int64_t lo, hi;
+  float alpha;
+  float copies;
+  int nrep;
+  int phase;
+  int copy;  // phase 0: Phase D requested
+  int pad_;
+};
+
+__global__ __launch_bounds__(256) void sma_tail_kernel(const TailArgs a) {
+  if (a.ctrl_out != nullptr && blockIdx.x == 0 && threadIdx.x < cbx::kCtrlFloats)
+    a.ctrl_out[threadIdx.x] = (threadIdx.x == 0) ? a.copies : 0.0f;
+  const int64_t i = a.lo + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= a.hi) return;
+  if (a.phase == 2) {
+    float D = a.D[i];
+    if (a.last) {
+      D = fmaf(cbx::kBaseMomentum, a.last[i], D);  // sma.c:155-164
+      a.last[i] = D;
+    }
+    const float z = fmaf(1.0f, D, a.z[i]);  // sma.c:169-174
+    a.z[i] = z;
+    if (a.ctrl_in[0] > 0.0f)
+      for (int r = 0; r < a.nrep; ++r) a.w[r][i] = z;  // sma.c:185-227
+    return;
+  }
+  const float z0 = a.z[i];
+  float acc = 0.0f;  // sma.c:66
+  for (int r = 0; r < a.nrep; ++r) {
+    const float d = fmaf(-1.0f, z0, a.s[r][i]);  // sma.c:79-90
+    a.w[r][i] = fmaf(-a.alpha, d, a.w[r][i]);    // :93-99
+    acc = fmaf(a.alpha, d, acc);                 // :102-107
+  }
+  if (a.phase == 1) {
+    a.acc[i] = acc;
+    return;
+  }
+  float D = acc;  // common.c:3-57 with one rank
+  if (a.last) {
+    D = fmaf(cbx::kBaseMomentum, a.last[i], D);
+    a.last[i] = D;
+  }
+  const float z = fmaf(1.0f, D, z0);
+  a.z[i] = z;
+  if (a.copy)
+    for (int r = 0; r < a.nrep; ++r) a.w[r][i] = z;
+}
+
+// The optimiser step's tail (kernels/optimisers/sma.cu:3-100, the same
+// per-element sequence as sma_optimise_kernel).
+__global__ __launch_bounds__(256) void sma_optimise_tail_kernel(float *w, float *g, float *last, float *s, int64_t lo,
+                                                                int64_t hi, float rate, float mu, float wd) {
+  const int64_t i = lo + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= hi) return;
+  const float wv = w[i];
+  float gv = g[i];
+  if (wd > 0.0f) gv = fmaf(wd, wv, gv);  // :24-31
+  s[i] = wv;                             // :71 / :87
+  if (mu > 0.0f) {
+    gv = rate * gv;              // :52-56
+    gv = fmaf(mu, last[i], gv);  // :59-64
+    last[i] = gv;                // :68
+    w[i] = fmaf(1.0f, gv, wv);   // :74
+    g[i] = gv;
+  } else {
+    w[i] = fmaf(rate, gv, wv);  // :90
+    if (wd > 0.0f) g[i] = gv;
+  }
+}
+
+hipError_t launch_tail(const TailArgs &a, hipStream_t st) {
+  const int64_t len = a.hi - a.lo;
+  if (len <= 0 && !a.ctrl_out) return hipSuccess;
+  const unsigned blocks = (unsigned)std::max<int64_t>(1, (len + 255) / 256);
+  hipLaunchKernelGGL(sma_tail_kernel, dim3(blocks), dim3(256), 0, st, a);
+  return hipGetLastError();
+}
+
+bool aligned16(const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
+
+int cus_of_current_device(int *cus) {
+  int dev = 0;
+  HIP_TRY(hipGetDevice(&dev));
+  static std::atomic<int> cache[cbx::kMaxDevices * 4] = {};
+  if (dev >= 0 && dev < (int)(sizeof(cache) / sizeof(cache[0])) && cache[dev].load(std::memory_order_relaxed) > 0) {
+    *cus = cache[dev].load(std::memory_order_relaxed);
+    return CBX_OK;
+  }
+  int n = 0;
+  HIP_TRY(hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev));
+  if (dev >= 0 && dev < (int)(sizeof(cache) / sizeof(cache[0]))) cache[dev].store(n, std::memory_order_relaxed);
+  *cus = n;
+  return CBX_OK;
+}
+
+// Largest whole-trip prefix of an n-float buffer, in float4s.
+int64_t bulk_float4s(int64_t n) { return (n / 4) / cbx::kPadFloat4 * cbx::kPadFloat4; }
+
+}  // namespace
+
+struct cbx_sma_plan {
+  struct Dev {
+    int hip_id = 0;
+    int num_cus = 256;
+    ncclComm_t comm = nullptr;
+    bool own_comm = false;
+    char *scratch = nullptr;  // [ctrl | acc (padded)] [ctrl | D (padded)]
+    float *acc_ctrl = nullptr;
+    float *D_ctrl = nullptr;
+  };
+  std::vector<Dev> devs;
+  int64_t n = 0;
+  int64_t n4b = 0;  // bulk float4s
+  int ranks = 1;    // ranks of the communicator (1: no collective)
+  cbx::LaunchConfig cfg;
+  cbx::LaunchConfig apply_cfg = cbx::sma_apply_launch_config();
+};
+
+extern "C" {
+
+int cbx_sma_plan_free(cbx_sma_plan *p) {
+  if (!p) return CBX_OK;
+  for (auto &d : p->devs) {
+    (void)hipSetDevice(d.hip_id);
+    (void)hipDeviceSynchronize();
+    if (d.own_comm && d.comm) (void)ncclCommDestroy(d.comm);
+    if (d.scratch) (void)hipFree(d.scratch);
+  }
+  delete p;
+  return CBX_OK;
+}
+
+int cbx_sma_plan_create(cbx_sma_plan **out, const int *devices, int ndevices, long long elements,
+                        void *const *comms) {
+  if (!out || !devices || ndevices <= 0 || ndevices > cbx::kMaxDevices)
+    return fail(CBX_ERR_INVALID, "cbx_sma_plan_create: need 1..%d devices", cbx::kMaxDevices);
+  *out = nullptr;
+  // model.h:35 `int bytes`; the kernels address a buffer with 32-bit byte offsets.
+  if (elements <= 0 || elements * 4 + 4096 >= (1ll << 32))
+    return fail(CBX_ERR_INVALID, "cbx_sma_plan_create: %lld elements out of range", elements);
+  cbx_sma_plan *p = new cbx_sma_plan();
+  p->n = elements;
+  p->n4b = bulk_float4s(elements);
+  p->devs.resize(ndevices);
+  const int64_t pad = cbx::kPadFloat4;
+  const int64_t n4 = ((elements + 3) / 4 + pad - 1) / pad * pad;
+  const size_t half = ((size_t)cbx::kCtrlFloats * 4 + (size_t)n4 * 16 + 255) / 256 * 256;
+  for (int k = 0; k < ndevices; ++k) {
+    auto &d = p->devs[k];
+    int rc = probe_device(devices[k], &d.num_cus);
+    if (rc < 0) {
+      std::string msg = g_last_error;
+      cbx_sma_plan_free(p);
+      return fail(rc, "%s", msg.c_str());
+    }
+    d.hip_id = devices[k];
+    hipError_t e = hipMalloc(reinterpret_cast<void **>(&d.scratch), 2 * half);
+    if (e == hipSuccess) e = hipMemset(d.scratch, 0, 2 * half);
+    if (e != hipSuccess) {
+      cbx_sma_plan_free(p);
+      return fail(CBX_ERR_HIP, "plan scratch of %zu bytes: %s", 2 * half, hipGetErrorString(e));
+    }
+    d.acc_ctrl = reinterpret_cast<float *>(d.scratch);
+    d.D_ctrl = reinterpret_cast<float *>(d.scratch + half);
+  }
+  if (comms) {
+    for (int k = 0; k < ndevices; ++k) {
+      p->devs[k].comm = static_cast<ncclComm_t>(comms[k]);
+      if (!p->devs[k].comm) {
+        cbx_sma_plan_free(p);
+        return fail(CBX_ERR_INVALID, "cbx_sma_plan_create: null communicator for device %d", k);
+      }
+    }
+    int count = 0;
+    ncclResult_t r = ncclCommCount(p->devs[0].comm, &count);
+    if (r != ncclSuccess) {
+      cbx_sma_plan_free(p);
+      return fail(CBX_ERR_RCCL, "ncclCommCount: %s", ncclGetErrorString(r));
+    }
+    p->ranks = count;
+  } else if (ndevices > 1) {
+    // executioncontext.c:185-201
+    std::vector<ncclComm_t> cs(ndevices);
+    ncclResult_t r = ncclCommInitAll(cs.data(), ndevices, devices);
+    if (r != ncclSuccess) {
+      cbx_sma_plan_free(p);
+      return fail(CBX_ERR_RCCL, "ncclCommInitAll: %s", ncclGetErrorString(r));
+    }
+    for (int k = 0; k < ndevices; ++k) {
+      p->devs[k].comm = cs[k];
+      p->devs[k].own_comm = true;
+    }
+    p->ranks = ndevices;
+  }
+  if (p->ranks < ndevices) {
+    cbx_sma_plan_free(p);
+    return fail(CBX_ERR_INVALID, "communicator of %d ranks for %d local devices", p->ranks, ndevices);
+  }
+  *out = p;
+  return CBX_OK;
+}
+
+int cbx_sma_plan_step(cbx_sma_plan *p, void *const *streams, float *const *z, float *const *last, int nreplicas,
+                      const int *replica_device, float *const *w, const float *const *s, const int *locked,
+                      const int *copy, float alpha, float momentum, int first) {
+  TraceRange trace("cbx_sma_plan_step");
+  if (!p) return fail(CBX_ERR_INVALID, "null plan");
+  const int G = (int)p->devs.size();
+  if (!streams || !z || nreplicas < 0 || (nreplicas > 0 && (!replica_device || !w || !s || !locked || !copy)))
+    return fail(CBX_ERR_INVALID, "cbx_sma_plan_step: missing arguments");
+  if (first < 0 || first > nreplicas) return fail(CBX_ERR_INVALID, "first replica %d out of range", first);
+  const bool mom = momentum > 0.0f;  // sma.c:150: base momentum forced to 0.9 when > 0
+  if (mom && !last) return fail(CBX_ERR_INVALID, "base momentum > 0 needs the base models' last buffers");
+  // Per device: its locked replicas from `first` on, in id order (sma.c:69-73).
+  std::vector<cbx::SmaArgs> args(G);
+  std::vector<TailArgs> tails(G);
+  int copies_total = 0;
+  for (int k = 0; k < G; ++k) {
+    std::memset(&args[k], 0, sizeof(cbx::SmaArgs));
+    std::memset(&tails[k], 0, sizeof(TailArgs));
+    if (!z[k] || !aligned16(z[k]) || (mom && (!last[k] || !aligned16(last[k]))))
+      return fail(CBX_ERR_INVALID, "device %d: base buffers must be non-null and 16-byte aligned", k);
+  }
+  for (int id = first; id < nreplicas; ++id) {
+    if (!locked[id]) continue;
+    const int k = replica_device[id];
+    if (k < 0 || k >= G) return fail(CBX_ERR_INVALID, "replica %d on device %d of %d", id, k, G);
+    if (!w[id] || !s[id] || !aligned16(w[id]) || !aligned16(s[id]))
+      return fail(CBX_ERR_INVALID, "replica %d: buffers must be non-null and 16-byte aligned", id);
+    cbx::SmaArgs &a = args[k];
+    if (a.nrep >= cbx::kMaxReplicas)
+      return fail(CBX_ERR_UNSUPPORTED, "more than %d locked replicas on one device", cbx::kMaxReplicas);
+    a.s[a.nrep] = reinterpret_cast<const cbx::v4f *>(s[id]);
+    a.w[a.nrep] = reinterpret_cast<cbx::v4f *>(w[id]);
+    tails[k].s[a.nrep] = s[id];
+    tails[k].w[a.nrep] = w[id];
+    if (copy[id]) {
+      a.copies += 1.0f;  // sma.c:113-120
+      ++copies_total;
+    }
+    ++a.nrep;
+  }
+  const int64_t lo = p->n4b * 4;
+  for (int k = 0; k < G; ++k) {
+    auto &d = p->devs[k];
+    cbx::SmaArgs &a = args[k];
+    a.z = reinterpret_cast<cbx::v4f *>(z[k]);
+    a.last = mom ? reinterpret_cast<cbx::v4f *>(last[k]) : nullptr;
+    a.acc = reinterpret_cast<cbx::v4f *>(d.acc_ctrl + cbx::kCtrlFloats);
+    a.D = reinterpret_cast<const cbx::v4f *>(d.D_ctrl + cbx::kCtrlFloats);
+    a.ctrl_out = d.acc_ctrl;
+    a.ctrl_in = d.D_ctrl;
+    a.n4 = p->n4b;
+    a.alpha = alpha;  // sma.c:33
+    TailArgs &t = tails[k];
+    t.z = z[k];
+    t.last = mom ? last[k] : nullptr;
+    t.acc = d.acc_ctrl + cbx::kCtrlFloats;
+    t.D = d.D_ctrl + cbx::kCtrlFloats;
+    t.ctrl_in = d.D_ctrl;
+    t.lo = lo;
+    t.hi = p->n;
+    t.alpha = alpha;
+    t.copies = a.copies;
+    t.nrep = a.nrep;
+    t.copy = copies_total > 0;
+  }
+  if (p->ranks == 1) {
+    // One GPU: the all-reduce of one buffer is the identity, so Phases A + C
+    // (+ D) fuse into one pass, as in the context's G = 1 step.
+    auto &d = p->devs[0];
+    hipStream_t st = static_cast<hipStream_t>(streams[0]);
+    HIP_TRY(hipSetDevice(d.hip_id));
+    cbx::LaunchConfig cfg = p->cfg;
+    cfg.num_cus = d.num_cus;
+    if (p->n4b > 0) HIP_TRY(cbx::launch_sma_fused(args[0], mom, copies_total > 0, cfg, st));
+    tails[0].phase = 0;
+    HIP_TRY(launch_tail(tails[0], st));
+    return copies_total > 0 ? 1 : 0;
+  }
+  // G > 1: kernel A, one grouped all-reduce of the control block + acc
+  // (common.c:14-54), kernel B -- in order on each device's stream.
+  for (int k = 0; k < G; ++k) {
+    auto &d = p->devs[k];
+    hipStream_t st = static_cast<hipStream_t>(streams[k]);
+    HIP_TRY(hipSetDevice(d.hip_id));
+    cbx::LaunchConfig cfg = p->cfg;
+    cfg.num_cus = d.num_cus;
+    if (p->n4b > 0) HIP_TRY(cbx::launch_sma_accumulate(args[k], true, cfg, st));
+    TailArgs t = tails[k];
+    t.phase = 1;
+    if (p->n4b == 0) {  // no bulk launch wrote the control block
+      t.ctrl_out = d.acc_ctrl;
+    }
+    HIP_TRY(launch_tail(t, st));
+  }
+  NCCL_TRY(ncclGroupStart());
+  for (int k = 0; k < G; ++k) {
+    auto &d = p->devs[k];
+    HIP_TRY(hipSetDevice(d.hip_id));
+    NCCL_TRY(ncclAllReduce(d.acc_ctrl, d.D_ctrl, (size_t)(cbx::kCtrlFloats + p->n), ncclFloat, ncclSum, d.comm,
+                           static_cast<hipStream_t>(streams[k])));
+  }
+  NCCL_TRY(ncclGroupEnd());
+  for (int k = 0; k < G; ++k) {
+    auto &d = p->devs[k];
+    hipStream_t st = static_cast<hipStream_t>(streams[k]);
+    HIP_TRY(hipSetDevice(d.hip_id));
+    cbx::LaunchConfig cfg = p->apply_cfg;
+    cfg.num_cus = d.num_cus;
+    if (p->n4b > 0) HIP_TRY(cbx::launch_sma_apply(args[k], mom, cfg, st));
+    TailArgs t = tails[k];
+    t.phase = 2;
+    HIP_TRY(launch_tail(t, st));
+  }
+  return copies_total > 0 ? 1 : 0;
+}
+
+int cbx_sma_optimise_buffers(void *stream, float *w, float *g, float *last, float *s, long long elements,
+                             float learning_rate, float momentum, float weight_decay) {
+  TraceRange trace("cbx_sma_optimise_buffers");
+  if (elements <= 0 || elements * 4 + 4096 >= (1ll << 32))
+    return fail(CBX_ERR_INVALID, "cbx_sma_optimise_buffers: %lld elements out of range", elements);
+  if (!w || !g || !s || (momentum > 0.0f && !last))
+    return fail(CBX_ERR_INVALID, "cbx_sma_optimise_buffers: missing buffers");
+  if (!aligned16(w) || !aligned16(g) || !aligned16(s) || (momentum > 0.0f && !aligned16(last)))
+    return fail(CBX_ERR_INVALID, "cbx_sma_optimise_buffers: buffers must be 16-byte aligned");
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  int cus = 256;
+  TRY(cus_of_current_device(&cus));
+  cbx::OptArgs a;
+  std::memset(&a, 0, sizeof(a));
+  a.w = reinterpret_cast<cbx::v4f *>(w);
+  a.g = reinterpret_cast<cbx::v4f *>(g);
+  a.last = momentum > 0.0f ? reinterpret_cast<cbx::v4f *>(last) : nullptr;
+  a.s = reinterpret_cast<cbx::v4f *>(s);
+  a.n4 = bulk_float4s(elements);
+  a.rate = -1.0f * learning_rate;  // sma.cu:43
+  a.momentum = momentum;
+  a.wd = weight_decay;
+  cbx::LaunchConfig cfg = cbx::aux_launch_config();
+  cfg.num_cus = cus;
+  if (a.n4 > 0) HIP_TRY(cbx::launch_sma_optimise(a, cfg, st));
+  const int64_t lo = a.n4 * 4;
+  if (elements > lo) {
+    const unsigned blocks = (unsigned)((elements - lo + 255) / 256);
+    hipLaunchKernelGGL(sma_optimise_tail_kernel, dim3(blocks), dim3(256), 0, st, w, g, a.last ? last : nullptr, s, lo,
+                       (int64_t)elements, a.rate, momentum, weight_decay);
+    HIP_TRY(hipGetLastError());
+  }
+  return CBX_OK;
+}
+
+}  // extern "C"

@@ -422,6 +422,62 @@ int cbx_fill_synthetic (cbx_context *ctx, unsigned long long seed);
  * buffer, `iters` timed launches; writes achieved GB/s (read + write).    */
 int cbx_bench_copy (cbx_context *ctx, size_t bytes, int iters, float *gbps);
 
+/* ---- the sma.c seam: buffers owned by the caller ------------------------
+ * For a Crossbow build that keeps its own model manager, model buffers and
+ * task side (modelmanager.c, model.c, executioncontext.c, the callback and
+ * task handlers, all untouched) and replaces only two function bodies:
+ *   crossbowSynchronisationSMA (synch/sma.c:233-248 -> :13-231)
+ *       -> cbx_sma_plan_step
+ *   crossbowKernelOptimiserSMA (kernels/optimisers/sma.cu:3-100)
+ *       -> cbx_sma_optimise_buffers
+ * (INTEGRATION.md section 3 shows both bodies).  Buffers hold exactly
+ * `elements` floats (no padding) and must be 16-byte aligned, as hipMalloc's
+ * are.  Same kernels and arithmetic as the context path: bit-exact against
+ * the oracle at one GPU and in rank order.  No context is involved.       */
+typedef struct cbx_sma_plan cbx_sma_plan;
+/* What the step needs beyond the caller's buffers, per device: the Phase-A
+ * accumulator and the all-reduced difference (base->gradient, base->diff in
+ * sma.c:66,82) with the control block that carries the Phase-D request
+ * count, and the communicators: `comms` = the caller's ncclComm_t per device
+ * (ctx->comms of executioncontext.c:185-201, as void*), or NULL to create
+ * them with ncclCommInitAll over `devices` (ndevices > 1).  `devices` are
+ * HIP device ids; `elements` = model->elements (model.h:35).             */
+int cbx_sma_plan_create (cbx_sma_plan **plan, const int *devices, int ndevices, long long elements,
+                         void *const *comms);
+int cbx_sma_plan_free (cbx_sma_plan *plan);
+/* One SMA step (sma.c:13-231), enqueued on the caller's streams, async:
+ *   streams[k]        dev->modelSynchronisationStream of devices[k] (hipStream_t)
+ *   z[k], last[k]     baseModels[k]->data->dev / ->last->dev (last may be NULL
+ *                     when momentum is 0, model.c:116-120)
+ *   nreplicas         modelmanager->size; for replica id:
+ *     replica_device[id]  position in `devices` of replicas[id]->dev
+ *     w[id], s[id]        replicas[id]->data->dev, replicas[id]->diff->dev
+ *     locked[id]          modelmanager->locked[id]
+ *     copy[id]            replicas[id]->conf->_copy
+ *   alpha             defaultModel->conf->alpha (sma.c:33)
+ *   momentum          the base model's conf->momentum: > 0 applies the
+ *                     hard-coded 0.9 (sma.c:150-152)
+ *   first             replicas below it take no part (sma.c:69)
+ * Locked replicas at or above `first` are averaged in id order per device.
+ * Returns 1 when Phase D ran (a locked replica from `first` on had _copy:
+ * every such replica now equals its device's base model; the caller resets
+ * their _copy, sma.c:217-220), 0 when not.  The caller's events
+ * (base->updated, synched[dev], replica->updated) are recorded on the same
+ * streams after the call, as sma.c:115,177,204,222 do.                   */
+int cbx_sma_plan_step (cbx_sma_plan *plan, void *const *streams, float *const *z, float *const *last,
+                       int nreplicas, const int *replica_device, float *const *w, const float *const *s,
+                       const int *locked, const int *copy, float alpha, float momentum, int first);
+/* The replica's optimiser step of one task (sma.cu:3-100) in one pass over
+ * its buffers, on `stream` (hipStream_t, the task stream; the current HIP
+ * device must be the buffers'): w = model->data, g = model->gradient
+ * (updated in place, as the reference leaves it), last = model->last (used
+ * iff momentum > 0), s = model->diff (the snapshot of w before the update);
+ * learning_rate = crossbowSolverConfGetLearningRate (conf, task)
+ * (solverconfiguration.c:116-162); momentum, weight_decay from the conf.
+ * Nesterov momentum stays the caller's err() (sma.cu:46-48).             */
+int cbx_sma_optimise_buffers (void *stream, float *w, float *g, float *last, float *s, long long elements,
+                              float learning_rate, float momentum, float weight_decay);
+
 #ifdef __cplusplus
 }
 #endif

@@ -11,7 +11,7 @@ N=tests/native
 mv "$N/libfakerccl.so.tmp" "$N/libfakerccl.so"
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -Wall -ffp-contract=off \
   -I include -o "$N/libcrossbow_sma_fakerccl.so.tmp" \
-  crossbow_amd/csrc/context.hip crossbow_amd/csrc/sync_steps.hip crossbow_amd/csrc/sma_kernels.hip \
+  crossbow_amd/csrc/context.hip crossbow_amd/csrc/sync_steps.hip crossbow_amd/csrc/sma_kernels.hip crossbow_amd/csrc/sma_seam.hip \
   -L "$N" -lfakerccl -Wl,-rpath,'$ORIGIN' -lrocprofiler-sdk-roctx -lpthread
 mv "$N/libcrossbow_sma_fakerccl.so.tmp" "$N/libcrossbow_sma_fakerccl.so"
 echo "built $N/libfakerccl.so $N/libcrossbow_sma_fakerccl.so"

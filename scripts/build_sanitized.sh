@@ -15,7 +15,7 @@ trap 'rm -rf "$TMP"' EXIT
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O1 -Xarch_host -gline-tables-only -std=c++17 -ffp-contract=off -fno-omit-frame-pointer \
   -Xarch_host -fsanitize=address -Xarch_host -fsanitize=undefined \
   -I include -o "$OUT.tmp" \
-  crossbow_amd/csrc/context.hip crossbow_amd/csrc/sync_steps.hip crossbow_amd/csrc/sma_kernels.hip -x none "$TMP/abi_driver.o" \
+  crossbow_amd/csrc/context.hip crossbow_amd/csrc/sync_steps.hip crossbow_amd/csrc/sma_kernels.hip crossbow_amd/csrc/sma_seam.hip -x none "$TMP/abi_driver.o" \
   -lrccl -lrocprofiler-sdk-roctx -lpthread
 mv "$OUT.tmp" "$OUT"
 echo "built $OUT"

@@ -274,6 +274,41 @@ int main (void) {
 
 	stress_autotune (n1, n2);
 
+	/* The sma.c seam over buffers the caller owns (here a context's, used as
+	 * plain device memory), ragged so the tail kernel runs, Phase D asked. */
+	c = setup (n1, n2, 2, CBX_SYNC_BSP, CBX_UPDATE_SMA, 0.9f);
+	{
+		const long long m = (long long) n - 5;
+		void *z = NULL, *last = NULL, *w0 = NULL, *w1 = NULL, *s0 = NULL, *s1 = NULL, *g = NULL, *lr = NULL;
+		CHECK (cbx_base_buffer (c, 0, CBX_BUF_DATA, &z));
+		CHECK (cbx_base_buffer (c, 0, CBX_BUF_LAST, &last));
+		CHECK (cbx_replica_buffer (c, 0, CBX_BUF_DATA, &w0));
+		CHECK (cbx_replica_buffer (c, 1, CBX_BUF_DATA, &w1));
+		CHECK (cbx_replica_buffer (c, 0, CBX_BUF_DIFF, &s0));
+		CHECK (cbx_replica_buffer (c, 1, CBX_BUF_DIFF, &s1));
+		CHECK (cbx_replica_buffer (c, 0, CBX_BUF_GRADIENT, &g));
+		CHECK (cbx_replica_buffer (c, 0, CBX_BUF_LAST, &lr));
+		cbx_sma_plan *plan = NULL;
+		int dev = 0;
+		CHECK (cbx_sma_plan_create (&plan, &dev, 1, m, NULL));
+		void *streams[1] = { NULL };
+		float *zz[1] = { (float *) z }, *ll[1] = { (float *) last }, *ww[2] = { (float *) w0, (float *) w1 };
+		const float *ss[2] = { (const float *) s0, (const float *) s1 };
+		int rdev[2] = { 0, 0 }, locked[2] = { 1, 1 }, copy[2] = { 0, 1 };
+		CHECK (cbx_sma_optimise_buffers (NULL, (float *) w0, (float *) g, (float *) lr, (float *) s0, m, 0.05f, 0.9f,
+			1e-4f));
+		EXPECT (cbx_sma_plan_step (plan, streams, zz, ll, 2, rdev, ww, ss, locked, copy, 0.1f, 0.9f, 0) == 1);
+		copy[1] = 0;
+		EXPECT (cbx_sma_plan_step (plan, streams, zz, ll, 2, rdev, ww, ss, locked, copy, 0.1f, 0.9f, 1) == 0);
+		EXPECT (cbx_sma_plan_step (plan, streams, zz, ll, 2, rdev, ww, ss, locked, copy, 0.1f, 0.9f, 3) == CBX_ERR_INVALID);
+		EXPECT (cbx_sma_plan_step (plan, streams, zz, NULL, 2, rdev, ww, ss, locked, copy, 0.1f, 0.9f, 0) == CBX_ERR_INVALID);
+		CHECK (cbx_sma_plan_free (plan));
+		CHECK (cbx_replica_read (c, 0, CBX_BUF_DATA, host, (size_t) 4 * n));
+		EXPECT (all_finite (host, (size_t) m));
+		EXPECT (cbx_sma_plan_create (&plan, &dev, 1, 0, NULL) == CBX_ERR_INVALID);
+	}
+	CHECK (cbx_free (c));
+
 	/* BN statistics averaging is a no-op with one device but walks its tables */
 	c = setup (n1, n2, 1, CBX_SYNC_BSP, CBX_UPDATE_SMA, 0.0f);
 	{

@@ -293,6 +293,12 @@ ncclResult_t ncclCommInitAll(ncclComm_t *comm, int ndev, const int *devlist) {
   return ncclSuccess;
 }
 
+ncclResult_t ncclCommCount(const ncclComm_t comm, int *count) {
+  if (!comm || !count) return ncclInvalidArgument;
+  *count = comm->nranks;
+  return ncclSuccess;
+}
+
 ncclResult_t ncclCommDestroy(ncclComm_t comm) {
   if (!comm) return ncclInvalidArgument;
   Clique *q = comm->clique;

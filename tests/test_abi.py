@@ -186,3 +186,19 @@ def test_code_object_digest_ties_traffic_to_the_build():
     for key, entry in tj.items():
         if key.startswith("sma_") and "code_object_sha256" in entry:
             assert re.fullmatch(r"[0-9a-f]{64}", entry["code_object_sha256"]), key
+
+
+def test_seam_fails_loudly_without_device():
+    # the sma.c seam (cbx_sma_plan_*) has no CPU fallback either
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is visible; this checks the no-device behaviour")
+    from crossbow_amd import CbxError, _lib
+    from crossbow_amd.seam import SmaPlan
+    with pytest.raises(CbxError) as e:
+        SmaPlan([0], 1024)
+    assert e.value.code == _lib.CBX_ERR_NO_DEVICE
+    lib = _lib.load()
+    assert lib.cbx_sma_plan_step(None, None, None, None, 0, None, None, None, None, None, 0.1, 0.0, 0) \
+        == _lib.CBX_ERR_INVALID
+    assert lib.cbx_sma_plan_free(None) == _lib.CBX_OK

@@ -1,0 +1,402 @@
+"""The sma.c seam: cbx_sma_plan_step / cbx_sma_optimise_buffers over buffers
+the CALLER owns (include/crossbow_sma.h, crossbow_amd/csrc/sma_seam.hip).
+
+A Crossbow build that keeps its own model manager replaces only the bodies of
+crossbowSynchronisationSMA (clib-multigpu/synch/sma.c:233-248 -> :13-231) and
+crossbowKernelOptimiserSMA (kernels/optimisers/sma.cu:3-100).  Its buffers hold
+exactly `elements` floats, so these cases use ragged sizes (the float4 bulk
+plus the scalar tail), buffers allocated by the test itself (torch, or raw
+hipMalloc in the torch-free workers), and the caller's own streams and
+communicators:
+
+* one GPU (the product library): the fused step, bit for bit against the
+  oracle, over sizes 1 .. LeNet, 1 .. 9 replicas, momentum 0 / 0.9, `first`,
+  unlocked replicas, Phase D, several steps back to back;
+* the optimiser step, bit for bit against the oracle's sma.cu restatement;
+* G devices in one process (the loopback clique, scripts/build_fake_rccl.sh):
+  communicators created by the plan (ncclCommInitAll) or handed over by the
+  caller, bit for bit in rank order, within the G > 1 tolerance in ring order;
+* G ranks with the REAL librccl (one process per rank, NCCL_HOSTID per rank,
+  as tests/test_gpu_realrccl.py): the caller's ncclCommInitRank communicator
+  spans the processes; bit for bit at G = 2, within the tolerance at G = 4,
+  z / last bitwise identical on every rank.
+"""
+from __future__ import annotations
+
+import ctypes
+import importlib.util
+import os
+import tempfile
+
+import numpy as np
+import pytest
+
+from tests import multidev_common as C
+
+pytestmark = pytest.mark.gpu
+
+ALPHA = 0.1
+
+
+def _bits_equal(got, want):
+    return np.array_equal(np.asarray(got, np.float32).view(np.uint32), np.asarray(want, np.float32).view(np.uint32))
+
+
+# (name, n, R, momentum, steps, first, held replica ids, {step: replica asking for Phase D})
+ONE_GPU = [
+    ("one-element", 1, 1, 0.9, 2, 0, (), {}),
+    ("three-elements-no-momentum", 3, 2, 0.0, 2, 0, (), {}),
+    ("ragged-4099", 4099, 4, 0.9, 3, 0, (), {1: 2}),
+    ("whole-trips", 4096 * 3, 8, 0.9, 2, 0, (), {}),
+    ("chunked-9-replicas", 65_541, 9, 0.9, 2, 0, (), {0: 3}),
+    ("first-and-held", 300_007, 8, 0.9, 2, 2, (5,), {1: 6}),
+    ("lenet-c2", 1_111_946, 4, 0.0, 2, 0, (), {}),
+    ("no-replica-locked", 10_001, 2, 0.9, 1, 0, (0, 1), {}),
+]
+
+
+@pytest.mark.parametrize("name,n,R,mom,steps,first,held,copy_at", ONE_GPU, ids=[c[0] for c in ONE_GPU])
+def test_seam_one_gpu_bitexact(name, n, R, mom, steps, first, held, copy_at):
+    import torch
+
+    from crossbow_amd.seam import SmaPlan
+    from oracle import oracle as O
+    st = O.make_state(n, 1, R, ALPHA, mom)
+    st.first = first
+    dev = torch.device("cuda:0")
+    z = torch.from_numpy(st.z[0].copy()).to(dev)
+    last = torch.from_numpy(st.last[0].copy()).to(dev) if mom > 0 else None
+    s = [torch.from_numpy(a.copy()).to(dev) for a in st.s]
+    w = [torch.from_numpy(a.copy()).to(dev) for a in st.w]
+    stream = torch.cuda.Stream()
+    torch.cuda.synchronize()
+    with SmaPlan([0], n) as plan:
+        for step in range(steps):
+            st.locked[:] = 1
+            for i in held:
+                st.locked[i] = 0
+            if step in copy_at:
+                st.copy[copy_at[step]] = 1
+            reps = [(0, w[i].data_ptr(), s[i].data_ptr(), int(st.locked[i]), int(st.copy[i])) for i in range(R)]
+            ran = plan.step([stream.cuda_stream], [z.data_ptr()], [last.data_ptr()] if last is not None else None,
+                            reps, ALPHA, mom, first)
+            copies = O.sma_step(st)  # resets the copy flags of the locked replicas it copied (sma.c:220)
+            assert ran == (1 if copies > 0 else 0), (step, ran, copies)
+        stream.synchronize()
+    assert _bits_equal(z.cpu().numpy(), st.z[0]), "z"
+    if last is not None:
+        assert _bits_equal(last.cpu().numpy(), st.last[0]), "last"
+    for i in range(R):
+        assert _bits_equal(w[i].cpu().numpy(), st.w[i]), f"w[{i}]"
+        assert _bits_equal(s[i].cpu().numpy(), st.s[i]), f"s[{i}] must be untouched"
+
+
+def test_seam_resnet50_full_size_bitexact():
+    """C3's buffers through the seam: n = 25,557,032 (not a multiple of the
+    kernels' 4096-float trip: a 2,088-element tail), 8 replicas, mu 0.9."""
+    import torch
+
+    from crossbow_amd.seam import SmaPlan
+    from oracle import oracle as O
+    n, R = 25_557_032, 8
+    st = O.make_state(n, 1, R, ALPHA, 0.9, threads=8)
+    dev = torch.device("cuda:0")
+    z = torch.from_numpy(st.z[0]).to(dev)
+    last = torch.from_numpy(st.last[0]).to(dev)
+    s = [torch.from_numpy(a).to(dev) for a in st.s]
+    w = [torch.from_numpy(a).to(dev) for a in st.w]
+    stream = torch.cuda.Stream()
+    torch.cuda.synchronize()
+    with SmaPlan([0], n) as plan:
+        reps = [(0, w[i].data_ptr(), s[i].data_ptr(), 1, 0) for i in range(R)]
+        assert plan.step([stream.cuda_stream], [z.data_ptr()], [last.data_ptr()], reps, ALPHA, 0.9) == 0
+        stream.synchronize()
+    O.sma_step(st)
+    assert _bits_equal(z.cpu().numpy(), st.z[0])
+    assert _bits_equal(last.cpu().numpy(), st.last[0])
+    for i in range(R):
+        assert _bits_equal(w[i].cpu().numpy(), st.w[i]), f"w[{i}]"
+
+
+@pytest.mark.parametrize("n", [1, 4099, 4096 * 2, 300_007])
+@pytest.mark.parametrize("mom,wd", [(0.9, 1e-4), (0.9, 0.0), (0.0, 1e-4), (0.0, 0.0)])
+def test_seam_optimise_bitexact(n, mom, wd):
+    import torch
+
+    from crossbow_amd.seam import optimise_buffers
+    from oracle import oracle as O
+    lr = 0.05
+    w0 = O.fill_normal(n, 11, 0.05)
+    g0 = O.fill_normal(n, 12, 0.01)
+    l0 = O.fill_normal(n, 13, 0.001)
+    s0 = O.fill_normal(n, 14, 1.0)
+    dev = torch.device("cuda:0")
+    w, g, last, s = (torch.from_numpy(a.copy()).to(dev) for a in (w0, g0, l0, s0))
+    stream = torch.cuda.Stream()
+    torch.cuda.synchronize()
+    for _ in range(2):  # two tasks back to back
+        optimise_buffers(stream.cuda_stream, w.data_ptr(), g.data_ptr(), last.data_ptr() if mom > 0 else None,
+                         s.data_ptr(), n, lr, mom, wd)
+        O.sma_optimise(-lr, mom, wd, w0, g0, l0 if mom > 0 else None, s0)
+    stream.synchronize()
+    assert _bits_equal(w.cpu().numpy(), w0), "w"
+    assert _bits_equal(g.cpu().numpy(), g0), "g"
+    assert _bits_equal(s.cpu().numpy(), s0), "s"
+    assert _bits_equal(last.cpu().numpy(), l0), "last"
+
+
+def test_seam_refuses_bad_arguments():
+    import torch
+
+    from crossbow_amd import CbxError
+    from crossbow_amd._lib import CBX_ERR_INVALID
+    from crossbow_amd.seam import SmaPlan, optimise_buffers
+    n = 4099
+    buf = torch.zeros(4 * n + 8, device="cuda:0")
+    p = buf.data_ptr()
+    stream = torch.cuda.Stream()
+    with SmaPlan([0], n) as plan:
+        with pytest.raises(CbxError) as e:  # misaligned replica buffer
+            plan.step([stream.cuda_stream], [p], None, [(0, p + 4, p, 1, 0)], ALPHA, 0.0)
+        assert e.value.code == CBX_ERR_INVALID and "aligned" in str(e.value)
+        with pytest.raises(CbxError):  # momentum without last buffers
+            plan.step([stream.cuda_stream], [p], None, [], ALPHA, 0.9)
+        with pytest.raises(CbxError):  # replica on a device the plan does not have
+            plan.step([stream.cuda_stream], [p], None, [(1, p, p, 1, 0)], ALPHA, 0.0)
+        with pytest.raises(CbxError):  # first out of range
+            plan.step([stream.cuda_stream], [p], None, [], ALPHA, 0.0, first=1)
+    with pytest.raises(CbxError):
+        SmaPlan([0], 0)
+    with pytest.raises(CbxError):
+        optimise_buffers(stream.cuda_stream, p + 4, p, None, p, 16, 0.1, 0.0, 0.0)
+
+
+# ---- G devices in one process: the loopback clique --------------------------
+
+class _Dev:
+    """Raw device buffers and streams through the HIP runtime (torch-free)."""
+
+    def __init__(self):
+        self.hip = ctypes.CDLL("libamdhip64.so.7")
+        self.hip.hipMalloc.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_size_t]
+        self.hip.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+        self.hip.hipFree.argtypes = [ctypes.c_void_p]
+        self.hip.hipStreamCreate.argtypes = [ctypes.POINTER(ctypes.c_void_p)]
+        self.hip.hipStreamSynchronize.argtypes = [ctypes.c_void_p]
+        self.hip.hipStreamDestroy.argtypes = [ctypes.c_void_p]
+        self.ptrs, self.streams = [], []
+
+    def upload(self, arr):
+        a = np.ascontiguousarray(arr, np.float32)
+        p = ctypes.c_void_p()
+        assert self.hip.hipMalloc(ctypes.byref(p), max(16, a.nbytes)) == 0
+        assert self.hip.hipMemcpy(p, a.ctypes.data, a.nbytes, 1) == 0
+        self.ptrs.append(p.value)
+        return p.value
+
+    def download(self, p, n):
+        out = np.empty(n, np.float32)
+        assert self.hip.hipMemcpy(out.ctypes.data, p, out.nbytes, 2) == 0
+        return out
+
+    def stream(self):
+        s = ctypes.c_void_p()
+        assert self.hip.hipStreamCreate(ctypes.byref(s)) == 0
+        self.streams.append(s.value)
+        return s.value
+
+    def sync(self):
+        for s in self.streams:
+            assert self.hip.hipStreamSynchronize(s) == 0
+
+    def free(self):
+        self.sync()
+        for s in self.streams:
+            self.hip.hipStreamDestroy(s)
+        for p in self.ptrs:
+            self.hip.hipFree(p)
+
+
+def _seam_standalone():
+    """crossbow_amd/seam.py without the package (whose __init__ loads torch)."""
+    spec = importlib.util.spec_from_file_location("cbx_seam_standalone",
+                                                  os.path.join(C.ROOT, "crossbow_amd", "seam.py"))
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    return m
+
+
+def _run_devices(L, world, local, n, R, mom, steps, copy_at, held, exact, comms=None, first=0):
+    """The seam over `local` devices (positions of this process's devices in
+    a G = world job; replica i on device i % world).  Returns (bad, digest of
+    z / last per device, differing elements)."""
+    SmaPlan = _seam_standalone().SmaPlan
+    O = C.oracle()
+    st = O.make_state(n, world, R, ALPHA, mom)
+    st.first = first
+    size = world * R
+    mem = _Dev()
+    z = {d: mem.upload(st.z[d]) for d in local}
+    last = {d: mem.upload(st.last[d]) for d in local} if mom > 0 else None
+    w = {i: mem.upload(st.w[i]) for i in range(size) if i % world in local}
+    s = {i: mem.upload(st.s[i]) for i in range(size) if i % world in local}
+    streams = [mem.stream() for _ in local]
+    pos = {d: k for k, d in enumerate(local)}
+    plan = SmaPlan([0] * len(local), n, comms=comms, lib=L)
+    try:
+        for step in range(steps):
+            st.locked[:] = 1
+            for i in held.get(step, ()):
+                st.locked[i] = 0
+            if step in copy_at:
+                st.copy[copy_at[step]] = 1
+            reps = [(pos[i % world], w[i], s[i], int(st.locked[i]), int(st.copy[i])) if i in w else (0, 0, 0, 0, 0)
+                    for i in range(size)]
+            local_copies = sum(int(st.copy[i]) for i in w if st.locked[i] and i >= first)
+            ran = plan.step(streams, [z[d] for d in local], [last[d] for d in local] if last else None, reps,
+                            ALPHA, mom, first)
+            O.sma_step(st)
+            assert ran == (1 if local_copies else 0), (step, ran, local_copies)
+        mem.sync()
+        check = C.Checker(exact=exact)
+        dig = {}
+        for d in local:
+            zd = mem.download(z[d], n)
+            ld = mem.download(last[d], n) if last else np.zeros(0, np.float32)
+            dig[d] = C.digest(zd, ld)
+            check(f"z[{d}]", zd, st.z[d])
+            if last:
+                check(f"last[{d}]", ld, st.last[d])
+        for i in w:
+            check(f"w[{i}]", mem.download(w[i], n), st.w[i])
+        return check.bad, dig, check.differs
+    finally:
+        plan.free()
+        mem.free()
+
+
+DEVICE_CASES = [
+    # (name, n, R, momentum, steps, {step: copy replica}, {step: held replicas}, first, order, caller comms)
+    ("plan-comms", 50_001, 2, 0.9, 3, {1: 3}, {0: (1,)}, 0, "rank", False),
+    ("caller-comms", 50_001, 2, 0.9, 2, {}, {}, 1, "rank", True),
+    ("tail-only", 1031, 3, 0.9, 2, {1: 0}, {}, 0, "rank", False),  # below one kernel trip: no bulk launch
+    ("no-momentum", 20_011, 1, 0.0, 2, {}, {}, 0, "rank", False),
+    ("ring-order", 300_007, 2, 0.9, 3, {2: 1}, {}, 0, "ring", False),
+]
+
+
+def _device_worker(G, q):
+    try:
+        L, A = C.load_variant()
+        F = ctypes.CDLL(os.path.join(C.ROOT, "tests", "native", "libfakerccl.so"))
+        out = []
+        for name, n, R, mom, steps, copy_at, held, first, order, caller in DEVICE_CASES:
+            if order == "ring" and G < 3:
+                continue
+            os.environ["FAKE_RCCL_ORDER"] = order
+            comms = None
+            if caller:  # the caller's communicators, as executioncontext.c:185-201 creates them
+                arr = (ctypes.c_void_p * G)()
+                devs = (ctypes.c_int * G)(*([0] * G))
+                assert F.ncclCommInitAll(arr, G, devs) == 0
+                comms = [arr[k] for k in range(G)]
+            try:
+                bad, dig, differs = _run_devices(L, G, list(range(G)), n, R, mom, steps, copy_at, held,
+                                                 exact=order == "rank", comms=comms, first=first)
+            finally:
+                for c in comms or ():
+                    F.ncclCommDestroy(ctypes.c_void_p(c))
+            out.append((name, order, bad, len(set(dig.values())), differs))
+        q.put((out, None))
+    except Exception:  # pragma: no cover - reported to the parent
+        import traceback
+        q.put((None, traceback.format_exc()))
+
+
+def _spawn(target, args, timeout=110):
+    import multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=target, args=args + (q,))
+    p.start()
+    try:
+        return q.get(timeout=timeout)
+    finally:
+        p.join(timeout=30)
+        if p.is_alive():
+            p.kill()
+
+
+@pytest.mark.skipif(not os.path.exists(C.VARIANT), reason="run scripts/build_fake_rccl.sh first")
+@pytest.mark.parametrize("G", [2, 4])
+def test_seam_devices_one_process(G):
+    res, err = _spawn(_device_worker, (G,))
+    assert err is None, err
+    assert res, "no case ran"
+    for name, order, bad, distinct, differs in res:
+        assert not bad, (name, bad)
+        assert distinct == 1, f"{name}: z / last differ across devices"
+        if order == "ring":
+            assert differs > 0, f"{name}: ring order never left the oracle's order"
+
+
+# ---- G ranks with the real librccl ------------------------------------------
+
+class _Uid(ctypes.Structure):
+    _fields_ = [("internal", ctypes.c_char * 128)]
+
+
+def _rank_worker(world, rank, d, q):
+    try:
+        from tests.test_gpu_realrccl import load_real, rank_env
+        rank_env(rank)
+        L, A = load_real()
+        R = ctypes.CDLL("librccl.so.1")
+        path = os.path.join(d, "uid")
+        if rank == 0:
+            uid = _Uid()
+            assert R.ncclGetUniqueId(ctypes.byref(uid)) == 0
+            with open(path + ".tmp", "wb") as f:
+                f.write(bytes(uid))
+            os.replace(path + ".tmp", path)
+        C.wait_files([path])
+        uid = _Uid.from_buffer_copy(open(path, "rb").read())
+        comm = ctypes.c_void_p()
+        R.ncclCommInitRank.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_int, _Uid, ctypes.c_int]
+        assert R.ncclCommInitRank(ctypes.byref(comm), world, uid, rank) == 0
+        try:
+            bad, dig, differs = _run_devices(L, world, [rank], 200_003, 2, 0.9, 3, {1: (world - 1) * 2 + 1},
+                                             {2: (0,)}, exact=world == 2, comms=[comm.value])
+        finally:
+            R.ncclCommDestroy(comm)
+        q.put(((bad, dig[rank], differs), None))
+    except Exception:  # pragma: no cover - reported to the parent
+        import traceback
+        q.put((None, traceback.format_exc()))
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_seam_real_rccl_ranks(world):
+    import multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    with tempfile.TemporaryDirectory() as d:
+        qs, ps = [], []
+        for rank in range(world):
+            q = ctx.Queue()
+            p = ctx.Process(target=_rank_worker, args=(world, rank, d, q))
+            p.start()
+            qs.append(q)
+            ps.append(p)
+        try:
+            res = [q.get(timeout=110) for q in qs]
+        finally:
+            for p in ps:
+                p.join(timeout=30)
+                if p.is_alive():
+                    p.kill()
+    errs = [e for _, e in res if e]
+    assert not errs, errs[0]
+    outs = [r for r, _ in res]
+    for rank, (bad, _, _) in enumerate(outs):
+        assert not bad, (rank, bad)
+    assert len({dg for _, dg, _ in outs}) == 1, "z / last differ across ranks"
