@@ -70,6 +70,7 @@ def parse():
     p.add_argument("--staged-buckets", type=int, default=8,
                    help="buckets of the pipelined host-staged step (cbx_synchronise_staged)")
     p.add_argument("--no-optimiser", action="store_true", help="skip the replica optimiser-step measurement")
+    p.add_argument("--no-seam", action="store_true", help="skip the sma.c seam measurement (caller-owned buffers)")
     p.add_argument("--rehearse-one-gpu", action="store_true",
                    help="N > 1 rehearsal on a one-GPU box: every rank on device 0, each its own RCCL 'host' "
                         "(NCCL_HOSTID), so real RCCL links the ranks by sockets over loopback; the numbers say "
@@ -208,6 +209,46 @@ def bench_optimiser(gpu, torch, n, args, rounds=10):
             "alg_bytes_per_launch": b, "achieved_GBs": round(b / (ms * 1e-3) / 1e9, 1),
             "frac": round(b / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
             "timed": "torch events around back-to-back launches on one stream (includes launch gaps)"}
+
+
+def bench_seam(torch, n, args, steps=20):
+    """The sma.c seam (cbx_sma_plan_step): the same step
+    over buffers the caller owns -- here one torch allocation per buffer,
+    exactly n floats each, as the reference's model manager allocates them --
+    so the fused kernel runs the whole-trip bulk and a tail kernel the last
+    elements.  Timed with torch events around back-to-back steps on the
+    caller's stream (launch gaps included)."""
+    from crossbow_amd.seam import SmaPlan
+    dev = torch.device("cuda:0")
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(SEED)
+    z = torch.randn(n, device=dev, generator=gen) * 0.05
+    last = torch.randn(n, device=dev, generator=gen) * 0.001
+    s = [z + 0.01 * torch.randn(n, device=dev, generator=gen) for _ in range(args.replicas)]
+    w = [si + 0.001 * torch.randn(n, device=dev, generator=gen) for si in s]
+    mom = args.momentum
+    stream = torch.cuda.Stream()
+    torch.cuda.synchronize()
+    with SmaPlan([0], n) as plan:
+        reps = [(0, w[i].data_ptr(), s[i].data_ptr(), 1, 0) for i in range(args.replicas)]
+        lp = [last.data_ptr()] if mom > 0 else None
+
+        def one():
+            plan.step([stream.cuda_stream], [z.data_ptr()], lp, reps, args.alpha, mom)
+        for _ in range(3):
+            one()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for _ in range(steps):
+            one()
+        e1.record(stream)
+        e1.synchronize()
+    ms = e0.elapsed_time(e1) / steps
+    b, _ = alg_bytes(n, args.replicas, mom, 1)
+    return {"entry": "cbx_sma_plan_step", "step_ms_mean": round(ms, 4), "steps": steps, "alg_bytes_per_step": b,
+            "achieved_GBs": round(b / (ms * 1e-3) / 1e9, 1), "frac": round(b / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+            "buffers": "caller-owned torch allocations of exactly n floats (no padding, no slot stagger)",
+            "timed": "torch events around back-to-back steps on the caller's stream (bulk + tail launch, gaps included)"}
 
 
 def main():
@@ -395,6 +436,8 @@ def main():
 
     if rank == 0 and world == 1 and not args.no_optimiser:
         result["replica_optimiser"] = bench_optimiser(gpu, torch, n, args)
+    if rank == 0 and world == 1 and not args.no_seam:
+        result["seam"] = bench_seam(torch, n, args)
 
     if rank == 0 and world == 1:
         if not args.no_copy_ceiling:

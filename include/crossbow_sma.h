@@ -463,7 +463,12 @@ int cbx_sma_plan_free (cbx_sma_plan *plan);
  * every such replica now equals its device's base model; the caller resets
  * their _copy, sma.c:217-220), 0 when not.  The caller's events
  * (base->updated, synched[dev], replica->updated) are recorded on the same
- * streams after the call, as sma.c:115,177,204,222 do.                   */
+ * streams after the call, as sma.c:115,177,204,222 do.  One step at a time
+ * per plan (the reference's single ResultCollector thread): the scratch is
+ * the plan's.  With a communicator that spans processes, each process
+ * passes only its own replicas as locked; a Phase-D request on any rank
+ * reaches every rank through the all-reduced control block, so the return
+ * value reports this process's requests only.                           */
 int cbx_sma_plan_step (cbx_sma_plan *plan, void *const *streams, float *const *z, float *const *last,
                        int nreplicas, const int *replica_device, float *const *w, const float *const *s,
                        const int *locked, const int *copy, float alpha, float momentum, int first);

@@ -24,5 +24,5 @@ STEPS=${STEPS:-smoke,tests,bench,rocprof}
 [[ $STEPS == *sweep* ]] && { run sweep 600 python scripts/sweep.py ${SWEEP_ARGS:-} || true; }
 [[ $STEPS == *pcie* ]] && { run pcie_bench 300 ./scripts/pcie_bench || true; }
 [[ $STEPS == *c2* ]] && { run c2_latency 300 rocprofv3 --kernel-trace --stats -d gpurun_out/c2prof -o run --output-format csv -- python3 scripts/c2_latency.py || true; }
-[[ $STEPS == *rocprof* ]] && { run rocprof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/rocprof -o run --output-format csv -- python3 bench.py --no-cpu-baseline --no-staged --no-copy-ceiling ${BENCH_ARGS:-} || true; }
+[[ $STEPS == *rocprof* ]] && { run rocprof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/rocprof -o run --output-format csv -- python3 bench.py --no-cpu-baseline --no-staged --no-copy-ceiling --no-seam ${BENCH_ARGS:-} || true; }
 exit 0

@@ -12,7 +12,7 @@ pass() {  # pass <tag> <bench args...>
   local tag=$1; shift
   for c in FETCH_SIZE WRITE_SIZE; do
     timeout -k 10 300 rocprofv3 --pmc $c -d gpurun_out/pmc_${tag}_$c -o run --output-format csv -- \
-      python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-staged --no-copy-ceiling "$@" \
+      python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-staged --no-copy-ceiling --no-seam "$@" \
       > gpurun_out/pmc_${tag}_$c.log 2>&1 || { echo "pmc $tag $c failed rc=$?"; tail -20 gpurun_out/pmc_${tag}_$c.log; exit 1; }
   done
 }

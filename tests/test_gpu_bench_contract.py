@@ -15,7 +15,7 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-QUICK = ["--steps", "3", "--warmup", "1", "--no-cpu-baseline", "--no-staged", "--no-copy-ceiling", "--no-optimiser"]
+QUICK = ["--steps", "3", "--warmup", "1", "--no-cpu-baseline", "--no-staged", "--no-copy-ceiling", "--no-optimiser", "--no-seam"]
 
 
 def _one_line(stdout: str) -> dict:
