@@ -434,6 +434,27 @@ def main():
                                "unpipelined_step_ms_median": round(statistics.median(calib["step"]), 4),
                                "timed_in": "calibration steps (one bucket, in order)"}
 
+    if world > 1 and not args.no_staged:
+        # Host-staged rate at N > 1 (north_star: the path starts and ends in
+        # host memory): each rank's replicas live in its own pinned mirror and
+        # cross its own GPU's PCIe link; zero-copy staging kernels, kernel A /
+        # all-reduce / kernel B per bucket.  Max over ranks of the median of 3.
+        gpu.set_staging_mode(_lib.STAGING_ZEROCOPY)
+        runs = []
+        for _ in range(3):
+            clock += 1
+            gpu.lockAny()
+            gpu.synchronise_staged(0, clock, 0, args.staged_buckets)
+            gpu.unlockAny()
+            gpu.wait()
+            runs.append(gpu.last_timing(0)[_lib.T_STEP])
+        ms = D.max_over_ranks(sorted(runs)[1], world)
+        result["host_staged"] = {"zerocopy": {
+            "buckets": args.staged_buckets, "step_ms": round(ms, 3),
+            "end_to_end_GBs": round(step_bytes * G / (ms * 1e-3) / 1e9, 2),
+            "per_gpu_GBs": round(step_bytes / (ms * 1e-3) / 1e9, 2),
+            "timed": "HIP events per rank (staged step: host in, host and device out), max over ranks"}}
+
     if rank == 0 and world == 1 and not args.no_optimiser:
         result["replica_optimiser"] = bench_optimiser(gpu, torch, n, args)
     if rank == 0 and world == 1 and not args.no_seam:

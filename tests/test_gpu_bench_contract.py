@@ -54,3 +54,18 @@ def test_bench_two_ranks_through_the_launcher_prints_one_json_line():
     d = _one_line(p.stdout)
     _check(d, 2)
     assert d["config"]["parallelism"] == "sma-dp2" and "allreduce" in d and "rehearsal" in d
+
+
+@pytest.mark.timeout(300)
+def test_bench_two_ranks_host_staged_field():
+    # the N > 1 host-staged leg (zero-copy staging over two rehearsal ranks)
+    quick = [a for a in QUICK if a != "--no-staged"]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", "29673", "bench.py", "--gpus", "2",
+           "--rehearse-one-gpu", "--bucket-mb", "16"] + quick
+    p = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=280)
+    assert p.returncode == 0, p.stderr[-2000:]
+    d = _one_line(p.stdout)
+    _check(d, 2)
+    z = d["host_staged"]["zerocopy"]
+    assert z["step_ms"] > 0 and z["end_to_end_GBs"] > 0 and z["per_gpu_GBs"] > 0
