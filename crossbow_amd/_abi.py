@@ -143,6 +143,7 @@ SIGNATURES = {
     "cbx_bench_copy": (_I, [_P, _S, _I, _FP]),
     "cbx_sma_plan_create": (_I, [_PP, _IP, _I, _c.c_longlong, _PP]),
     "cbx_sma_plan_free": (_I, [_P]),
+    "cbx_sma_plan_set_buckets": (_I, [_P, _I]),
     "cbx_sma_plan_step": (_I, [_P, _PP, _PP, _PP, _I, _IP, _PP, _PP, _IP, _IP, _F, _F, _I]),
     "cbx_sma_optimise_buffers": (_I, [_P, _P, _P, _P, _P, _c.c_longlong, _F, _F, _F]),
 }

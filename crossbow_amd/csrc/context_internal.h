@@ -647,6 +647,8 @@ inline int ring_span(Device &d, int slot, int a, int b, float *out) {
 }
 
 // ---- the barrier steps (sync_steps.hip) ------------------------------------
+// The same arguments over float4s [start4, start4 + len4) of every buffer.
+cbx::SmaArgs offset_args(const cbx::SmaArgs &a, int64_t start4, int64_t len4);
 // SMA (synch/sma.c:13-231): fused at G = 1; kernel A / collective / kernel B
 // per bucket at G > 1 (or forced); the peer-read form.
 int sma_step(cbx_context *c, int first);

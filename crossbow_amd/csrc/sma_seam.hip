@@ -144,14 +144,38 @@ struct cbx_sma_plan {
     char *scratch = nullptr;  // [ctrl | acc (padded)] [ctrl | D (padded)]
     float *acc_ctrl = nullptr;
     float *D_ctrl = nullptr;
+    // Bucketed pipeline (G > 1): the all-reduces run on this stream beside
+    // kernel A of the next bucket; per bucket, kernel A done / all-reduce done.
+    hipStream_t comm_stream = nullptr;
+    std::vector<hipEvent_t> ev_a, ev_r;
   };
   std::vector<Dev> devs;
   int64_t n = 0;
   int64_t n4b = 0;  // bulk float4s
   int ranks = 1;    // ranks of the communicator (1: no collective)
+  int buckets = 0;  // G > 1: 0 = kDefaultBuckets, 1 = in order on the caller's stream
   cbx::LaunchConfig cfg;
   cbx::LaunchConfig apply_cfg = cbx::sma_apply_launch_config();
 };
+
+namespace {
+
+int ensure_pipeline(cbx_sma_plan *p, int64_t nb) {
+  for (auto &d : p->devs) {
+    HIP_TRY(hipSetDevice(d.hip_id));
+    if (!d.comm_stream) HIP_TRY(hipStreamCreateWithFlags(&d.comm_stream, hipStreamNonBlocking));
+    while ((int64_t)d.ev_a.size() < nb) {
+      hipEvent_t a, r;
+      HIP_TRY(hipEventCreateWithFlags(&a, hipEventDisableTiming));
+      HIP_TRY(hipEventCreateWithFlags(&r, hipEventDisableTiming));
+      d.ev_a.push_back(a);
+      d.ev_r.push_back(r);
+    }
+  }
+  return CBX_OK;
+}
+
+}  // namespace
 
 extern "C" {
 
@@ -162,6 +186,9 @@ int cbx_sma_plan_free(cbx_sma_plan *p) {
     (void)hipDeviceSynchronize();
     if (d.own_comm && d.comm) (void)ncclCommDestroy(d.comm);
     if (d.scratch) (void)hipFree(d.scratch);
+    for (hipEvent_t e : d.ev_a) (void)hipEventDestroy(e);
+    for (hipEvent_t e : d.ev_r) (void)hipEventDestroy(e);
+    if (d.comm_stream) (void)hipStreamDestroy(d.comm_stream);
   }
   delete p;
   return CBX_OK;
@@ -315,42 +342,98 @@ int cbx_sma_plan_step(cbx_sma_plan *p, void *const *streams, float *const *z, fl
     HIP_TRY(launch_tail(tails[0], st));
     return copies_total > 0 ? 1 : 0;
   }
-  // G > 1: kernel A, one grouped all-reduce of the control block + acc
-  // (common.c:14-54), kernel B -- in order on each device's stream.
-  for (int k = 0; k < G; ++k) {
-    auto &d = p->devs[k];
-    hipStream_t st = static_cast<hipStream_t>(streams[k]);
-    HIP_TRY(hipSetDevice(d.hip_id));
-    cbx::LaunchConfig cfg = p->cfg;
-    cfg.num_cus = d.num_cus;
-    if (p->n4b > 0) HIP_TRY(cbx::launch_sma_accumulate(args[k], true, cfg, st));
-    TailArgs t = tails[k];
-    t.phase = 1;
-    if (p->n4b == 0) {  // no bulk launch wrote the control block
-      t.ctrl_out = d.acc_ctrl;
+  // G > 1: kernel A, the grouped all-reduce of the control block + acc
+  // (common.c:14-54), kernel B.  One bucket: everything in order on each
+  // device's stream, the reference's structure.  nb > 1 buckets (the
+  // default): the all-reduce of bucket k runs on a stream of the plan's,
+  // beside kernel A of bucket k+1, as in the context's pipeline:
+  //   stream      : A(0) A(1) [wait r(0)] B(0) A(2) [wait r(1)] B(1) ...
+  //   comm_stream : [wait a(0)] AR(0) [wait a(1)] AR(1) ...
+  // The control block rides bucket 0; the tail rides the last bucket (its
+  // kernel A / B tail launches follow the bulk ones, its all-reduce extends
+  // to n).  The next step's AR(k) waits for its A(k), which follows this
+  // step's last B on the caller's stream, so no buffer is overwritten early.
+  const int64_t pad = cbx::kPadFloat4;
+  int64_t nb = p->buckets > 0 ? p->buckets : kDefaultBuckets;
+  int64_t b4 = p->n4b;
+  if (nb > 1 && p->n4b > 0) b4 = ((p->n4b + nb - 1) / nb + pad - 1) / pad * pad;
+  nb = b4 > 0 ? (p->n4b + b4 - 1) / b4 : 1;
+  const bool piped = nb > 1;
+  if (piped) TRY(ensure_pipeline(p, nb));
+  auto start_of = [&](int64_t b) { return b * b4; };
+  auto len_of = [&](int64_t b) { return std::min(b4, p->n4b - b * b4); };
+  auto apply = [&](int64_t b) -> int {
+    for (int k = 0; k < G; ++k) {
+      auto &d = p->devs[k];
+      hipStream_t st = static_cast<hipStream_t>(streams[k]);
+      HIP_TRY(hipSetDevice(d.hip_id));
+      if (piped) HIP_TRY(hipStreamWaitEvent(st, d.ev_r[b], 0));
+      cbx::LaunchConfig cfg = p->apply_cfg;
+      cfg.num_cus = d.num_cus;
+      if (len_of(b) > 0) HIP_TRY(cbx::launch_sma_apply(offset_args(args[k], start_of(b), len_of(b)), mom, cfg, st));
+      if (b == nb - 1) {
+        TailArgs t = tails[k];
+        t.phase = 2;
+        HIP_TRY(launch_tail(t, st));
+      }
     }
-    HIP_TRY(launch_tail(t, st));
+    return CBX_OK;
+  };
+  for (int64_t b = 0; b < nb; ++b) {
+    for (int k = 0; k < G; ++k) {
+      auto &d = p->devs[k];
+      hipStream_t st = static_cast<hipStream_t>(streams[k]);
+      HIP_TRY(hipSetDevice(d.hip_id));
+      cbx::LaunchConfig cfg = p->cfg;
+      cfg.num_cus = d.num_cus;
+      if (len_of(b) > 0)
+        HIP_TRY(cbx::launch_sma_accumulate(offset_args(args[k], start_of(b), len_of(b)), b == 0, cfg, st));
+      if (b == nb - 1) {
+        TailArgs t = tails[k];
+        t.phase = 1;
+        if (p->n4b == 0) t.ctrl_out = d.acc_ctrl;  // no bulk launch wrote the control block
+        HIP_TRY(launch_tail(t, st));
+      }
+      if (piped) {
+        HIP_TRY(hipEventRecord(d.ev_a[b], st));
+        HIP_TRY(hipStreamWaitEvent(d.comm_stream, d.ev_a[b], 0));
+      }
+    }
+    NCCL_TRY(ncclGroupStart());
+    for (int k = 0; k < G; ++k) {
+      auto &d = p->devs[k];
+      HIP_TRY(hipSetDevice(d.hip_id));
+      const int64_t lo_f = start_of(b) * 4;
+      const int64_t hi_f = b == nb - 1 ? p->n : (start_of(b) + len_of(b)) * 4;
+      float *src = d.acc_ctrl + cbx::kCtrlFloats + lo_f, *dst = d.D_ctrl + cbx::kCtrlFloats + lo_f;
+      size_t count = (size_t)(hi_f - lo_f);
+      if (b == 0) {
+        src -= cbx::kCtrlFloats;
+        dst -= cbx::kCtrlFloats;
+        count += cbx::kCtrlFloats;
+      }
+      NCCL_TRY(ncclAllReduce(src, dst, count, ncclFloat, ncclSum, d.comm,
+                             piped ? d.comm_stream : static_cast<hipStream_t>(streams[k])));
+    }
+    NCCL_TRY(ncclGroupEnd());
+    if (piped) {
+      for (int k = 0; k < G; ++k) {
+        auto &d = p->devs[k];
+        HIP_TRY(hipSetDevice(d.hip_id));
+        HIP_TRY(hipEventRecord(d.ev_r[b], d.comm_stream));
+      }
+      if (b >= 1) TRY(apply(b - 1));
+    }
   }
-  NCCL_TRY(ncclGroupStart());
-  for (int k = 0; k < G; ++k) {
-    auto &d = p->devs[k];
-    HIP_TRY(hipSetDevice(d.hip_id));
-    NCCL_TRY(ncclAllReduce(d.acc_ctrl, d.D_ctrl, (size_t)(cbx::kCtrlFloats + p->n), ncclFloat, ncclSum, d.comm,
-                           static_cast<hipStream_t>(streams[k])));
-  }
-  NCCL_TRY(ncclGroupEnd());
-  for (int k = 0; k < G; ++k) {
-    auto &d = p->devs[k];
-    hipStream_t st = static_cast<hipStream_t>(streams[k]);
-    HIP_TRY(hipSetDevice(d.hip_id));
-    cbx::LaunchConfig cfg = p->apply_cfg;
-    cfg.num_cus = d.num_cus;
-    if (p->n4b > 0) HIP_TRY(cbx::launch_sma_apply(args[k], mom, cfg, st));
-    TailArgs t = tails[k];
-    t.phase = 2;
-    HIP_TRY(launch_tail(t, st));
-  }
+  TRY(apply(nb - 1));
   return copies_total > 0 ? 1 : 0;
+}
+
+int cbx_sma_plan_set_buckets(cbx_sma_plan *p, int buckets) {
+  if (!p) return fail(CBX_ERR_INVALID, "null plan");
+  if (buckets < 0 || buckets > 4096) return fail(CBX_ERR_INVALID, "plan buckets must be 0..4096, got %d", buckets);
+  p->buckets = buckets;
+  return CBX_OK;
 }
 
 int cbx_sma_optimise_buffers(void *stream, float *w, float *g, float *last, float *s, long long elements,

@@ -50,7 +50,8 @@ class SmaPlan:
     ``elements`` floats; ``comms`` = the caller's ncclComm_t handles (ints), or
     None to let the plan create them (ncclCommInitAll, more than one device)."""
 
-    def __init__(self, devices: Sequence[int], elements: int, comms: Optional[Sequence[int]] = None, lib=None):
+    def __init__(self, devices: Sequence[int], elements: int, comms: Optional[Sequence[int]] = None, lib=None,
+                 buckets: int = 0):
         self.lib = lib if lib is not None else _default_lib()
         self.G = len(devices)
         p = ctypes.c_void_p()
@@ -58,6 +59,8 @@ class SmaPlan:
                                                       _ptrs(comms) if comms is not None else None),
                "cbx_sma_plan_create")
         self._p = p
+        if buckets:
+            self.set_buckets(buckets)
 
     def step(self, streams: Sequence[int], z: Sequence[int], last: Optional[Sequence[Optional[int]]],
              replicas: Sequence[Tuple[int, int, int, int, int]], alpha: float, momentum: float,
@@ -70,6 +73,10 @@ class SmaPlan:
             _ints(dev), _ptrs([r[1] for r in replicas]), _ptrs([r[2] for r in replicas]),
             _ints([r[3] for r in replicas]), _ints([r[4] for r in replicas]), ctypes.c_float(alpha),
             ctypes.c_float(momentum), first), "cbx_sma_plan_step")
+
+    def set_buckets(self, buckets: int) -> None:
+        """G > 1: buckets of the all-reduce pipeline (0 = default 8, 1 = in order)."""
+        _raise(self.lib, self.lib.cbx_sma_plan_set_buckets(self._p, buckets), "cbx_sma_plan_set_buckets")
 
     def free(self) -> None:
         if self._p:

@@ -445,6 +445,12 @@ typedef struct cbx_sma_plan cbx_sma_plan;
 int cbx_sma_plan_create (cbx_sma_plan **plan, const int *devices, int ndevices, long long elements,
                          void *const *comms);
 int cbx_sma_plan_free (cbx_sma_plan *plan);
+/* G > 1: cut the step into `buckets` buckets and run the all-reduce of
+ * bucket k on a stream of the plan's beside kernel A of bucket k+1 (as the
+ * context's pipeline does; the caller's stream still orders the step
+ * against its other work).  0 (default) = 8 buckets; 1 = the reference's
+ * order, everything on the caller's stream.  Same results bit for bit.    */
+int cbx_sma_plan_set_buckets (cbx_sma_plan *plan, int buckets);
 /* One SMA step (sma.c:13-231), enqueued on the caller's streams, async:
  *   streams[k]        dev->modelSynchronisationStream of devices[k] (hipStream_t)
  *   z[k], last[k]     baseModels[k]->data->dev / ->last->dev (last may be NULL

@@ -226,7 +226,7 @@ def _seam_standalone():
     return m
 
 
-def _run_devices(L, world, local, n, R, mom, steps, copy_at, held, exact, comms=None, first=0):
+def _run_devices(L, world, local, n, R, mom, steps, copy_at, held, exact, comms=None, first=0, buckets=0):
     """The seam over `local` devices (positions of this process's devices in
     a G = world job; replica i on device i % world).  Returns (bad, digest of
     z / last per device, differing elements)."""
@@ -242,7 +242,7 @@ def _run_devices(L, world, local, n, R, mom, steps, copy_at, held, exact, comms=
     s = {i: mem.upload(st.s[i]) for i in range(size) if i % world in local}
     streams = [mem.stream() for _ in local]
     pos = {d: k for k, d in enumerate(local)}
-    plan = SmaPlan([0] * len(local), n, comms=comms, lib=L)
+    plan = SmaPlan([0] * len(local), n, comms=comms, lib=L, buckets=buckets)
     try:
         for step in range(steps):
             st.locked[:] = 1
@@ -276,12 +276,15 @@ def _run_devices(L, world, local, n, R, mom, steps, copy_at, held, exact, comms=
 
 
 DEVICE_CASES = [
-    # (name, n, R, momentum, steps, {step: copy replica}, {step: held replicas}, first, order, caller comms)
-    ("plan-comms", 50_001, 2, 0.9, 3, {1: 3}, {0: (1,)}, 0, "rank", False),
-    ("caller-comms", 50_001, 2, 0.9, 2, {}, {}, 1, "rank", True),
-    ("tail-only", 1031, 3, 0.9, 2, {1: 0}, {}, 0, "rank", False),  # below one kernel trip: no bulk launch
-    ("no-momentum", 20_011, 1, 0.0, 2, {}, {}, 0, "rank", False),
-    ("ring-order", 300_007, 2, 0.9, 3, {2: 1}, {}, 0, "ring", False),
+    # (name, n, R, momentum, steps, {step: copy replica}, {step: held replicas}, first, order, caller comms,
+    #  buckets: 0 = the default pipeline of 8, 1 = in order on the caller's stream)
+    ("plan-comms", 50_001, 2, 0.9, 3, {1: 3}, {0: (1,)}, 0, "rank", False, 0),
+    ("plan-comms-in-order", 50_001, 2, 0.9, 3, {1: 3}, {0: (1,)}, 0, "rank", False, 1),
+    ("caller-comms", 50_001, 2, 0.9, 2, {}, {}, 1, "rank", True, 0),
+    ("tail-only", 1031, 3, 0.9, 2, {1: 0}, {}, 0, "rank", False, 0),  # below one kernel trip: no bulk launch
+    ("no-momentum", 20_011, 1, 0.0, 2, {}, {}, 0, "rank", False, 3),
+    ("many-buckets", 300_007, 2, 0.9, 4, {2: 1}, {1: (0,)}, 0, "rank", False, 37),  # more buckets than trips allow
+    ("ring-order", 300_007, 2, 0.9, 3, {2: 1}, {}, 0, "ring", False, 0),
 ]
 
 
@@ -290,7 +293,7 @@ def _device_worker(G, q):
         L, A = C.load_variant()
         F = ctypes.CDLL(os.path.join(C.ROOT, "tests", "native", "libfakerccl.so"))
         out = []
-        for name, n, R, mom, steps, copy_at, held, first, order, caller in DEVICE_CASES:
+        for name, n, R, mom, steps, copy_at, held, first, order, caller, buckets in DEVICE_CASES:
             if order == "ring" and G < 3:
                 continue
             os.environ["FAKE_RCCL_ORDER"] = order
@@ -302,7 +305,8 @@ def _device_worker(G, q):
                 comms = [arr[k] for k in range(G)]
             try:
                 bad, dig, differs = _run_devices(L, G, list(range(G)), n, R, mom, steps, copy_at, held,
-                                                 exact=order == "rank", comms=comms, first=first)
+                                                 exact=order == "rank", comms=comms, first=first,
+                                                 buckets=buckets)
             finally:
                 for c in comms or ():
                     F.ncclCommDestroy(ctypes.c_void_p(c))
@@ -346,7 +350,7 @@ class _Uid(ctypes.Structure):
     _fields_ = [("internal", ctypes.c_char * 128)]
 
 
-def _rank_worker(world, rank, d, q):
+def _rank_worker(world, rank, d, buckets, q):
     try:
         from tests.test_gpu_realrccl import load_real, rank_env
         rank_env(rank)
@@ -366,7 +370,7 @@ def _rank_worker(world, rank, d, q):
         assert R.ncclCommInitRank(ctypes.byref(comm), world, uid, rank) == 0
         try:
             bad, dig, differs = _run_devices(L, world, [rank], 200_003, 2, 0.9, 3, {1: (world - 1) * 2 + 1},
-                                             {2: (0,)}, exact=world == 2, comms=[comm.value])
+                                             {2: (0,)}, exact=world == 2, comms=[comm.value], buckets=buckets)
         finally:
             R.ncclCommDestroy(comm)
         q.put(((bad, dig[rank], differs), None))
@@ -375,15 +379,15 @@ def _rank_worker(world, rank, d, q):
         q.put((None, traceback.format_exc()))
 
 
-@pytest.mark.parametrize("world", [2, 4])
-def test_seam_real_rccl_ranks(world):
+@pytest.mark.parametrize("world,buckets", [(2, 0), (2, 1), (4, 0), (4, 5)])
+def test_seam_real_rccl_ranks(world, buckets):
     import multiprocessing as mp
     ctx = mp.get_context("spawn")
     with tempfile.TemporaryDirectory() as d:
         qs, ps = [], []
         for rank in range(world):
             q = ctx.Queue()
-            p = ctx.Process(target=_rank_worker, args=(world, rank, d, q))
+            p = ctx.Process(target=_rank_worker, args=(world, rank, d, buckets, q))
             p.start()
             qs.append(q)
             ps.append(p)
