@@ -37,6 +37,7 @@ class TheGPU:
     def __init__(self):
         self._L = _lib.load()
         self._ctx = ctypes.c_void_p()
+        self._capacity = {}  # (op id, order) -> bytes setModelVariableBuffer copies
 
     # ---- lifecycle ------------------------------------------------------
     @staticmethod
@@ -88,10 +89,19 @@ class TheGPU:
     def setModelVariable(self, id: int, order: int, shape: Sequence[int], capacity: int) -> int:
         _java_int("setModelVariable capacity", capacity)
         arr = (ctypes.c_int * max(1, len(shape)))(*shape)
-        return check(self._L.cbx_set_model_variable(self._ctx, id, order, len(shape), arr, capacity))
+        rc = check(self._L.cbx_set_model_variable(self._ctx, id, order, len(shape), arr, capacity))
+        self._capacity[(id, order)] = capacity
+        return rc
 
     def setModelVariableBuffer(self, id: int, order: int, buffer) -> int:
-        a = np.ascontiguousarray(np.frombuffer(memoryview(buffer), dtype=np.uint8))
+        # The library copies the variable's whole capacity from the buffer
+        # (executioncontext.c:1583-1590, a direct ByteBuffer of that size on the
+        # Java side): a shorter Python buffer would be over-read, so refuse it.
+        a = np.ascontiguousarray(np.frombuffer(memoryview(buffer).cast("B"), dtype=np.uint8))
+        need = self._capacity.get((id, order))
+        if need is not None and a.nbytes < need:
+            raise CbxError(_lib.CBX_ERR_INVALID, f"variable ({id}, {order}) buffer of {a.nbytes} bytes is shorter "
+                                                 f"than its capacity of {need} bytes")
         return check(self._L.cbx_set_model_variable_buffer(self._ctx, id, order, _ptr(a)))
 
     def setModelVariableLearningRateMultiplier(self, id: int, order: int, multiplier: float) -> int:

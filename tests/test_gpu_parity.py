@@ -960,3 +960,21 @@ def test_fused_timing_excludes_work_enqueued_between_steps():
         assert statistics.median(mixed) < 1.3 * statistics.median(plain), (plain, mixed)
     finally:
         g.free()
+
+
+def test_short_variable_buffer_is_refused():
+    # setModelVariableBuffer copies the variable's whole capacity: a shorter
+    # host buffer is refused before the library would over-read it.
+    import numpy as np
+
+    from crossbow_amd import CbxError, TheGPU
+    g = TheGPU()
+    g.init([0])
+    try:
+        g.setModel(1, 4 * 100)
+        g.setModelVariable(0, 1, [100], 4 * 100)
+        with pytest.raises(CbxError, match="shorter than its capacity"):
+            g.setModelVariableBuffer(0, 1, np.zeros(99, np.float32))
+        g.setModelVariableBuffer(0, 1, np.zeros(100, np.float32))
+    finally:
+        g.free()
