@@ -71,7 +71,7 @@ def max_over_ranks(value: float, world: int) -> float:
 
 def tune_buckets(gpu, n: int, world: int, step: Callable[[], None], candidates=(1, 2, 4, 8),
                  steps: int = 10, warmup: int = 2, modes=(0, 1), strides=(1, 2, 4), passes: int = 2,
-                 group_candidates=(2, 4)):
+                 group_candidates=(2, 4), progress: Optional[Callable[[str], None]] = None):
     """Pick the configuration of the G > 1 pipeline (kernel A / collective /
     kernel B per bucket) by timing each candidate on the live communicator,
     the way a runtime tunes itself in its warm-up.
@@ -100,6 +100,8 @@ def tune_buckets(gpu, n: int, world: int, step: Callable[[], None], candidates=(
     form are reset first, so an earlier setting never skews the sweep.
     Candidates are timed in ``passes`` interleaved passes and each keeps its
     best pass, so one noisy sample (a few percent on one GPU) does not decide.
+
+    ``progress`` (if given) receives one line per timed candidate.
 
     Returns (bucket_elements, mode, stride, group, algorithm, {key: ms_per_step})
     with keys "<buckets>/<mode>" for stride 1, "<buckets>/<mode>/s<stride>",
@@ -143,6 +145,8 @@ def tune_buckets(gpu, n: int, world: int, step: Callable[[], None], candidates=(
                     ms = timed_steps()
                     key = (nb, mode, stride, algo)
                     results[key] = min(ms, results.get(key, ms))
+                    if progress:
+                        progress(f"tune {tuning_key(*key)}: {ms:.4f} ms/step")
     best = min(results, key=lambda k: (results[k], k))
     nb, mode, stride, algorithm = best
     gpu.set_allreduce_algorithm(algorithm)
@@ -162,6 +166,8 @@ def tune_buckets(gpu, n: int, world: int, step: Callable[[], None], candidates=(
                 gpu.set_allreduce_group(grp)
                 ms = timed_steps()
                 timed[grp] = min(ms, timed.get(grp, ms))
+                if progress:
+                    progress(f"tune {tuning_key(*best)}/g{grp}: {ms:.4f} ms/step")
         for grp in groups:
             out[tuning_key(*best) + f"/g{grp}"] = timed[grp]
         group = min(timed, key=lambda g: (timed[g], g))
