@@ -43,6 +43,11 @@ struct SmaArgs {
   // all-reduce may already be overwriting).
   int decision_mode;
   float *decision;
+  // Caller-owned buffers (the sma.c seam): elements [tail_lo, tail_hi) past
+  // the last whole trip, done by the launch's first tail_blocks workgroups
+  // (set by the launcher).  Zero for the context's padded buffers.
+  int64_t tail_lo, tail_hi;
+  int tail_blocks;
 };
 
 // Buffers are padded to this many float4s so every trip of every kernel is
@@ -265,6 +270,8 @@ struct OptArgs {
   float momentum;  // replica conf->momentum
   float wd;        // replica conf->weightDecay
   int pad_;
+  int64_t tail_lo, tail_hi;  // caller-owned buffers: elements past the last whole trip (see SmaArgs)
+  int tail_blocks;
 };
 hipError_t launch_sma_optimise(const OptArgs &a, const LaunchConfig &cfg, hipStream_t stream, Timing t = {});
 // DEFAULT update model (0, kernels/optimisers/default.cu:3-131): the task

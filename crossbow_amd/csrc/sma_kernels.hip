@@ -60,12 +60,59 @@ __device__ __forceinline__ void sto(v4f *base, uint32_t off, v4f v) {
 // contiguous KiB, and a wave's U instructions per stream cover U KiB in a
 // row (U = 2 at 64-thread blocks measured best: scripts/sweep.py --interleave).
 template <int U>
+__device__ __forceinline__ uint32_t first_elem(uint32_t block) {
+  return (block * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 64u * U + (threadIdx.x & 63u);
+}
+
+template <int U>
 __device__ __forceinline__ uint32_t first_elem() {
-  return (blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 64u * U + (threadIdx.x & 63u);
+  return first_elem<U>(blockIdx.x);
 }
 
 __device__ __forceinline__ v4f vfma(v4f a, v4f b, v4f c) {
   return __builtin_elementwise_fma(a, b, c);
+}
+
+// Buffers the caller owns (the sma.c seam, sma_seam.hip) hold exactly n
+// floats, not whole kernel trips.  Their last elements [a.tail_lo, a.tail_hi)
+// go to the first a.tail_blocks workgroups of the same launch (TAIL
+// instantiations), one float per lane, with the float4 path's fma sequence;
+// the bulk runs on the remaining workgroups.  One launch per phase instead of
+// a second tail launch (a separate tail kernel cost ~20 us per step on
+// separately allocated buffers: scripts/seam_layout_ab.py).
+// PHASE 0: the fused step; 1: Phase A into acc; 2: Phases C (+ D if `copy`).
+template <int PHASE, bool MOM>
+__device__ __forceinline__ void sma_tail_elem(const SmaArgs &a, bool copy) {
+  const int64_t i = a.tail_lo + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= a.tail_hi) return;
+  float *z = reinterpret_cast<float *>(a.z);
+  float *last = reinterpret_cast<float *>(a.last);
+  float D;
+  float z0 = z[i];
+  if constexpr (PHASE == 2) {
+    D = reinterpret_cast<const float *>(a.D)[i];
+  } else {
+    float acc = 0.0f;  // sma.c:66
+    for (int r = 0; r < a.nrep; ++r) {
+      float *w = reinterpret_cast<float *>(a.w[r]);
+      const float d = fmaf(-1.0f, z0, reinterpret_cast<const float *>(a.s[r])[i]);  // sma.c:79-90
+      w[i] = fmaf(-a.alpha, d, w[i]);                                                // :93-99
+      acc = fmaf(a.alpha, d, acc);                                                   // :102-107
+    }
+    if constexpr (PHASE == 1) {
+      reinterpret_cast<float *>(a.acc)[i] = acc;
+      return;
+    }
+    D = acc;
+  }
+  if constexpr (MOM) {
+    D = fmaf(kBaseMomentum, last[i], D);  // sma.c:155-164
+    last[i] = D;
+  }
+  z0 = fmaf(1.0f, D, z0);  // sma.c:169-174
+  z[i] = z0;
+  if (copy)
+    for (int r = 0; r < a.nrep; ++r) reinterpret_cast<float *>(a.w[r])[i] = z0;  // sma.c:185-227
 }
 
 // ---------------------------------------------------------------------------
@@ -80,17 +127,24 @@ __device__ __forceinline__ v4f vfma(v4f a, v4f b, v4f c) {
 //   z   = fma(1, D, z)                 :168-174
 //   w_i = z                            :185-227 (if any replica asked to copy)
 // ---------------------------------------------------------------------------
-template <int R, bool MOM, bool COPY, int P, int U>
+template <int R, bool MOM, bool COPY, int P, bool TAIL, int U>
 __global__ __launch_bounds__(256) void sma_fused_kernel(const SmaArgs a) {
   constexpr int RR = (R > 0) ? R : kChunk;
-  const uint32_t trip = gridDim.x * blockDim.x * U;
+  if constexpr (TAIL) {
+    if (blockIdx.x < (uint32_t)a.tail_blocks) {
+      sma_tail_elem<0, MOM>(a, COPY);
+      return;
+    }
+  }
+  const uint32_t tb = TAIL ? (uint32_t)a.tail_blocks : 0u;
+  const uint32_t trip = (gridDim.x - tb) * blockDim.x * U;
   const uint32_t n4 = (uint32_t)a.n4;
   const v4f al = a.alpha;
   const v4f nal = -a.alpha;
   const v4f mb = kBaseMomentum;
   const v4f one = 1.0f;
   const v4f mone = -1.0f;
-  for (uint32_t base = first_elem<U>(); base < n4; base += trip) {
+  for (uint32_t base = first_elem<U>(blockIdx.x - tb); base < n4; base += trip) {
     v4f zv[U], lv[U], acc[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -160,17 +214,24 @@ __global__ __launch_bounds__(256) void sma_fused_kernel(const SmaArgs a) {
 // ---------------------------------------------------------------------------
 // Kernel A (G > 1): Phase A on this device's locked replicas -> acc.
 // ---------------------------------------------------------------------------
-template <int R, int P, int U>
+template <int R, int P, bool TAIL, int U>
 __global__ __launch_bounds__(256) void sma_accumulate_kernel(const SmaArgs a) {
   constexpr int RR = (R > 0) ? R : kChunk;
   if (a.ctrl_out != nullptr && blockIdx.x == 0 && threadIdx.x < kCtrlFloats)
     a.ctrl_out[threadIdx.x] = (threadIdx.x == 0) ? a.copies : 0.0f;
-  const uint32_t trip = gridDim.x * blockDim.x * U;
+  if constexpr (TAIL) {
+    if (blockIdx.x < (uint32_t)a.tail_blocks) {
+      sma_tail_elem<1, false>(a, false);
+      return;
+    }
+  }
+  const uint32_t tb = TAIL ? (uint32_t)a.tail_blocks : 0u;
+  const uint32_t trip = (gridDim.x - tb) * blockDim.x * U;
   const uint32_t n4 = (uint32_t)a.n4;
   const v4f al = a.alpha;
   const v4f nal = -a.alpha;
   const v4f mone = -1.0f;
-  for (uint32_t base = first_elem<U>(); base < n4; base += trip) {
+  for (uint32_t base = first_elem<U>(blockIdx.x - tb); base < n4; base += trip) {
     v4f zv[U], acc[U];
     const int nrep = (R >= 0) ? R : a.nrep;
 #pragma unroll
@@ -218,16 +279,23 @@ __global__ __launch_bounds__(256) void sma_accumulate_kernel(const SmaArgs a) {
 // Kernel B (G > 1): Phase C on the all-reduced D, then Phase D when the
 // reduced control block says any device had a copy request.
 // ---------------------------------------------------------------------------
-template <bool MOM, int P, int U>
+template <bool MOM, int P, bool TAIL, int U>
 __global__ __launch_bounds__(256) void sma_apply_kernel(const SmaArgs a) {
   const float requests = a.decision_mode == 2 ? *a.decision : a.ctrl_in[0];
   if (a.decision_mode == 1 && blockIdx.x == 0 && threadIdx.x == 0) *a.decision = requests;
   const bool copy = requests > 0.0f;
-  const uint32_t trip = gridDim.x * blockDim.x * U;
+  if constexpr (TAIL) {
+    if (blockIdx.x < (uint32_t)a.tail_blocks) {
+      sma_tail_elem<2, MOM>(a, copy);
+      return;
+    }
+  }
+  const uint32_t tb = TAIL ? (uint32_t)a.tail_blocks : 0u;
+  const uint32_t trip = (gridDim.x - tb) * blockDim.x * U;
   const uint32_t n4 = (uint32_t)a.n4;
   const v4f mb = kBaseMomentum;
   const v4f one = 1.0f;
-  for (uint32_t base = first_elem<U>(); base < n4; base += trip) {
+  for (uint32_t base = first_elem<U>(blockIdx.x - tb); base < n4; base += trip) {
     v4f Dv[U], zv[U], lv[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -531,12 +599,36 @@ __global__ __launch_bounds__(256) void sma_peer_apply_kernel(const SmaArgs a, co
 //   s = w                                :71 / :87
 //   w = fma(1, g, w)  or  fma(rate, g, w) without momentum  :74 / :90
 // ---------------------------------------------------------------------------
-template <bool MOM, bool WD, int P, int U>
+template <bool MOM, bool WD, int P, bool TAIL, int U>
 __global__ __launch_bounds__(512) void sma_optimise_kernel(const OptArgs a) {
-  const uint32_t trip = gridDim.x * blockDim.x * U;
+  if constexpr (TAIL) {
+    if (blockIdx.x < (uint32_t)a.tail_blocks) {  // the caller's last elements (see sma_tail_elem)
+      const int64_t i = a.tail_lo + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+      if (i >= a.tail_hi) return;
+      float *w = reinterpret_cast<float *>(a.w), *g = reinterpret_cast<float *>(a.g);
+      const float wv = w[i];
+      float gv = g[i];
+      if constexpr (WD) gv = fmaf(a.wd, wv, gv);  // sma.cu:24-31
+      reinterpret_cast<float *>(a.s)[i] = wv;     // :71 / :87
+      if constexpr (MOM) {
+        float *last = reinterpret_cast<float *>(a.last);
+        gv = a.rate * gv;                  // :52-56
+        gv = fmaf(a.momentum, last[i], gv);  // :59-64
+        last[i] = gv;                      // :68
+        w[i] = fmaf(1.0f, gv, wv);         // :74
+        g[i] = gv;
+      } else {
+        w[i] = fmaf(a.rate, gv, wv);  // :90
+        if constexpr (WD) g[i] = gv;
+      }
+      return;
+    }
+  }
+  const uint32_t tb = TAIL ? (uint32_t)a.tail_blocks : 0u;
+  const uint32_t trip = (gridDim.x - tb) * blockDim.x * U;
   const uint32_t n4 = (uint32_t)a.n4;
   const v4f rate = a.rate, mu = a.momentum, wd = a.wd, one = 1.0f;
-  for (uint32_t base = first_elem<U>(); base < n4; base += trip) {
+  for (uint32_t base = first_elem<U>(blockIdx.x - tb); base < n4; base += trip) {
     v4f w[U], g[U], l[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -769,17 +861,39 @@ inline dim3 grid_for(int64_t n4, const LaunchConfig &cfg) {
   return dim3((unsigned)blocks);
 }
 
+// Workgroups for a launch's tail elements (SmaArgs / OptArgs tail_lo..hi).
+inline unsigned tail_blocks_for(int64_t lo, int64_t hi, int block) {
+  return hi > lo ? (unsigned)((hi - lo + block - 1) / block) : 0u;
+}
+
 template <int R, bool MOM, bool COPY, int P>
-hipError_t fused_u(const SmaArgs &a, const LaunchConfig &cfg0, hipStream_t s, Timing t) {
-  const LaunchConfig cfg = small_launch_shape(cfg0, a.n4);
-  const dim3 g = grid_for(a.n4, cfg);
-  const unsigned lds = lds_for_occupancy(cfg, (COPY ? 1 : 2) * a.nrep + 1 + (MOM ? 1 : 0), a.nrep + 1 + (MOM ? 1 : 0), g.x);
+hipError_t fused_u(const SmaArgs &a0, const LaunchConfig &cfg0, hipStream_t s, Timing t) {
+  const LaunchConfig cfg = small_launch_shape(cfg0, a0.n4);
+  dim3 g = grid_for(a0.n4, cfg);
+  const unsigned lds = lds_for_occupancy(cfg, (COPY ? 1 : 2) * a0.nrep + 1 + (MOM ? 1 : 0), a0.nrep + 1 + (MOM ? 1 : 0), g.x);
+  if (a0.tail_hi > a0.tail_lo) {  // caller-owned buffers: the tail rides the same launch
+    if constexpr (P != 1) {
+      return hipErrorInvalidValue;
+    } else {
+      SmaArgs a = a0;
+      a.tail_blocks = (int)tail_blocks_for(a.tail_lo, a.tail_hi, cfg.block);
+      g.x += (unsigned)a.tail_blocks;
+      if (cfg.unroll == 2)
+        hipExtLaunchKernelGGL((sma_fused_kernel<R, MOM, COPY, P, true, 2>), g, dim3(cfg.block), lds, s, t.start, t.stop, 0, a);
+      else if (cfg.unroll == 1)
+        hipExtLaunchKernelGGL((sma_fused_kernel<R, MOM, COPY, P, true, 1>), g, dim3(cfg.block), lds, s, t.start, t.stop, 0, a);
+      else
+        return hipErrorInvalidValue;
+      return hipGetLastError();
+    }
+  }
+  const SmaArgs &a = a0;
   if (cfg.unroll == 4)
-    hipExtLaunchKernelGGL((sma_fused_kernel<R, MOM, COPY, P, 4>), g, dim3(cfg.block), lds, s, t.start, t.stop, 0, a);
+    hipExtLaunchKernelGGL((sma_fused_kernel<R, MOM, COPY, P, false, 4>), g, dim3(cfg.block), lds, s, t.start, t.stop, 0, a);
   else if (cfg.unroll == 2)
-    hipExtLaunchKernelGGL((sma_fused_kernel<R, MOM, COPY, P, 2>), g, dim3(cfg.block), lds, s, t.start, t.stop, 0, a);
+    hipExtLaunchKernelGGL((sma_fused_kernel<R, MOM, COPY, P, false, 2>), g, dim3(cfg.block), lds, s, t.start, t.stop, 0, a);
   else
-    hipExtLaunchKernelGGL((sma_fused_kernel<R, MOM, COPY, P, 1>), g, dim3(cfg.block), lds, s, t.start, t.stop, 0, a);
+    hipExtLaunchKernelGGL((sma_fused_kernel<R, MOM, COPY, P, false, 1>), g, dim3(cfg.block), lds, s, t.start, t.stop, 0, a);
   return hipGetLastError();
 }
 
@@ -800,16 +914,33 @@ hipError_t fused_r(const SmaArgs &a, const LaunchConfig &cfg, hipStream_t s, Tim
 }
 
 template <int R, int P>
-hipError_t acc_u(const SmaArgs &a, const LaunchConfig &cfg0, hipStream_t s, Timing t) {
-  const LaunchConfig cfg = small_launch_shape(cfg0, a.n4);
-  const dim3 g = grid_for(a.n4, cfg);
-  const unsigned lds = lds_for_occupancy(cfg, 2 * a.nrep + 1, a.nrep + 1, g.x);
+hipError_t acc_u(const SmaArgs &a0, const LaunchConfig &cfg0, hipStream_t s, Timing t) {
+  const LaunchConfig cfg = small_launch_shape(cfg0, a0.n4);
+  dim3 g = grid_for(a0.n4, cfg);
+  const unsigned lds = lds_for_occupancy(cfg, 2 * a0.nrep + 1, a0.nrep + 1, g.x);
+  if (a0.tail_hi > a0.tail_lo) {
+    if constexpr (P != 1) {
+      return hipErrorInvalidValue;
+    } else {
+      SmaArgs a = a0;
+      a.tail_blocks = (int)tail_blocks_for(a.tail_lo, a.tail_hi, cfg.block);
+      g.x += (unsigned)a.tail_blocks;
+      if (cfg.unroll == 2)
+        hipExtLaunchKernelGGL((sma_accumulate_kernel<R, P, true, 2>), g, dim3(cfg.block), lds, s, t.start, t.stop, 0, a);
+      else if (cfg.unroll == 1)
+        hipExtLaunchKernelGGL((sma_accumulate_kernel<R, P, true, 1>), g, dim3(cfg.block), lds, s, t.start, t.stop, 0, a);
+      else
+        return hipErrorInvalidValue;
+      return hipGetLastError();
+    }
+  }
+  const SmaArgs &a = a0;
   if (cfg.unroll == 4)
-    hipExtLaunchKernelGGL((sma_accumulate_kernel<R, P, 4>), g, dim3(cfg.block), lds, s, t.start, t.stop, 0, a);
+    hipExtLaunchKernelGGL((sma_accumulate_kernel<R, P, false, 4>), g, dim3(cfg.block), lds, s, t.start, t.stop, 0, a);
   else if (cfg.unroll == 2)
-    hipExtLaunchKernelGGL((sma_accumulate_kernel<R, P, 2>), g, dim3(cfg.block), lds, s, t.start, t.stop, 0, a);
+    hipExtLaunchKernelGGL((sma_accumulate_kernel<R, P, false, 2>), g, dim3(cfg.block), lds, s, t.start, t.stop, 0, a);
   else
-    hipExtLaunchKernelGGL((sma_accumulate_kernel<R, P, 1>), g, dim3(cfg.block), lds, s, t.start, t.stop, 0, a);
+    hipExtLaunchKernelGGL((sma_accumulate_kernel<R, P, false, 1>), g, dim3(cfg.block), lds, s, t.start, t.stop, 0, a);
   return hipGetLastError();
 }
 
@@ -830,16 +961,33 @@ hipError_t acc_r(const SmaArgs &a, const LaunchConfig &cfg, hipStream_t s, Timin
 }
 
 template <bool MOM, int P>
-hipError_t apply_u(const SmaArgs &a, const LaunchConfig &cfg0, hipStream_t s, Timing t) {
-  const LaunchConfig cfg = small_launch_shape(cfg0, a.n4);
-  const dim3 g = grid_for(a.n4, cfg);
+hipError_t apply_u(const SmaArgs &a0, const LaunchConfig &cfg0, hipStream_t s, Timing t) {
+  const LaunchConfig cfg = small_launch_shape(cfg0, a0.n4);
+  dim3 g = grid_for(a0.n4, cfg);
   const unsigned lds = lds_for_occupancy(cfg, MOM ? 3 : 2, MOM ? 2 : 1, g.x);
+  if (a0.tail_hi > a0.tail_lo) {
+    if constexpr (P != 1) {
+      return hipErrorInvalidValue;
+    } else {
+      SmaArgs a = a0;
+      a.tail_blocks = (int)tail_blocks_for(a.tail_lo, a.tail_hi, cfg.block);
+      g.x += (unsigned)a.tail_blocks;
+      if (cfg.unroll == 2)
+        hipExtLaunchKernelGGL((sma_apply_kernel<MOM, P, true, 2>), g, dim3(cfg.block), lds, s, t.start, t.stop, 0, a);
+      else if (cfg.unroll == 1)
+        hipExtLaunchKernelGGL((sma_apply_kernel<MOM, P, true, 1>), g, dim3(cfg.block), lds, s, t.start, t.stop, 0, a);
+      else
+        return hipErrorInvalidValue;
+      return hipGetLastError();
+    }
+  }
+  const SmaArgs &a = a0;
   if (cfg.unroll == 4)
-    hipExtLaunchKernelGGL((sma_apply_kernel<MOM, P, 4>), g, dim3(cfg.block), lds, s, t.start, t.stop, 0, a);
+    hipExtLaunchKernelGGL((sma_apply_kernel<MOM, P, false, 4>), g, dim3(cfg.block), lds, s, t.start, t.stop, 0, a);
   else if (cfg.unroll == 2)
-    hipExtLaunchKernelGGL((sma_apply_kernel<MOM, P, 2>), g, dim3(cfg.block), lds, s, t.start, t.stop, 0, a);
+    hipExtLaunchKernelGGL((sma_apply_kernel<MOM, P, false, 2>), g, dim3(cfg.block), lds, s, t.start, t.stop, 0, a);
   else
-    hipExtLaunchKernelGGL((sma_apply_kernel<MOM, P, 1>), g, dim3(cfg.block), lds, s, t.start, t.stop, 0, a);
+    hipExtLaunchKernelGGL((sma_apply_kernel<MOM, P, false, 1>), g, dim3(cfg.block), lds, s, t.start, t.stop, 0, a);
   return hipGetLastError();
 }
 
@@ -1021,9 +1169,28 @@ hipError_t launch_sma_shard_momentum(const SmaArgs &a, const LaunchConfig &cfg0,
   } while (0)
 
 template <bool MOM, bool WD, int P>
-hipError_t optimise_p(const OptArgs &a, const LaunchConfig &cfg, hipStream_t stream, Timing t) {
+hipError_t optimise_p(const OptArgs &a0, const LaunchConfig &cfg, hipStream_t stream, Timing t) {
   const int reads = 2 + (MOM ? 1 : 0), writes = MOM ? 4 : (WD ? 3 : 2);
-  CBX_LAUNCH_U(sma_optimise_kernel, MOM, WD, P);
+  if (a0.tail_hi > a0.tail_lo) {  // caller-owned buffers: the tail rides the same launch
+    if constexpr (P != 1) {
+      return hipErrorInvalidValue;
+    } else {
+      OptArgs a = a0;
+      dim3 g = grid_for(a.n4, cfg);
+      const unsigned l = lds_for_occupancy(cfg, reads, writes, g.x);
+      a.tail_blocks = (int)tail_blocks_for(a.tail_lo, a.tail_hi, cfg.block);
+      g.x += (unsigned)a.tail_blocks;
+      if (cfg.unroll == 2)
+        hipExtLaunchKernelGGL((sma_optimise_kernel<MOM, WD, P, true, 2>), g, dim3(cfg.block), l, stream, t.start, t.stop, 0, a);
+      else if (cfg.unroll == 1)
+        hipExtLaunchKernelGGL((sma_optimise_kernel<MOM, WD, P, true, 1>), g, dim3(cfg.block), l, stream, t.start, t.stop, 0, a);
+      else
+        return hipErrorInvalidValue;
+      return hipGetLastError();
+    }
+  }
+  const OptArgs &a = a0;
+  CBX_LAUNCH_U(sma_optimise_kernel, MOM, WD, P, false);
   return hipGetLastError();
 }
 

@@ -7,10 +7,12 @@
 //
 // The context API (context.hip) owns an arena whose buffers are padded to
 // whole kernel trips; the reference's buffers hold exactly `elements` floats.
-// So every step here is the bulk of the buffers through the same float4
-// kernels (n4b float4s, a multiple of kPadFloat4) plus a scalar tail kernel
-// over the last < 4 * kPadFloat4 + 3 elements, with the same fma sequence per
-// element: the results equal the context path's and the oracle's bit for bit.
+// So every launch here runs the bulk of the buffers through the same float4
+// kernels (n4b float4s, a multiple of kPadFloat4) and the last < 4 *
+// kPadFloat4 elements on extra workgroups of the same launch, one float per
+// lane (the kernels' TAIL instantiations, sma_kernels.hip), with the same fma
+// sequence per element: the results equal the context path's and the
+// oracle's bit for bit.
 //
 // The plan owns what the step needs beyond the caller's buffers: the
 // accumulator and the all-reduced difference (base->gradient and base->diff
@@ -22,96 +24,6 @@
 using namespace cbx::host;
 
 namespace {
-
-// Elements [lo, hi) outside the float4 kernels' trips.  phase 0: the fused
-// one-GPU step; 1: kernel A (Phase A into acc); 2: kernel B (Phase C, and
-// Phase D when the reduced control block counts a request).
-struct TailArgs {
-  const float *s[cbx::kMaxReplicas];
-  float *w[cbx::kMaxReplicas];
-  float *z;
-  float *last;  // null without base momentum
-  float *acc;
-  const float *D;
-  float *ctrl_out;       // phase 1: write this device's control block (when the bulk launch does not)
-  const float *ctrl_in;  // phase 2: the reduced control block
-  int64_t lo, hi;
-  float alpha;
-  float copies;
-  int nrep;
-  int phase;
-  int copy;  // phase 0: Phase D requested
-  int pad_;
-};
-
-__global__ __launch_bounds__(256) void sma_tail_kernel(const TailArgs a) {
-  if (a.ctrl_out != nullptr && blockIdx.x == 0 && threadIdx.x < cbx::kCtrlFloats)
-    a.ctrl_out[threadIdx.x] = (threadIdx.x == 0) ? a.copies : 0.0f;
-  const int64_t i = a.lo + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= a.hi) return;
-  if (a.phase == 2) {
-    float D = a.D[i];
-    if (a.last) {
-      D = fmaf(cbx::kBaseMomentum, a.last[i], D);  // sma.c:155-164
-      a.last[i] = D;
-    }
-    const float z = fmaf(1.0f, D, a.z[i]);  // sma.c:169-174
-    a.z[i] = z;
-    if (a.ctrl_in[0] > 0.0f)
-      for (int r = 0; r < a.nrep; ++r) a.w[r][i] = z;  // sma.c:185-227
-    return;
-  }
-  const float z0 = a.z[i];
-  float acc = 0.0f;  // sma.c:66
-  for (int r = 0; r < a.nrep; ++r) {
-    const float d = fmaf(-1.0f, z0, a.s[r][i]);  // sma.c:79-90
-    a.w[r][i] = fmaf(-a.alpha, d, a.w[r][i]);    // :93-99
-    acc = fmaf(a.alpha, d, acc);                 // :102-107
-  }
-  if (a.phase == 1) {
-    a.acc[i] = acc;
-    return;
-  }
-  float D = acc;  // common.c:3-57 with one rank
-  if (a.last) {
-    D = fmaf(cbx::kBaseMomentum, a.last[i], D);
-    a.last[i] = D;
-  }
-  const float z = fmaf(1.0f, D, z0);
-  a.z[i] = z;
-  if (a.copy)
-    for (int r = 0; r < a.nrep; ++r) a.w[r][i] = z;
-}
-
-// The optimiser step's tail (kernels/optimisers/sma.cu:3-100, the same
-// per-element sequence as sma_optimise_kernel).
-__global__ __launch_bounds__(256) void sma_optimise_tail_kernel(float *w, float *g, float *last, float *s, int64_t lo,
-                                                                int64_t hi, float rate, float mu, float wd) {
-  const int64_t i = lo + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= hi) return;
-  const float wv = w[i];
-  float gv = g[i];
-  if (wd > 0.0f) gv = fmaf(wd, wv, gv);  // :24-31
-  s[i] = wv;                             // :71 / :87
-  if (mu > 0.0f) {
-    gv = rate * gv;              // :52-56
-    gv = fmaf(mu, last[i], gv);  // :59-64
-    last[i] = gv;                // :68
-    w[i] = fmaf(1.0f, gv, wv);   // :74
-    g[i] = gv;
-  } else {
-    w[i] = fmaf(rate, gv, wv);  // :90
-    if (wd > 0.0f) g[i] = gv;
-  }
-}
-
-hipError_t launch_tail(const TailArgs &a, hipStream_t st) {
-  const int64_t len = a.hi - a.lo;
-  if (len <= 0 && !a.ctrl_out) return hipSuccess;
-  const unsigned blocks = (unsigned)std::max<int64_t>(1, (len + 255) / 256);
-  hipLaunchKernelGGL(sma_tail_kernel, dim3(blocks), dim3(256), 0, st, a);
-  return hipGetLastError();
-}
 
 bool aligned16(const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
 
@@ -277,11 +189,9 @@ int cbx_sma_plan_step(cbx_sma_plan *p, void *const *streams, float *const *z, fl
   if (mom && !last) return fail(CBX_ERR_INVALID, "base momentum > 0 needs the base models' last buffers");
   // Per device: its locked replicas from `first` on, in id order (sma.c:69-73).
   std::vector<cbx::SmaArgs> args(G);
-  std::vector<TailArgs> tails(G);
   int copies_total = 0;
   for (int k = 0; k < G; ++k) {
     std::memset(&args[k], 0, sizeof(cbx::SmaArgs));
-    std::memset(&tails[k], 0, sizeof(TailArgs));
     if (!z[k] || !aligned16(z[k]) || (mom && (!last[k] || !aligned16(last[k]))))
       return fail(CBX_ERR_INVALID, "device %d: base buffers must be non-null and 16-byte aligned", k);
   }
@@ -296,15 +206,12 @@ int cbx_sma_plan_step(cbx_sma_plan *p, void *const *streams, float *const *z, fl
       return fail(CBX_ERR_UNSUPPORTED, "more than %d locked replicas on one device", cbx::kMaxReplicas);
     a.s[a.nrep] = reinterpret_cast<const cbx::v4f *>(s[id]);
     a.w[a.nrep] = reinterpret_cast<cbx::v4f *>(w[id]);
-    tails[k].s[a.nrep] = s[id];
-    tails[k].w[a.nrep] = w[id];
     if (copy[id]) {
       a.copies += 1.0f;  // sma.c:113-120
       ++copies_total;
     }
     ++a.nrep;
   }
-  const int64_t lo = p->n4b * 4;
   for (int k = 0; k < G; ++k) {
     auto &d = p->devs[k];
     cbx::SmaArgs &a = args[k];
@@ -316,19 +223,15 @@ int cbx_sma_plan_step(cbx_sma_plan *p, void *const *streams, float *const *z, fl
     a.ctrl_in = d.D_ctrl;
     a.n4 = p->n4b;
     a.alpha = alpha;  // sma.c:33
-    TailArgs &t = tails[k];
-    t.z = z[k];
-    t.last = mom ? last[k] : nullptr;
-    t.acc = d.acc_ctrl + cbx::kCtrlFloats;
-    t.D = d.D_ctrl + cbx::kCtrlFloats;
-    t.ctrl_in = d.D_ctrl;
-    t.lo = lo;
-    t.hi = p->n;
-    t.alpha = alpha;
-    t.copies = a.copies;
-    t.nrep = a.nrep;
-    t.copy = copies_total > 0;
   }
+  // The elements past the last whole trip, done by extra workgroups of the
+  // launch that covers the buffers' end; float indices relative to the
+  // launch's pointers (offset by start4 float4s).
+  auto with_tail = [&](cbx::SmaArgs a, int64_t start4) {
+    a.tail_lo = (p->n4b - start4) * 4;
+    a.tail_hi = p->n - start4 * 4;
+    return a;
+  };
   if (p->ranks == 1) {
     // One GPU: the all-reduce of one buffer is the identity, so Phases A + C
     // (+ D) fuse into one pass, as in the context's G = 1 step.
@@ -337,9 +240,7 @@ int cbx_sma_plan_step(cbx_sma_plan *p, void *const *streams, float *const *z, fl
     HIP_TRY(hipSetDevice(d.hip_id));
     cbx::LaunchConfig cfg = p->cfg;
     cfg.num_cus = d.num_cus;
-    if (p->n4b > 0) HIP_TRY(cbx::launch_sma_fused(args[0], mom, copies_total > 0, cfg, st));
-    tails[0].phase = 0;
-    HIP_TRY(launch_tail(tails[0], st));
+    HIP_TRY(cbx::launch_sma_fused(with_tail(args[0], 0), mom, copies_total > 0, cfg, st));
     return copies_total > 0 ? 1 : 0;
   }
   // G > 1: kernel A, the grouped all-reduce of the control block + acc
@@ -350,8 +251,7 @@ int cbx_sma_plan_step(cbx_sma_plan *p, void *const *streams, float *const *z, fl
   //   stream      : A(0) A(1) [wait r(0)] B(0) A(2) [wait r(1)] B(1) ...
   //   comm_stream : [wait a(0)] AR(0) [wait a(1)] AR(1) ...
   // The control block rides bucket 0; the tail rides the last bucket (its
-  // kernel A / B tail launches follow the bulk ones, its all-reduce extends
-  // to n).  The next step's AR(k) waits for its A(k), which follows this
+  // kernel A / B launches take the tail too, its all-reduce extends to n).  The next step's AR(k) waits for its A(k), which follows this
   // step's last B on the caller's stream, so no buffer is overwritten early.
   const int64_t pad = cbx::kPadFloat4;
   int64_t nb = p->buckets > 0 ? p->buckets : kDefaultBuckets;
@@ -370,12 +270,9 @@ int cbx_sma_plan_step(cbx_sma_plan *p, void *const *streams, float *const *z, fl
       if (piped) HIP_TRY(hipStreamWaitEvent(st, d.ev_r[b], 0));
       cbx::LaunchConfig cfg = p->apply_cfg;
       cfg.num_cus = d.num_cus;
-      if (len_of(b) > 0) HIP_TRY(cbx::launch_sma_apply(offset_args(args[k], start_of(b), len_of(b)), mom, cfg, st));
-      if (b == nb - 1) {
-        TailArgs t = tails[k];
-        t.phase = 2;
-        HIP_TRY(launch_tail(t, st));
-      }
+      cbx::SmaArgs a = offset_args(args[k], start_of(b), len_of(b));
+      if (b == nb - 1) a = with_tail(a, start_of(b));
+      HIP_TRY(cbx::launch_sma_apply(a, mom, cfg, st));
     }
     return CBX_OK;
   };
@@ -386,14 +283,9 @@ int cbx_sma_plan_step(cbx_sma_plan *p, void *const *streams, float *const *z, fl
       HIP_TRY(hipSetDevice(d.hip_id));
       cbx::LaunchConfig cfg = p->cfg;
       cfg.num_cus = d.num_cus;
-      if (len_of(b) > 0)
-        HIP_TRY(cbx::launch_sma_accumulate(offset_args(args[k], start_of(b), len_of(b)), b == 0, cfg, st));
-      if (b == nb - 1) {
-        TailArgs t = tails[k];
-        t.phase = 1;
-        if (p->n4b == 0) t.ctrl_out = d.acc_ctrl;  // no bulk launch wrote the control block
-        HIP_TRY(launch_tail(t, st));
-      }
+      cbx::SmaArgs a = offset_args(args[k], start_of(b), len_of(b));
+      if (b == nb - 1) a = with_tail(a, start_of(b));
+      HIP_TRY(cbx::launch_sma_accumulate(a, b == 0, cfg, st));
       if (piped) {
         HIP_TRY(hipEventRecord(d.ev_a[b], st));
         HIP_TRY(hipStreamWaitEvent(d.comm_stream, d.ev_a[b], 0));
@@ -460,14 +352,9 @@ int cbx_sma_optimise_buffers(void *stream, float *w, float *g, float *last, floa
   a.wd = weight_decay;
   cbx::LaunchConfig cfg = cbx::aux_launch_config();
   cfg.num_cus = cus;
-  if (a.n4 > 0) HIP_TRY(cbx::launch_sma_optimise(a, cfg, st));
-  const int64_t lo = a.n4 * 4;
-  if (elements > lo) {
-    const unsigned blocks = (unsigned)((elements - lo + 255) / 256);
-    hipLaunchKernelGGL(sma_optimise_tail_kernel, dim3(blocks), dim3(256), 0, st, w, g, a.last ? last : nullptr, s, lo,
-                       (int64_t)elements, a.rate, momentum, weight_decay);
-    HIP_TRY(hipGetLastError());
-  }
+  a.tail_lo = a.n4 * 4;  // the elements past the last whole trip ride the same launch
+  a.tail_hi = elements;
+  HIP_TRY(cbx::launch_sma_optimise(a, cfg, st));
   return CBX_OK;
 }
 
