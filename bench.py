@@ -248,7 +248,7 @@ def bench_seam(torch, n, args, steps=20):
     return {"entry": "cbx_sma_plan_step", "step_ms_mean": round(ms, 4), "steps": steps, "alg_bytes_per_step": b,
             "achieved_GBs": round(b / (ms * 1e-3) / 1e9, 1), "frac": round(b / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
             "buffers": "caller-owned torch allocations of exactly n floats (no padding, no slot stagger)",
-            "timed": "torch events around back-to-back steps on the caller's stream (bulk + tail launch, gaps included)"}
+            "timed": "torch events around back-to-back steps on the caller's stream (one launch per step: bulk + tail workgroups; gaps included)"}
 
 
 def main():
