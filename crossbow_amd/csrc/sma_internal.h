@@ -297,6 +297,8 @@ struct SsgdArgs {
   float momentum;        // barrier: base conf->momentum (synchronoussgd.c:64)
   int nrep;
   int pad_;
+  int64_t tail_lo, tail_hi;  // caller-owned buffers: elements past the last whole trip (see SmaArgs)
+  int tail_blocks;
 };
 // Per task (synchronoussgd.cu:3-56): g = fma(wd, w, g); acc = fma(rate, g, acc).
 hipError_t launch_ssgd_accumulate(const SsgdArgs &a, const LaunchConfig &cfg, hipStream_t stream, Timing t = {});

@@ -726,12 +726,27 @@ __global__ __launch_bounds__(512) void broadcast_kernel(const SmaArgs a) {
 //   acc = fma(rate, g, acc)  :46-52
 // Reads g, acc (, w) and writes acc (, g): 12n B (+8n with weight decay).
 // ---------------------------------------------------------------------------
-template <bool WD, int P, int U>
+template <bool WD, int P, bool TAIL, int U>
 __global__ __launch_bounds__(512) void ssgd_accumulate_kernel(const SsgdArgs a) {
-  const uint32_t trip = gridDim.x * blockDim.x * U;
+  if constexpr (TAIL) {
+    if (blockIdx.x < (uint32_t)a.tail_blocks) {  // the caller's last elements (see sma_tail_elem)
+      const int64_t i = a.tail_lo + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+      if (i >= a.tail_hi) return;
+      float *g = reinterpret_cast<float *>(a.g), *acc = reinterpret_cast<float *>(a.acc);
+      float gv = g[i];
+      if constexpr (WD) {
+        gv = fmaf(a.wd, reinterpret_cast<const float *>(a.wsrc)[i], gv);  // synchronoussgd.cu:20-26
+        g[i] = gv;
+      }
+      acc[i] = fmaf(a.rate, gv, acc[i]);  // :46-52
+      return;
+    }
+  }
+  const uint32_t tb = TAIL ? (uint32_t)a.tail_blocks : 0u;
+  const uint32_t trip = (gridDim.x - tb) * blockDim.x * U;
   const uint32_t n4 = (uint32_t)a.n4;
   const v4f rate = a.rate, wd = a.wd;
-  for (uint32_t base = first_elem<U>(); base < n4; base += trip) {
+  for (uint32_t base = first_elem<U>(blockIdx.x - tb); base < n4; base += trip) {
     v4f g[U], acc[U], w[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -760,12 +775,31 @@ __global__ __launch_bounds__(512) void ssgd_accumulate_kernel(const SsgdArgs a) 
 //   acc = 0                           :103
 //   w_i = z for locked replicas       common.c:198-220
 // Reads D, z (, last) and writes z, acc, R x w (, last).
-template <bool MOM, int P, int U>
+template <bool MOM, int P, bool TAIL, int U>
 __global__ __launch_bounds__(512) void ssgd_apply_kernel(const SsgdArgs a) {
-  const uint32_t trip = gridDim.x * blockDim.x * U;
+  if constexpr (TAIL) {
+    if (blockIdx.x < (uint32_t)a.tail_blocks) {  // the caller's last elements (see sma_tail_elem)
+      const int64_t i = a.tail_lo + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+      if (i >= a.tail_hi) return;
+      float *z = reinterpret_cast<float *>(a.z);
+      float D = a.ratio * reinterpret_cast<const float *>(a.D)[i];  // synchronoussgd.c:55-62
+      if constexpr (MOM) {
+        float *last = reinterpret_cast<float *>(a.last);
+        D = fmaf(a.momentum, last[i], D);  // :64-76
+        last[i] = D;
+      }
+      const float zv = fmaf(1.0f, D, z[i]);  // :79-84
+      z[i] = zv;
+      reinterpret_cast<float *>(a.acc)[i] = 0.0f;  // :103
+      for (int r = 0; r < a.nrep; ++r) reinterpret_cast<float *>(a.w[r])[i] = zv;  // common.c:198-220
+      return;
+    }
+  }
+  const uint32_t tb = TAIL ? (uint32_t)a.tail_blocks : 0u;
+  const uint32_t trip = (gridDim.x - tb) * blockDim.x * U;
   const uint32_t n4 = (uint32_t)a.n4;
   const v4f ratio = a.ratio, mu = a.momentum, one = 1.0f, zero = 0.0f;
-  for (uint32_t base = first_elem<U>(); base < n4; base += trip) {
+  for (uint32_t base = first_elem<U>(blockIdx.x - tb); base < n4; base += trip) {
     v4f D[U], z[U], l[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -1232,10 +1266,34 @@ hipError_t launch_broadcast(const SmaArgs &a, const LaunchConfig &cfg, hipStream
   return cfg.policy == 1 ? broadcast_p<1>(a, cfg, stream, t) : broadcast_p<0>(a, cfg, stream, t);
 }
 
+// Launch KERNEL<..., TAIL = true, U> with the launch's tail workgroups in
+// front (caller-owned buffers: a.tail_lo .. a.tail_hi); policy 1, unroll 1 or 2.
+#define CBX_LAUNCH_TAIL(KERNEL, ...)                                                                     \
+  do {                                                                                                   \
+    if constexpr (P != 1) {                                                                              \
+      return hipErrorInvalidValue;                                                                       \
+    } else {                                                                                             \
+      auto a = a0;                                                                                       \
+      dim3 g_ = grid_for(a.n4, cfg);                                                                     \
+      const unsigned l_ = lds_for_occupancy(cfg, reads, writes, g_.x);                                   \
+      a.tail_blocks = (int)tail_blocks_for(a.tail_lo, a.tail_hi, cfg.block);                             \
+      g_.x += (unsigned)a.tail_blocks;                                                                   \
+      if (cfg.unroll == 2)                                                                               \
+        hipExtLaunchKernelGGL((KERNEL<__VA_ARGS__, true, 2>), g_, dim3(cfg.block), l_, stream, t.start, t.stop, 0, a); \
+      else if (cfg.unroll == 1)                                                                          \
+        hipExtLaunchKernelGGL((KERNEL<__VA_ARGS__, true, 1>), g_, dim3(cfg.block), l_, stream, t.start, t.stop, 0, a); \
+      else                                                                                               \
+        return hipErrorInvalidValue;                                                                     \
+      return hipGetLastError();                                                                          \
+    }                                                                                                    \
+  } while (0)
+
 template <bool WD, int P>
-hipError_t ssgd_acc_p(const SsgdArgs &a, const LaunchConfig &cfg, hipStream_t stream, Timing t) {
+hipError_t ssgd_acc_p(const SsgdArgs &a0, const LaunchConfig &cfg, hipStream_t stream, Timing t) {
   const int reads = 2 + (WD ? 1 : 0), writes = 1 + (WD ? 1 : 0);
-  CBX_LAUNCH_U(ssgd_accumulate_kernel, WD, P);
+  if (a0.tail_hi > a0.tail_lo) CBX_LAUNCH_TAIL(ssgd_accumulate_kernel, WD, P);
+  const SsgdArgs &a = a0;
+  CBX_LAUNCH_U(ssgd_accumulate_kernel, WD, P, false);
   return hipGetLastError();
 }
 
@@ -1246,9 +1304,11 @@ hipError_t launch_ssgd_accumulate(const SsgdArgs &a, const LaunchConfig &cfg, hi
 }
 
 template <bool MOM, int P>
-hipError_t ssgd_apply_p(const SsgdArgs &a, const LaunchConfig &cfg, hipStream_t stream, Timing t) {
-  const int reads = 2 + (MOM ? 1 : 0), writes = 2 + (MOM ? 1 : 0) + a.nrep;
-  CBX_LAUNCH_U(ssgd_apply_kernel, MOM, P);
+hipError_t ssgd_apply_p(const SsgdArgs &a0, const LaunchConfig &cfg, hipStream_t stream, Timing t) {
+  const int reads = 2 + (MOM ? 1 : 0), writes = 2 + (MOM ? 1 : 0) + a0.nrep;
+  if (a0.tail_hi > a0.tail_lo) CBX_LAUNCH_TAIL(ssgd_apply_kernel, MOM, P);
+  const SsgdArgs &a = a0;
+  CBX_LAUNCH_U(ssgd_apply_kernel, MOM, P, false);
   return hipGetLastError();
 }
 
@@ -1259,6 +1319,7 @@ hipError_t launch_ssgd_apply(const SsgdArgs &a, const LaunchConfig &cfg, hipStre
 }
 
 #undef CBX_LAUNCH_U
+#undef CBX_LAUNCH_TAIL
 
 hipError_t launch_bn_pack(const BnSegment *segs, int nseg, uint32_t maxlen, float *scratch, hipStream_t stream) {
   if (nseg <= 0 || maxlen == 0) return hipSuccess;

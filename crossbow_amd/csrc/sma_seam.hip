@@ -68,6 +68,7 @@ struct cbx_sma_plan {
   int buckets = 0;  // G > 1: 0 = kDefaultBuckets, 1 = in order on the caller's stream
   cbx::LaunchConfig cfg;
   cbx::LaunchConfig apply_cfg = cbx::sma_apply_launch_config();
+  cbx::LaunchConfig ssgd_apply_cfg = cbx::ssgd_apply_launch_config();
 };
 
 namespace {
@@ -319,6 +320,140 @@ int cbx_sma_plan_step(cbx_sma_plan *p, void *const *streams, float *const *z, fl
   }
   TRY(apply(nb - 1));
   return copies_total > 0 ? 1 : 0;
+}
+
+// crossbowSynchronisationSynchronousSGD (synch/synchronoussgd.c:13-106) over
+// the caller's buffers: the all-reduce of every device's accumulated,
+// lr-scaled gradient, the 1/wpc scale, the base momentum (the configured one,
+// not forced to 0.9), z += D, the reset of the accumulator and base ->
+// replica copies (common.c:198-220), in one apply pass per bucket.  G = 1 runs
+// the multi-GPU algorithm with the identity all-reduce (the reference's
+// single-GPU variant is err(), :5-11), as the context does.
+int cbx_ssgd_plan_step(cbx_sma_plan *p, void *const *streams, float *const *z, float *const *last, float *const *acc,
+                       int nreplicas, const int *replica_device, float *const *w, const int *locked, float momentum,
+                       int wpc, int first) {
+  TraceRange trace("cbx_ssgd_plan_step");
+  if (!p) return fail(CBX_ERR_INVALID, "null plan");
+  const int G = (int)p->devs.size();
+  if (!streams || !z || !acc || nreplicas < 0 || (nreplicas > 0 && (!replica_device || !w || !locked)))
+    return fail(CBX_ERR_INVALID, "cbx_ssgd_plan_step: missing arguments");
+  if (wpc <= 0) return fail(CBX_ERR_INVALID, "S-SGD needs the work per clock (wpc %d)", wpc);
+  if (first < 0 || first > nreplicas) return fail(CBX_ERR_INVALID, "first replica %d out of range", first);
+  const bool mom = momentum > 0.0f;  // synchronoussgd.c:64
+  if (mom && !last) return fail(CBX_ERR_INVALID, "momentum > 0 needs the base models' last buffers");
+  std::vector<cbx::SsgdArgs> args(G);
+  for (int k = 0; k < G; ++k) {
+    cbx::SsgdArgs &a = args[k];
+    std::memset(&a, 0, sizeof(a));
+    if (!z[k] || !acc[k] || !aligned16(z[k]) || !aligned16(acc[k]) || (mom && (!last[k] || !aligned16(last[k]))))
+      return fail(CBX_ERR_INVALID, "device %d: base buffers must be non-null and 16-byte aligned", k);
+    a.z = reinterpret_cast<cbx::v4f *>(z[k]);
+    a.last = mom ? reinterpret_cast<cbx::v4f *>(last[k]) : nullptr;
+    a.acc = reinterpret_cast<cbx::v4f *>(acc[k]);
+    a.D = p->ranks == 1 ? a.acc : reinterpret_cast<const cbx::v4f *>(p->devs[k].D_ctrl + cbx::kCtrlFloats);
+    a.n4 = p->n4b;
+    a.ratio = (float)(1.0 / (double)(float)wpc);  // :55
+    a.momentum = mom ? momentum : 0.0f;
+  }
+  for (int id = first; id < nreplicas; ++id) {  // common.c:208: locked replicas from `first` on
+    if (!locked[id]) continue;
+    const int k = replica_device[id];
+    if (k < 0 || k >= G) return fail(CBX_ERR_INVALID, "replica %d on device %d of %d", id, k, G);
+    if (!w[id] || !aligned16(w[id])) return fail(CBX_ERR_INVALID, "replica %d: buffer must be 16-byte aligned", id);
+    if (args[k].nrep >= cbx::kMaxReplicas)
+      return fail(CBX_ERR_UNSUPPORTED, "more than %d locked replicas on one device", cbx::kMaxReplicas);
+    args[k].w[args[k].nrep++] = reinterpret_cast<cbx::v4f *>(w[id]);
+  }
+  // Buckets as in the SMA step; at G > 1 with more than one, the all-reduce
+  // of bucket k+1 runs on the plan's stream beside the apply of bucket k:
+  //   stream      : [entry] [wait r(0)] K(0) [wait r(1)] K(1) ...
+  //   comm_stream : [wait entry] AR(0) AR(1) ...
+  const int64_t pad = cbx::kPadFloat4;
+  int64_t nb = p->ranks == 1 ? 1 : (p->buckets > 0 ? p->buckets : kDefaultBuckets);
+  int64_t b4 = p->n4b;
+  if (nb > 1 && p->n4b > 0) b4 = ((p->n4b + nb - 1) / nb + pad - 1) / pad * pad;
+  nb = b4 > 0 ? (p->n4b + b4 - 1) / b4 : 1;
+  const bool piped = p->ranks > 1 && nb > 1;
+  if (piped) {
+    TRY(ensure_pipeline(p, nb));
+    for (int k = 0; k < G; ++k) {  // everything the task steps accumulated, in stream order
+      auto &d = p->devs[k];
+      HIP_TRY(hipSetDevice(d.hip_id));
+      HIP_TRY(hipEventRecord(d.ev_a[0], static_cast<hipStream_t>(streams[k])));
+      HIP_TRY(hipStreamWaitEvent(d.comm_stream, d.ev_a[0], 0));
+    }
+  }
+  for (int64_t b = 0; b < nb; ++b) {
+    const int64_t s4 = b * b4, l4 = std::min(b4, p->n4b - s4);
+    if (p->ranks > 1) {
+      NCCL_TRY(ncclGroupStart());
+      for (int k = 0; k < G; ++k) {
+        auto &d = p->devs[k];
+        HIP_TRY(hipSetDevice(d.hip_id));
+        const int64_t hi_f = b == nb - 1 ? p->n : (s4 + l4) * 4;
+        NCCL_TRY(ncclAllReduce(acc[k] + s4 * 4, d.D_ctrl + cbx::kCtrlFloats + s4 * 4, (size_t)(hi_f - s4 * 4),
+                               ncclFloat, ncclSum, d.comm,
+                               piped ? d.comm_stream : static_cast<hipStream_t>(streams[k])));
+      }
+      NCCL_TRY(ncclGroupEnd());
+    }
+    for (int k = 0; k < G; ++k) {
+      auto &d = p->devs[k];
+      hipStream_t st = static_cast<hipStream_t>(streams[k]);
+      HIP_TRY(hipSetDevice(d.hip_id));
+      if (piped) {
+        HIP_TRY(hipEventRecord(d.ev_r[b], d.comm_stream));
+        HIP_TRY(hipStreamWaitEvent(st, d.ev_r[b], 0));
+      }
+      cbx::SsgdArgs a = args[k];
+      for (int r = 0; r < a.nrep; ++r) a.w[r] += s4;
+      a.z += s4;
+      if (a.last) a.last += s4;
+      a.acc += s4;
+      a.D += s4;
+      a.n4 = l4;
+      if (b == nb - 1) {  // the elements past the last whole trip ride this launch
+        a.tail_lo = (p->n4b - s4) * 4;
+        a.tail_hi = p->n - s4 * 4;
+      }
+      cbx::LaunchConfig cfg = p->ssgd_apply_cfg;
+      cfg.num_cus = d.num_cus;
+      HIP_TRY(cbx::launch_ssgd_apply(a, cfg, st));
+    }
+  }
+  return CBX_OK;
+}
+
+// crossbowKernelOptimiserSynchronousSGD (kernels/optimisers/synchronoussgd.cu:
+// 3-56) over the caller's buffers, one pass: weight decay into the replica's
+// gradient, then the lr-scaled gradient added into the device's base-model
+// gradient.  On `stream` = the device's model-synchronisation stream, after
+// it waits for the task's gradient (:37-40), so the tasks of a clock add in
+// stream order.
+int cbx_ssgd_accumulate_buffers(void *stream, const float *w, float *g, float *acc, long long elements,
+                                float learning_rate, float weight_decay) {
+  TraceRange trace("cbx_ssgd_accumulate_buffers");
+  if (elements <= 0 || elements * 4 + 4096 >= (1ll << 32))
+    return fail(CBX_ERR_INVALID, "cbx_ssgd_accumulate_buffers: %lld elements out of range", elements);
+  if (!g || !acc || (weight_decay > 0.0f && !w)) return fail(CBX_ERR_INVALID, "cbx_ssgd_accumulate_buffers: missing buffers");
+  if (!aligned16(g) || !aligned16(acc) || (weight_decay > 0.0f && !aligned16(w)))
+    return fail(CBX_ERR_INVALID, "cbx_ssgd_accumulate_buffers: buffers must be 16-byte aligned");
+  int cus = 256;
+  TRY(cus_of_current_device(&cus));
+  cbx::SsgdArgs a;
+  std::memset(&a, 0, sizeof(a));
+  a.wsrc = reinterpret_cast<const cbx::v4f *>(w);
+  a.g = reinterpret_cast<cbx::v4f *>(g);
+  a.acc = reinterpret_cast<cbx::v4f *>(acc);
+  a.n4 = bulk_float4s(elements);
+  a.rate = -1.0f * learning_rate;  // :46
+  a.wd = weight_decay;
+  a.tail_lo = a.n4 * 4;
+  a.tail_hi = elements;
+  cbx::LaunchConfig cfg = cbx::aux_launch_config();
+  cfg.num_cus = cus;
+  HIP_TRY(cbx::launch_ssgd_accumulate(a, cfg, static_cast<hipStream_t>(stream)));
+  return CBX_OK;
 }
 
 int cbx_sma_plan_set_buckets(cbx_sma_plan *p, int buckets) {

@@ -74,6 +74,16 @@ class SmaPlan:
             _ints([r[3] for r in replicas]), _ints([r[4] for r in replicas]), ctypes.c_float(alpha),
             ctypes.c_float(momentum), first), "cbx_sma_plan_step")
 
+    def ssgd_step(self, streams: Sequence[int], z: Sequence[int], last: Optional[Sequence[Optional[int]]],
+                  acc: Sequence[int], replicas: Sequence[Tuple[int, int, int]], momentum: float, wpc: int,
+                  first: int = 0) -> None:
+        """One synchronous-SGD barrier (update model WORKER).  ``replicas[id]`` =
+        (device index, w, locked)."""
+        _raise(self.lib, self.lib.cbx_ssgd_plan_step(
+            self._p, _ptrs(streams), _ptrs(z), _ptrs(last) if last is not None else None, _ptrs(acc),
+            len(replicas), _ints([r[0] for r in replicas]), _ptrs([r[1] for r in replicas]),
+            _ints([r[2] for r in replicas]), ctypes.c_float(momentum), wpc, first), "cbx_ssgd_plan_step")
+
     def set_buckets(self, buckets: int) -> None:
         """G > 1: buckets of the all-reduce pipeline (0 = default 8, 1 = in order)."""
         _raise(self.lib, self.lib.cbx_sma_plan_set_buckets(self._p, buckets), "cbx_sma_plan_set_buckets")
@@ -97,3 +107,12 @@ def optimise_buffers(stream: int, w: int, g: int, last: Optional[int], s: int, e
     _raise(lib, lib.cbx_sma_optimise_buffers(stream or None, w, g, last or None, s, elements,
                                              ctypes.c_float(learning_rate), ctypes.c_float(momentum),
                                              ctypes.c_float(weight_decay)), "cbx_sma_optimise_buffers")
+
+
+def ssgd_accumulate_buffers(stream: int, w: Optional[int], g: int, acc: int, elements: int, learning_rate: float,
+                            weight_decay: float, lib=None) -> None:
+    """``cbx_ssgd_accumulate_buffers``: one task's synchronous-SGD step."""
+    lib = lib if lib is not None else _default_lib()
+    _raise(lib, lib.cbx_ssgd_accumulate_buffers(stream or None, w or None, g, acc, elements,
+                                                ctypes.c_float(learning_rate), ctypes.c_float(weight_decay)),
+           "cbx_ssgd_accumulate_buffers")

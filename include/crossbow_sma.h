@@ -488,6 +488,23 @@ int cbx_sma_plan_step (cbx_sma_plan *plan, void *const *streams, float *const *z
  * Nesterov momentum stays the caller's err() (sma.cu:46-48).             */
 int cbx_sma_optimise_buffers (void *stream, float *w, float *g, float *last, float *s, long long elements,
                               float learning_rate, float momentum, float weight_decay);
+/* The same seam for update model WORKER (synchronous SGD):
+ * crossbowSynchronisationSynchronousSGD (synch/synchronoussgd.c:13-106) ->
+ * cbx_ssgd_plan_step, over acc[k] = baseModels[k]->gradient->dev (the
+ * accumulated lr-scaled task gradients; reset to 0 by the step), z, last
+ * (used iff momentum > 0: the base model's conf->momentum, NOT forced to
+ * 0.9), the locked replicas from `first` on (set to their device's new base
+ * model, common.c:198-220) and wpc = defaultBaseModel->wpc (D *= 1/wpc).
+ * Buckets as cbx_sma_plan_set_buckets sets them.
+ * crossbowKernelOptimiserSynchronousSGD (kernels/optimisers/synchronoussgd.cu:
+ * 3-56) -> cbx_ssgd_accumulate_buffers: g += weight_decay * w, then
+ * acc += -learning_rate * g, on `stream` = the device's model-synchronisation
+ * stream once it has waited for the task's gradient (:37-40).            */
+int cbx_ssgd_plan_step (cbx_sma_plan *plan, void *const *streams, float *const *z, float *const *last,
+                        float *const *acc, int nreplicas, const int *replica_device, float *const *w,
+                        const int *locked, float momentum, int wpc, int first);
+int cbx_ssgd_accumulate_buffers (void *stream, const float *w, float *g, float *acc, long long elements,
+                                 float learning_rate, float weight_decay);
 
 #ifdef __cplusplus
 }

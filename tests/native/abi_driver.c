@@ -302,6 +302,13 @@ int main (void) {
 		EXPECT (cbx_sma_plan_step (plan, streams, zz, ll, 2, rdev, ww, ss, locked, copy, 0.1f, 0.9f, 1) == 0);
 		EXPECT (cbx_sma_plan_step (plan, streams, zz, ll, 2, rdev, ww, ss, locked, copy, 0.1f, 0.9f, 3) == CBX_ERR_INVALID);
 		EXPECT (cbx_sma_plan_step (plan, streams, zz, NULL, 2, rdev, ww, ss, locked, copy, 0.1f, 0.9f, 0) == CBX_ERR_INVALID);
+		/* the S-SGD seam: a task step into the base gradient, then the barrier */
+		void *acc = NULL;
+		CHECK (cbx_base_buffer (c, 0, CBX_BUF_GRADIENT, &acc));
+		float *aa[1] = { (float *) acc };
+		CHECK (cbx_ssgd_accumulate_buffers (NULL, (const float *) w0, (float *) g, (float *) acc, m, 0.05f, 1e-4f));
+		CHECK (cbx_ssgd_plan_step (plan, streams, zz, ll, aa, 2, rdev, ww, locked, 0.9f, 4, 0));
+		EXPECT (cbx_ssgd_plan_step (plan, streams, zz, ll, aa, 2, rdev, ww, locked, 0.9f, 0, 0) == CBX_ERR_INVALID);
 		CHECK (cbx_sma_plan_free (plan));
 		CHECK (cbx_replica_read (c, 0, CBX_BUF_DATA, host, (size_t) 4 * n));
 		EXPECT (all_finite (host, (size_t) m));

@@ -145,6 +145,54 @@ def test_seam_optimise_bitexact(n, mom, wd):
     assert _bits_equal(last.cpu().numpy(), l0), "last"
 
 
+@pytest.mark.parametrize("n,R,mom,wd,buckets", [(4099, 3, 0.9, 1e-4, 0), (300_007, 2, 0.0, 0.0, 0),
+                                                 (1, 1, 0.9, 1e-4, 0)])
+def test_seam_ssgd_one_gpu_bitexact(n, R, mom, wd, buckets):
+    """Synchronous SGD through the seam: task steps (cbx_ssgd_accumulate_buffers)
+    into the caller's base gradient, then the barrier (cbx_ssgd_plan_step),
+    two clocks, against the oracle's synchronoussgd.cu / .c restatement."""
+    import torch
+
+    from crossbow_amd.seam import SmaPlan, ssgd_accumulate_buffers
+    from oracle import oracle as O
+    lr, wpc = 0.05, 2 * R
+    st = O.make_state(n, 1, R, ALPHA, mom)
+    acc0 = np.zeros(n, np.float32)
+    dev = torch.device("cuda:0")
+    z = torch.from_numpy(st.z[0].copy()).to(dev)
+    last = torch.from_numpy(st.last[0].copy()).to(dev) if mom > 0 else None
+    w = [torch.from_numpy(a.copy()).to(dev) for a in st.w]
+    acc = torch.zeros(n, device=dev)
+    stream = torch.cuda.Stream()
+    torch.cuda.synchronize()
+    task = 0
+    with SmaPlan([0], n, buckets=buckets) as plan:
+        for clock in range(2):
+            for k in range(wpc):
+                i = k % R
+                g0 = O.fill_normal(n, 9000 + task, 0.01)
+                g = torch.from_numpy(g0.copy()).to(dev)
+                torch.cuda.synchronize()
+                ssgd_accumulate_buffers(stream.cuda_stream, w[i].data_ptr(), g.data_ptr(), acc.data_ptr(), n, lr, wd)
+                O.ssgd_worker(np.float32(-lr), wd, st.w[i], g0, acc0)
+                stream.synchronize()
+                assert _bits_equal(g.cpu().numpy(), g0), f"task {task}: g"
+                task += 1
+            st.locked[:] = 1
+            if clock == 1:
+                st.locked[0] = 0  # a held replica keeps its weights (common.c:208)
+            plan.ssgd_step([stream.cuda_stream], [z.data_ptr()], [last.data_ptr()] if last is not None else None,
+                           [acc.data_ptr()], [(0, w[i].data_ptr(), int(st.locked[i])) for i in range(R)], mom, wpc)
+            O.ssgd_sync(st, [acc0], wpc)
+        stream.synchronize()
+    assert _bits_equal(z.cpu().numpy(), st.z[0]), "z"
+    if last is not None:
+        assert _bits_equal(last.cpu().numpy(), st.last[0]), "last"
+    assert _bits_equal(acc.cpu().numpy(), acc0), "acc must be reset"
+    for i in range(R):
+        assert _bits_equal(w[i].cpu().numpy(), st.w[i]), f"w[{i}]"
+
+
 def test_seam_refuses_bad_arguments():
     import torch
 
@@ -275,6 +323,63 @@ def _run_devices(L, world, local, n, R, mom, steps, copy_at, held, exact, comms=
         mem.free()
 
 
+def _run_ssgd_devices(L, world, local, n, R, mom, steps, exact, comms=None, buckets=0):
+    """S-SGD through the seam over `local` devices of a G = world job: each
+    process runs its replicas' tasks into its devices' accumulators, then the
+    barrier.  Returns (bad, digest of z / last per device, differing elements)."""
+    seam = _seam_standalone()
+    O = C.oracle()
+    lr, wd, wpc = 0.05, 1e-4, 2 * world * R
+    st = O.make_state(n, world, R, ALPHA, mom)
+    size = world * R
+    mem = _Dev()
+    z = {d: mem.upload(st.z[d]) for d in local}
+    last = {d: mem.upload(st.last[d]) for d in local} if mom > 0 else None
+    w = {i: mem.upload(st.w[i]) for i in range(size) if i % world in local}
+    zeros = np.zeros(n, np.float32)
+    acc = {d: mem.upload(zeros) for d in local}
+    acc_ref = [zeros.copy() for _ in range(world)]
+    gbuf = mem.upload(zeros)
+    streams = [mem.stream() for _ in local]
+    pos = {d: k for k, d in enumerate(local)}
+    plan = seam.SmaPlan([0] * len(local), n, comms=comms, lib=L, buckets=buckets)
+    try:
+        task = 0
+        for step in range(steps):
+            for k in range(wpc):  # the global task list; each process runs its replicas' tasks
+                i = k % size
+                g0 = O.fill_normal(n, 5000 + task, 0.01)
+                if i in w:
+                    mem.sync()
+                    assert mem.hip.hipMemcpy(gbuf, g0.ctypes.data, g0.nbytes, 1) == 0
+                    seam.ssgd_accumulate_buffers(streams[pos[i % world]], w[i], gbuf, acc[i % world], n, lr, wd, lib=L)
+                    mem.sync()
+                O.ssgd_worker(np.float32(-lr), wd, st.w[i], g0, acc_ref[i % world])
+                task += 1
+            st.locked[:] = 1
+            reps = [(pos[i % world], w[i], 1) if i in w else (0, 0, 0) for i in range(size)]
+            plan.ssgd_step(streams, [z[d] for d in local], [last[d] for d in local] if last else None,
+                           [acc[d] for d in local], reps, mom, wpc)
+            O.ssgd_sync(st, acc_ref, wpc)
+        mem.sync()
+        check = C.Checker(exact=exact)
+        dig = {}
+        for d in local:
+            zd = mem.download(z[d], n)
+            ld = mem.download(last[d], n) if last else np.zeros(0, np.float32)
+            dig[d] = C.digest(zd, ld)
+            check(f"ssgd z[{d}]", zd, st.z[d])
+            if last:
+                check(f"ssgd last[{d}]", ld, st.last[d])
+            check(f"ssgd acc[{d}] reset", mem.download(acc[d], n), zeros)
+        for i in w:
+            check(f"ssgd w[{i}]", mem.download(w[i], n), st.w[i])
+        return check.bad, dig, check.differs
+    finally:
+        plan.free()
+        mem.free()
+
+
 DEVICE_CASES = [
     # (name, n, R, momentum, steps, {step: copy replica}, {step: held replicas}, first, order, caller comms,
     #  buckets: 0 = the default pipeline of 8, 1 = in order on the caller's stream)
@@ -311,6 +416,11 @@ def _device_worker(G, q):
                 for c in comms or ():
                     F.ncclCommDestroy(ctypes.c_void_p(c))
             out.append((name, order, bad, len(set(dig.values())), differs))
+        for name, buckets in (("ssgd", 0), ("ssgd-in-order", 1)):
+            os.environ["FAKE_RCCL_ORDER"] = "rank"
+            bad, dig, differs = _run_ssgd_devices(L, G, list(range(G)), 40_009, 2, 0.9, 2, exact=True,
+                                                  buckets=buckets)
+            out.append((name, "rank", bad, len(set(dig.values())), differs))
         q.put((out, None))
     except Exception:  # pragma: no cover - reported to the parent
         import traceback
@@ -350,7 +460,7 @@ class _Uid(ctypes.Structure):
     _fields_ = [("internal", ctypes.c_char * 128)]
 
 
-def _rank_worker(world, rank, d, buckets, q):
+def _rank_worker(world, rank, d, buckets, kind, q):
     try:
         from tests.test_gpu_realrccl import load_real, rank_env
         rank_env(rank)
@@ -369,8 +479,12 @@ def _rank_worker(world, rank, d, buckets, q):
         R.ncclCommInitRank.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_int, _Uid, ctypes.c_int]
         assert R.ncclCommInitRank(ctypes.byref(comm), world, uid, rank) == 0
         try:
-            bad, dig, differs = _run_devices(L, world, [rank], 200_003, 2, 0.9, 3, {1: (world - 1) * 2 + 1},
-                                             {2: (0,)}, exact=world == 2, comms=[comm.value], buckets=buckets)
+            if kind == "ssgd":
+                bad, dig, differs = _run_ssgd_devices(L, world, [rank], 100_003, 2, 0.9, 2, exact=world == 2,
+                                                      comms=[comm.value], buckets=buckets)
+            else:
+                bad, dig, differs = _run_devices(L, world, [rank], 200_003, 2, 0.9, 3, {1: (world - 1) * 2 + 1},
+                                                 {2: (0,)}, exact=world == 2, comms=[comm.value], buckets=buckets)
         finally:
             R.ncclCommDestroy(comm)
         q.put(((bad, dig[rank], differs), None))
@@ -379,15 +493,16 @@ def _rank_worker(world, rank, d, buckets, q):
         q.put((None, traceback.format_exc()))
 
 
-@pytest.mark.parametrize("world,buckets", [(2, 0), (2, 1), (4, 0), (4, 5)])
-def test_seam_real_rccl_ranks(world, buckets):
+@pytest.mark.parametrize("world,buckets,kind", [(2, 0, "sma"), (2, 1, "sma"), (4, 0, "sma"), (4, 5, "sma"),
+                                                (2, 0, "ssgd"), (4, 0, "ssgd")])
+def test_seam_real_rccl_ranks(world, buckets, kind):
     import multiprocessing as mp
     ctx = mp.get_context("spawn")
     with tempfile.TemporaryDirectory() as d:
         qs, ps = [], []
         for rank in range(world):
             q = ctx.Queue()
-            p = ctx.Process(target=_rank_worker, args=(world, rank, d, buckets, q))
+            p = ctx.Process(target=_rank_worker, args=(world, rank, d, buckets, kind, q))
             p.start()
             qs.append(q)
             ps.append(p)
