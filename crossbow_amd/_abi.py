@@ -146,6 +146,7 @@ SIGNATURES = {
     "cbx_sma_plan_set_buckets": (_I, [_P, _I]),
     "cbx_sma_plan_step": (_I, [_P, _PP, _PP, _PP, _I, _IP, _PP, _PP, _IP, _IP, _F, _F, _I]),
     "cbx_sma_optimise_buffers": (_I, [_P, _P, _P, _P, _P, _c.c_longlong, _F, _F, _F]),
+    "cbx_sma_plan_average_batchnorm": (_I, [_P, _I, _IP, _PP, _PP, _IP]),
     "cbx_ssgd_plan_step": (_I, [_P, _PP, _PP, _PP, _PP, _I, _IP, _PP, _IP, _F, _I, _I]),
     "cbx_ssgd_accumulate_buffers": (_I, [_P, _P, _P, _P, _c.c_longlong, _F, _F]),
 }

@@ -936,7 +936,11 @@ static int replica_optimise_impl(cbx_context *c, int id, int task, void *stream)
 }
 
 // ---- batch-norm running statistics (cudnn/cudnnbatchnormparams.c:157-222) --
-static int grow(void **p, size_t *have, size_t need) {
+}  // extern "C"
+
+namespace cbx::host {
+
+int grow_device_buffer(void **p, size_t *have, size_t need) {
   if (*have >= need) return CBX_OK;
   if (*p) HIP_TRY(hipFree(*p));
   *p = nullptr;
@@ -945,6 +949,60 @@ static int grow(void **p, size_t *have, size_t need) {
   *have = need;
   return CBX_OK;
 }
+
+// crossbowCudnnBatchNormParamsSynchroniseEstimatedMeanAndVariable
+// (cudnn/cudnnbatchnormparams.c:157-222) over `devs`: every layer's mean and
+// variance packed into one scratch buffer per device (with a count slot per
+// layer), one all-reduce, unpacked with the 1/count scale.
+int bn_average(std::vector<BnDevice> &devs, int layers, const int *elements, float *const *mean,
+               float *const *variance, const int *updated) {
+  uint32_t maxlen = 0;
+  size_t total = 0;
+  for (int l = 0; l < layers; ++l) {
+    if (elements[l] < 0) return fail(CBX_ERR_INVALID, "layer %d has %d elements", l, elements[l]);
+    maxlen = std::max(maxlen, (uint32_t)elements[l]);
+    total += (size_t)elements[l];
+  }
+  const size_t head = ((size_t)layers + 63) / 64 * 64;  // count slots, one per layer
+  const size_t floats = head + 2 * total;
+  const int nseg = 2 * layers;
+  std::vector<cbx::BnSegment> segs(nseg);
+  for (size_t k = 0; k < devs.size(); ++k) {
+    BnDevice &d = devs[k];
+    HIP_TRY(hipSetDevice(d.hip_id));
+    size_t off = head;
+    for (int l = 0; l < layers; ++l) {
+      const size_t j = k * (size_t)layers + l;
+      if (!mean[j] || !variance[j]) return fail(CBX_ERR_INVALID, "null statistics buffer (device %zu, layer %d)", k, l);
+      // :175: the default device (global 0) always counts, the others iff updated.
+      const float scale = (d.global == 0 || updated[j]) ? 1.0f : 0.0f;
+      segs[2 * l] = {mean[j], (uint32_t)elements[l], (uint32_t)off, (uint32_t)l, scale};
+      segs[2 * l + 1] = {variance[j], (uint32_t)elements[l], (uint32_t)(off + elements[l]), (uint32_t)l, scale};
+      off += 2 * (size_t)elements[l];
+    }
+    TRY(grow_device_buffer(reinterpret_cast<void **>(d.table), d.table_bytes, segs.size() * sizeof(cbx::BnSegment)));
+    TRY(grow_device_buffer(reinterpret_cast<void **>(d.scratch), d.scratch_bytes, floats * sizeof(float)));
+    HIP_TRY(hipDeviceSynchronize());  // :171 (producers on any stream are done)
+    HIP_TRY(hipMemcpy(*d.table, segs.data(), segs.size() * sizeof(cbx::BnSegment), hipMemcpyHostToDevice));
+    HIP_TRY(cbx::launch_bn_pack(*d.table, nseg, maxlen, *d.scratch, d.stream));
+  }
+  NCCL_TRY(ncclGroupStart());
+  for (BnDevice &d : devs) {
+    HIP_TRY(hipSetDevice(d.hip_id));
+    NCCL_TRY(ncclAllReduce(*d.scratch, *d.scratch, floats, ncclFloat, ncclSum, d.comm, d.stream));
+  }
+  NCCL_TRY(ncclGroupEnd());
+  for (BnDevice &d : devs) {
+    HIP_TRY(hipSetDevice(d.hip_id));
+    HIP_TRY(cbx::launch_bn_unpack(*d.table, nseg, maxlen, *d.scratch, d.stream));
+    HIP_TRY(hipStreamSynchronize(d.stream));  // :218
+  }
+  return CBX_OK;
+}
+
+}  // namespace cbx::host
+
+extern "C" {
 
 int cbx_average_batchnorm_stats(cbx_context *c, int layers, const int *elements, float *const *mean,
                                 float *const *variance, const int *updated) {
@@ -962,48 +1020,10 @@ int cbx_average_batchnorm_stats(cbx_context *c, int layers, const int *elements,
     int dev = d.hip_id;
     NCCL_TRY(ncclCommInitAll(&d.comm, 1, &dev));
   }
-  uint32_t maxlen = 0;
-  size_t total = 0;
-  for (int l = 0; l < layers; ++l) {
-    if (elements[l] < 0) return fail(CBX_ERR_INVALID, "layer %d has %d elements", l, elements[l]);
-    maxlen = std::max(maxlen, (uint32_t)elements[l]);
-    total += (size_t)elements[l];
-  }
-  const size_t head = ((size_t)layers + 63) / 64 * 64;  // count slots, one per layer
-  const size_t floats = head + 2 * total;
-  const int nseg = 2 * layers;
-  std::vector<cbx::BnSegment> segs(nseg);
-  for (size_t k = 0; k < c->devs.size(); ++k) {
-    Device &d = c->devs[k];
-    HIP_TRY(hipSetDevice(d.hip_id));
-    size_t off = head;
-    for (int l = 0; l < layers; ++l) {
-      const size_t j = k * (size_t)layers + l;
-      if (!mean[j] || !variance[j]) return fail(CBX_ERR_INVALID, "null statistics buffer (device %zu, layer %d)", k, l);
-      // :175: the default device (global 0) always counts, the others iff updated.
-      const float scale = (d.g == 0 || updated[j]) ? 1.0f : 0.0f;
-      segs[2 * l] = {mean[j], (uint32_t)elements[l], (uint32_t)off, (uint32_t)l, scale};
-      segs[2 * l + 1] = {variance[j], (uint32_t)elements[l], (uint32_t)(off + elements[l]), (uint32_t)l, scale};
-      off += 2 * (size_t)elements[l];
-    }
-    TRY(grow(reinterpret_cast<void **>(&d.bn_table), &d.bn_table_bytes, segs.size() * sizeof(cbx::BnSegment)));
-    TRY(grow(reinterpret_cast<void **>(&d.bn_scratch), &d.bn_scratch_bytes, floats * sizeof(float)));
-    HIP_TRY(hipDeviceSynchronize());  // :171 (producers on any stream are done)
-    HIP_TRY(hipMemcpy(d.bn_table, segs.data(), segs.size() * sizeof(cbx::BnSegment), hipMemcpyHostToDevice));
-    HIP_TRY(cbx::launch_bn_pack(d.bn_table, nseg, maxlen, d.bn_scratch, d.stream));
-  }
-  NCCL_TRY(ncclGroupStart());
-  for (Device &d : c->devs) {
-    HIP_TRY(hipSetDevice(d.hip_id));
-    NCCL_TRY(ncclAllReduce(d.bn_scratch, d.bn_scratch, floats, ncclFloat, ncclSum, d.comm, d.stream));
-  }
-  NCCL_TRY(ncclGroupEnd());
-  for (Device &d : c->devs) {
-    HIP_TRY(hipSetDevice(d.hip_id));
-    HIP_TRY(cbx::launch_bn_unpack(d.bn_table, nseg, maxlen, d.bn_scratch, d.stream));
-    HIP_TRY(hipStreamSynchronize(d.stream));  // :218
-  }
-  return CBX_OK;
+  std::vector<BnDevice> devs;
+  for (Device &d : c->devs)
+    devs.push_back({d.hip_id, d.g, d.comm, d.stream, &d.bn_table, &d.bn_table_bytes, &d.bn_scratch, &d.bn_scratch_bytes});
+  return bn_average(devs, layers, elements, mean, variance, updated);
 }
 
 // ---- task-side replica access ---------------------------------------------

@@ -646,6 +646,24 @@ inline int ring_span(Device &d, int slot, int a, int b, float *out) {
   return CBX_OK;
 }
 
+// ---- batch-norm running-statistics averaging (context.hip) ------------------
+// One device of an averaging: its HIP id, global index (0 = the default
+// device, which always counts), communicator, stream, and the segment table
+// and packed scratch it grows on demand.
+struct BnDevice {
+  int hip_id;
+  int global;
+  ncclComm_t comm;
+  hipStream_t stream;
+  cbx::BnSegment **table;
+  size_t *table_bytes;
+  float **scratch;
+  size_t *scratch_bytes;
+};
+int bn_average(std::vector<BnDevice> &devs, int layers, const int *elements, float *const *mean,
+               float *const *variance, const int *updated);
+int grow_device_buffer(void **p, size_t *have, size_t need);
+
 // ---- the barrier steps (sync_steps.hip) ------------------------------------
 // The same arguments over float4s [start4, start4 + len4) of every buffer.
 cbx::SmaArgs offset_args(const cbx::SmaArgs &a, int64_t start4, int64_t len4);

@@ -60,6 +60,12 @@ struct cbx_sma_plan {
     // kernel A of the next bucket; per bucket, kernel A done / all-reduce done.
     hipStream_t comm_stream = nullptr;
     std::vector<hipEvent_t> ev_a, ev_r;
+    int global = 0;  // rank in the communicator (0: the default device)
+    // Batch-norm statistics averaging: segment table and packed scratch.
+    cbx::BnSegment *bn_table = nullptr;
+    size_t bn_table_bytes = 0;
+    float *bn_scratch = nullptr;
+    size_t bn_scratch_bytes = 0;
   };
   std::vector<Dev> devs;
   int64_t n = 0;
@@ -99,6 +105,8 @@ int cbx_sma_plan_free(cbx_sma_plan *p) {
     (void)hipDeviceSynchronize();
     if (d.own_comm && d.comm) (void)ncclCommDestroy(d.comm);
     if (d.scratch) (void)hipFree(d.scratch);
+    if (d.bn_table) (void)hipFree(d.bn_table);
+    if (d.bn_scratch) (void)hipFree(d.bn_scratch);
     for (hipEvent_t e : d.ev_a) (void)hipEventDestroy(e);
     for (hipEvent_t e : d.ev_r) (void)hipEventDestroy(e);
     if (d.comm_stream) (void)hipStreamDestroy(d.comm_stream);
@@ -150,9 +158,10 @@ int cbx_sma_plan_create(cbx_sma_plan **out, const int *devices, int ndevices, lo
     }
     int count = 0;
     ncclResult_t r = ncclCommCount(p->devs[0].comm, &count);
+    for (int k = 0; r == ncclSuccess && k < ndevices; ++k) r = ncclCommUserRank(p->devs[k].comm, &p->devs[k].global);
     if (r != ncclSuccess) {
       cbx_sma_plan_free(p);
-      return fail(CBX_ERR_RCCL, "ncclCommCount: %s", ncclGetErrorString(r));
+      return fail(CBX_ERR_RCCL, "ncclCommCount / ncclCommUserRank: %s", ncclGetErrorString(r));
     }
     p->ranks = count;
   } else if (ndevices > 1) {
@@ -166,6 +175,7 @@ int cbx_sma_plan_create(cbx_sma_plan **out, const int *devices, int ndevices, lo
     for (int k = 0; k < ndevices; ++k) {
       p->devs[k].comm = cs[k];
       p->devs[k].own_comm = true;
+      p->devs[k].global = k;
     }
     p->ranks = ndevices;
   }
@@ -454,6 +464,25 @@ int cbx_ssgd_accumulate_buffers(void *stream, const float *w, float *g, float *a
   cfg.num_cus = cus;
   HIP_TRY(cbx::launch_ssgd_accumulate(a, cfg, static_cast<hipStream_t>(stream)));
   return CBX_OK;
+}
+
+// crossbowCudnnBatchNormParamsSynchroniseEstimatedMeanAndVariable
+// (cudnn/cudnnbatchnormparams.c:157-222) over the caller's statistics buffers,
+// the same packed all-reduce as cbx_average_batchnorm_stats, on the plan's
+// stream; device-synchronises before and after, as the reference does.
+int cbx_sma_plan_average_batchnorm(cbx_sma_plan *p, int layers, const int *elements, float *const *mean,
+                                   float *const *variance, const int *updated) {
+  TraceRange trace("cbx_sma_plan_average_batchnorm");
+  if (!p) return fail(CBX_ERR_INVALID, "null plan");
+  if (layers < 0 || (layers > 0 && (!elements || !mean || !variance || !updated)))
+    return fail(CBX_ERR_INVALID, "bad batch-norm statistics arguments");
+  if (layers == 0 || p->ranks == 1) return CBX_OK;  // :165-166: nothing to average with one device
+  TRY(ensure_pipeline(p, 1));
+  std::vector<BnDevice> devs;
+  for (auto &d : p->devs)
+    devs.push_back({d.hip_id, d.global, d.comm, d.comm_stream, &d.bn_table, &d.bn_table_bytes, &d.bn_scratch,
+                    &d.bn_scratch_bytes});
+  return bn_average(devs, layers, elements, mean, variance, updated);
 }
 
 int cbx_sma_plan_set_buckets(cbx_sma_plan *p, int buckets) {

@@ -84,6 +84,14 @@ class SmaPlan:
             len(replicas), _ints([r[0] for r in replicas]), _ptrs([r[1] for r in replicas]),
             _ints([r[2] for r in replicas]), ctypes.c_float(momentum), wpc, first), "cbx_ssgd_plan_step")
 
+    def average_batchnorm(self, elements: Sequence[int], mean: Sequence[int], variance: Sequence[int],
+                          updated: Sequence[int]) -> None:
+        """BN running-statistics averaging; ``mean``/``variance``/``updated`` are
+        indexed [k * layers + l] (k: position in the plan's devices)."""
+        _raise(self.lib, self.lib.cbx_sma_plan_average_batchnorm(
+            self._p, len(elements), _ints(elements), _ptrs(mean), _ptrs(variance), _ints(updated)),
+            "cbx_sma_plan_average_batchnorm")
+
     def set_buckets(self, buckets: int) -> None:
         """G > 1: buckets of the all-reduce pipeline (0 = default 8, 1 = in order)."""
         _raise(self.lib, self.lib.cbx_sma_plan_set_buckets(self._p, buckets), "cbx_sma_plan_set_buckets")

@@ -500,6 +500,13 @@ int cbx_sma_optimise_buffers (void *stream, float *w, float *g, float *last, flo
  * 3-56) -> cbx_ssgd_accumulate_buffers: g += weight_decay * w, then
  * acc += -learning_rate * g, on `stream` = the device's model-synchronisation
  * stream once it has waited for the task's gradient (:37-40).            */
+/* crossbowCudnnBatchNormParamsSynchroniseEstimatedMeanAndVariable
+ * (cudnn/cudnnbatchnormparams.c:157-222) over the caller's statistics
+ * buffers: arguments as cbx_average_batchnorm_stats, with k the position in
+ * the plan's devices (the default device is rank 0 of the communicator).
+ * No-op with one rank.  Device-synchronises before and after.             */
+int cbx_sma_plan_average_batchnorm (cbx_sma_plan *plan, int layers, const int *elements, float *const *mean,
+                                    float *const *variance, const int *updated);
 int cbx_ssgd_plan_step (cbx_sma_plan *plan, void *const *streams, float *const *z, float *const *last,
                         float *const *acc, int nreplicas, const int *replica_device, float *const *w,
                         const int *locked, float momentum, int wpc, int first);

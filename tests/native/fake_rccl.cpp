@@ -299,6 +299,12 @@ ncclResult_t ncclCommCount(const ncclComm_t comm, int *count) {
   return ncclSuccess;
 }
 
+ncclResult_t ncclCommUserRank(const ncclComm_t comm, int *rank) {
+  if (!comm || !rank) return ncclInvalidArgument;
+  *rank = comm->rank;
+  return ncclSuccess;
+}
+
 ncclResult_t ncclCommDestroy(ncclComm_t comm) {
   if (!comm) return ncclInvalidArgument;
   Clique *q = comm->clique;

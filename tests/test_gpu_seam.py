@@ -380,6 +380,46 @@ def _run_ssgd_devices(L, world, local, n, R, mom, steps, exact, comms=None, buck
         mem.free()
 
 
+def _run_bn_plan(L, world, local, exact, comms=None):
+    """BN running-statistics averaging through the plan
+    (cbx_sma_plan_average_batchnorm) over the caller's buffers: three layers,
+    non-counting devices poisoned with NaN / +-Inf (the reference never reads
+    them, cudnnbatchnormparams.c:177-184).  Returns the list of mismatches."""
+    seam = _seam_standalone()
+    O = C.oracle()
+    elements = [16, 40, 7]
+    updated = [[1, 1, 1]] + [[1, 0, 1] if d % 2 else [0, 1, 1] for d in range(1, world)]
+    mean = [[O.fill_normal(e, 50 + 10 * d + l, 0.5) for l, e in enumerate(elements)] for d in range(world)]
+    var = [[O.fill_normal(e, 90 + 10 * d + l, 0.5) for l, e in enumerate(elements)] for d in range(world)]
+    for d in range(1, world):
+        for l in range(len(elements)):
+            if not updated[d][l]:
+                mean[d][l][:] = np.nan
+                var[d][l][::2] = np.inf
+                var[d][l][1::2] = -np.inf
+    ref_m = [[a.copy() for a in r] for r in mean]
+    ref_v = [[a.copy() for a in r] for r in var]
+    O.bn_average(ref_m, ref_v, updated)
+    mem = _Dev()
+    pm = {(d, l): mem.upload(mean[d][l]) for d in local for l in range(len(elements))}
+    pv = {(d, l): mem.upload(var[d][l]) for d in local for l in range(len(elements))}
+    plan = seam.SmaPlan([0] * len(local), 4096, comms=comms, lib=L)
+    try:
+        L3 = len(elements)
+        plan.average_batchnorm(elements, [pm[(d, l)] for d in local for l in range(L3)],
+                               [pv[(d, l)] for d in local for l in range(L3)],
+                               [updated[d][l] for d in local for l in range(L3)])
+        check = C.Checker(exact=exact)
+        for d in local:
+            for l, e in enumerate(elements):
+                check(f"bn mean[{l}] on device {d}", mem.download(pm[(d, l)], e), ref_m[d][l])
+                check(f"bn var[{l}] on device {d}", mem.download(pv[(d, l)], e), ref_v[d][l])
+        return check.bad
+    finally:
+        plan.free()
+        mem.free()
+
+
 DEVICE_CASES = [
     # (name, n, R, momentum, steps, {step: copy replica}, {step: held replicas}, first, order, caller comms,
     #  buckets: 0 = the default pipeline of 8, 1 = in order on the caller's stream)
@@ -421,6 +461,7 @@ def _device_worker(G, q):
             bad, dig, differs = _run_ssgd_devices(L, G, list(range(G)), 40_009, 2, 0.9, 2, exact=True,
                                                   buckets=buckets)
             out.append((name, "rank", bad, len(set(dig.values())), differs))
+        out.append(("bn", "rank", _run_bn_plan(L, G, list(range(G)), exact=True), 1, 0))
         q.put((out, None))
     except Exception:  # pragma: no cover - reported to the parent
         import traceback
@@ -479,7 +520,9 @@ def _rank_worker(world, rank, d, buckets, kind, q):
         R.ncclCommInitRank.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_int, _Uid, ctypes.c_int]
         assert R.ncclCommInitRank(ctypes.byref(comm), world, uid, rank) == 0
         try:
-            if kind == "ssgd":
+            if kind == "bn":
+                bad, dig, differs = _run_bn_plan(L, world, [rank], exact=world == 2, comms=[comm.value]), "bn", 0
+            elif kind == "ssgd":
                 bad, dig, differs = _run_ssgd_devices(L, world, [rank], 100_003, 2, 0.9, 2, exact=world == 2,
                                                       comms=[comm.value], buckets=buckets)
             else:
@@ -487,14 +530,14 @@ def _rank_worker(world, rank, d, buckets, kind, q):
                                                  {2: (0,)}, exact=world == 2, comms=[comm.value], buckets=buckets)
         finally:
             R.ncclCommDestroy(comm)
-        q.put(((bad, dig[rank], differs), None))
+        q.put(((bad, dig if kind == "bn" else dig[rank], differs), None))
     except Exception:  # pragma: no cover - reported to the parent
         import traceback
         q.put((None, traceback.format_exc()))
 
 
 @pytest.mark.parametrize("world,buckets,kind", [(2, 0, "sma"), (2, 1, "sma"), (4, 0, "sma"), (4, 5, "sma"),
-                                                (2, 0, "ssgd"), (4, 0, "ssgd")])
+                                                (2, 0, "ssgd"), (4, 0, "ssgd"), (4, 0, "bn")])
 def test_seam_real_rccl_ranks(world, buckets, kind):
     import multiprocessing as mp
     ctx = mp.get_context("spawn")
