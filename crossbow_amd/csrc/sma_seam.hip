@@ -1,9 +1,13 @@
-// sma_seam.hip -- the SMA step and the replica optimiser step over buffers the
-// CALLER owns: the seam at crossbowSynchronisationSMA (clib-multigpu/synch/
-// sma.c:233-248 -> :13-231) and at crossbowKernelOptimiserSMA
-// (kernels/optimisers/sma.cu:3-100) for a Crossbow build that keeps its own
-// model manager, model buffers and task side (modelmanager.c, model.c,
-// executioncontext.c) and replaces only those two function bodies.
+// sma_seam.hip -- the synchronisation steps over buffers the CALLER owns, for
+// a Crossbow build that keeps its own model manager, model buffers and task
+// side (modelmanager.c, model.c, executioncontext.c) and replaces only these
+// function bodies:
+//   crossbowSynchronisationSMA (clib-multigpu/synch/sma.c:233-248 -> :13-231)
+//   crossbowKernelOptimiserSMA (kernels/optimisers/sma.cu:3-100)
+//   crossbowSynchronisationSynchronousSGD (synch/synchronoussgd.c:13-106)
+//   crossbowKernelOptimiserSynchronousSGD (kernels/optimisers/synchronoussgd.cu:3-56)
+//   crossbowCudnnBatchNormParamsSynchroniseEstimatedMeanAndVariable
+//     (cudnn/cudnnbatchnormparams.c:157-222)
 //
 // The context API (context.hip) owns an arena whose buffers are padded to
 // whole kernel trips; the reference's buffers hold exactly `elements` floats.
