@@ -91,6 +91,39 @@ def test_seam_one_gpu_bitexact(name, n, R, mom, steps, first, held, copy_at):
         assert _bits_equal(s[i].cpu().numpy(), st.s[i]), f"s[{i}] must be untouched"
 
 
+def _golden(G):
+    from tests.test_oracle import load_golden_cases
+    return [c for c in load_golden_cases() if c["G"] == G]
+
+
+@pytest.mark.parametrize("gcase", _golden(1), ids=lambda c: c["name"])
+def test_seam_golden_fixtures_one_gpu(gcase):
+    """The committed fixtures (tests/golden/, the oracle's outputs) through the
+    seam on caller-owned buffers: one step, bit for bit."""
+    import torch
+
+    from crossbow_amd.seam import SmaPlan
+    st = gcase["state"]
+    n = st.n
+    dev = torch.device("cuda:0")
+    z = torch.from_numpy(st.z[0].copy()).to(dev)
+    last = torch.from_numpy(st.last[0].copy()).to(dev) if st.last is not None else None
+    s_ = [torch.from_numpy(a.copy()).to(dev) for a in st.s]
+    w = [torch.from_numpy(a.copy()).to(dev) for a in st.w]
+    stream = torch.cuda.Stream()
+    torch.cuda.synchronize()
+    with SmaPlan([0], n) as plan:
+        reps = [(0, w[i].data_ptr(), s_[i].data_ptr(), int(st.locked[i]), int(st.copy[i])) for i in range(st.size)]
+        plan.step([stream.cuda_stream], [z.data_ptr()], [last.data_ptr()] if last is not None else None, reps,
+                  st.alpha, st.momentum, st.first)
+        stream.synchronize()
+    assert _bits_equal(z.cpu().numpy(), gcase["z_out"][0]), "z"
+    if gcase["last_out"] is not None:
+        assert _bits_equal(last.cpu().numpy(), gcase["last_out"][0]), "last"
+    for i in range(st.size):
+        assert _bits_equal(w[i].cpu().numpy(), gcase["w_out"][i]), f"w[{i}]"
+
+
 def test_seam_resnet50_full_size_bitexact():
     """C3's buffers through the seam: n = 25,557,032 (not a multiple of the
     kernels' 4096-float trip: a 2,088-element tail), 8 replicas, mu 0.9."""
@@ -420,6 +453,40 @@ def _run_bn_plan(L, world, local, exact, comms=None):
         mem.free()
 
 
+def _run_golden_devices(L, world, local, gcase, comms=None):
+    """One committed G > 1 fixture through the seam over `local` devices, bit
+    for bit (rank-order loopback or G = 2).  Returns the list of mismatches."""
+    seam = _seam_standalone()
+    st = gcase["state"]
+    n, size = st.n, st.size
+    mem = _Dev()
+    z = {d: mem.upload(st.z[d]) for d in local}
+    last = {d: mem.upload(st.last[d]) for d in local} if st.last is not None else None
+    mine = [i for i in range(size) if i % world in local]
+    w = {i: mem.upload(st.w[i]) for i in mine}
+    s_ = {i: mem.upload(st.s[i]) for i in mine}
+    streams = [mem.stream() for _ in local]
+    pos = {d: k for k, d in enumerate(local)}
+    plan = seam.SmaPlan([0] * len(local), n, comms=comms, lib=L)
+    try:
+        reps = [(pos[i % world], w[i], s_[i], int(st.locked[i]), int(st.copy[i])) if i in w else (0, 0, 0, 0, 0)
+                for i in range(size)]
+        plan.step(streams, [z[d] for d in local], [last[d] for d in local] if last else None, reps, st.alpha,
+                  st.momentum, st.first)
+        mem.sync()
+        check = C.Checker(exact=True)
+        for d in local:
+            check(f"{gcase['name']} z[{d}]", mem.download(z[d], n), gcase["z_out"][d])
+            if last:
+                check(f"{gcase['name']} last[{d}]", mem.download(last[d], n), gcase["last_out"][d])
+        for i in mine:
+            check(f"{gcase['name']} w[{i}]", mem.download(w[i], n), gcase["w_out"][i])
+        return check.bad
+    finally:
+        plan.free()
+        mem.free()
+
+
 DEVICE_CASES = [
     # (name, n, R, momentum, steps, {step: copy replica}, {step: held replicas}, first, order, caller comms,
     #  buckets: 0 = the default pipeline of 8, 1 = in order on the caller's stream)
@@ -462,6 +529,9 @@ def _device_worker(G, q):
                                                   buckets=buckets)
             out.append((name, "rank", bad, len(set(dig.values())), differs))
         out.append(("bn", "rank", _run_bn_plan(L, G, list(range(G)), exact=True), 1, 0))
+        for gcase in C.golden_cases(G):
+            os.environ["FAKE_RCCL_ORDER"] = "rank"
+            out.append((f"golden {gcase['name']}", "rank", _run_golden_devices(L, G, list(range(G)), gcase), 1, 0))
         q.put((out, None))
     except Exception:  # pragma: no cover - reported to the parent
         import traceback
@@ -483,7 +553,7 @@ def _spawn(target, args, timeout=110):
 
 
 @pytest.mark.skipif(not os.path.exists(C.VARIANT), reason="run scripts/build_fake_rccl.sh first")
-@pytest.mark.parametrize("G", [2, 4])
+@pytest.mark.parametrize("G", [2, 4, 8])
 def test_seam_devices_one_process(G):
     res, err = _spawn(_device_worker, (G,))
     assert err is None, err
