@@ -77,6 +77,8 @@ def run(variant):
 
 def main():
     variants = ["separate", "staggered", "separate-no-tail", "staggered-no-tail"]
+    if len(sys.argv) > 1:  # --only V: one variant (e.g. under rocprofv3 --kernel-trace)
+        variants = [sys.argv[sys.argv.index("--only") + 1]]
     res = {v: [] for v in variants}
     for _ in range(ROUNDS):
         for v in variants:
