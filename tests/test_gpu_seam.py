@@ -632,3 +632,41 @@ def test_seam_real_rccl_ranks(world, buckets, kind):
     for rank, (bad, _, _) in enumerate(outs):
         assert not bad, (rank, bad)
     assert len({dg for _, dg, _ in outs}) == 1, "z / last differ across ranks"
+
+
+def test_seam_largest_model_windows_bitexact():
+    """The largest model the reference's `int bytes` allows (model.h:35):
+    n = 536,870,911 floats per caller-owned buffer, the tail's byte offsets
+    just below 2^31.  The step is elementwise, so dense windows (head, around
+    byte 2^30, the last whole trip and the tail) are checked against the
+    oracle run on the same windows, bit for bit."""
+    import torch
+
+    from crossbow_amd.seam import SmaPlan
+    from oracle import oracle as O
+    n, R, mom = (2**31 - 1) // 4, 2, 0.9
+    dev = torch.device("cuda:0")
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(7)
+    z = torch.randn(n, device=dev, generator=gen) * 0.05
+    last = torch.randn(n, device=dev, generator=gen) * 0.001
+    s = [z + 0.01 * torch.randn(n, device=dev, generator=gen) for _ in range(R)]
+    w = [si + 0.001 * torch.randn(n, device=dev, generator=gen) for si in s]
+    bulk = (n // 4) // 1024 * 1024 * 4
+    windows = [(0, 70_000), ((1 << 28) - 35_000, (1 << 28) + 35_000), (bulk - 40_000, n)]
+    before = [[t[a:b].cpu().numpy().copy() for t in [z, last] + s + w] for a, b in windows]
+    stream = torch.cuda.Stream()
+    torch.cuda.synchronize()
+    with SmaPlan([0], n) as plan:
+        plan.step([stream.cuda_stream], [z.data_ptr()], [last.data_ptr()],
+                  [(0, w[i].data_ptr(), s[i].data_ptr(), 1, 0) for i in range(R)], ALPHA, mom)
+        stream.synchronize()
+    for (a, b), arrs in zip(windows, before):
+        st = O.SmaState(1, R, b - a, ALPHA, mom, [arrs[0]], [arrs[1]], arrs[2:2 + R], arrs[2 + R:])
+        O.sma_step(st)
+        assert _bits_equal(z[a:b].cpu().numpy(), st.z[0]), f"z[{a}:{b}]"
+        assert _bits_equal(last[a:b].cpu().numpy(), st.last[0]), f"last[{a}:{b}]"
+        for i in range(R):
+            assert _bits_equal(w[i][a:b].cpu().numpy(), st.w[i]), f"w[{i}][{a}:{b}]"
+    del z, last, s, w
+    torch.cuda.empty_cache()
