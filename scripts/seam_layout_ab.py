@@ -1,8 +1,8 @@
 #!/usr/bin/env python3
 """Where the sma.c seam's step loses to the context's (bench.py field `seam`):
 the seam's buffers are the caller's (one allocation per buffer, each starting
-on a 2 MiB boundary) and a step is two launches (the whole-trip bulk + the
-scalar tail).  Interleaved A/B over C3 (ResNet-50, R = 8, mu 0.9):
+on a 2 MiB boundary) and a step covers a scalar tail (the elements past the
+last whole kernel trip) on extra workgroups.  Interleaved A/B over C3 (ResNet-50, R = 8, mu 0.9):
 
   separate       one torch allocation per buffer (as bench.py's seam leg)
   staggered      one allocation carved into buffers 2 MiB + 4 KiB apart
