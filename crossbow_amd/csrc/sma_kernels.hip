@@ -89,15 +89,33 @@ __device__ __forceinline__ void sma_tail_elem(const SmaArgs &a, bool copy) {
   float *last = reinterpret_cast<float *>(a.last);
   float D;
   float z0 = z[i];
+  float l0 = 0.0f;
+  if constexpr (MOM) l0 = last[i];
   if constexpr (PHASE == 2) {
     D = reinterpret_cast<const float *>(a.D)[i];
   } else {
+    // Replicas in chunks of kTailChunk whose loads are all issued before the
+    // chunk's first store (a store to w_r may alias any later load, so a
+    // plain loop pays one HBM round trip per replica).
+    constexpr int kTailChunk = 8;
     float acc = 0.0f;  // sma.c:66
-    for (int r = 0; r < a.nrep; ++r) {
-      float *w = reinterpret_cast<float *>(a.w[r]);
-      const float d = fmaf(-1.0f, z0, reinterpret_cast<const float *>(a.s[r])[i]);  // sma.c:79-90
-      w[i] = fmaf(-a.alpha, d, w[i]);                                                // :93-99
-      acc = fmaf(a.alpha, d, acc);                                                   // :102-107
+    for (int c = 0; c < a.nrep; c += kTailChunk) {
+      float sv[kTailChunk], wv[kTailChunk];
+#pragma unroll
+      for (int r = 0; r < kTailChunk; ++r) {
+        if (c + r < a.nrep) {
+          sv[r] = reinterpret_cast<const float *>(a.s[c + r])[i];
+          wv[r] = reinterpret_cast<const float *>(a.w[c + r])[i];
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < kTailChunk; ++r) {
+        if (c + r < a.nrep) {
+          const float d = fmaf(-1.0f, z0, sv[r]);                                     // sma.c:79-90
+          reinterpret_cast<float *>(a.w[c + r])[i] = fmaf(-a.alpha, d, wv[r]);       // :93-99
+          acc = fmaf(a.alpha, d, acc);                                               // :102-107
+        }
+      }
     }
     if constexpr (PHASE == 1) {
       reinterpret_cast<float *>(a.acc)[i] = acc;
@@ -106,7 +124,7 @@ __device__ __forceinline__ void sma_tail_elem(const SmaArgs &a, bool copy) {
     D = acc;
   }
   if constexpr (MOM) {
-    D = fmaf(kBaseMomentum, last[i], D);  // sma.c:155-164
+    D = fmaf(kBaseMomentum, l0, D);  // sma.c:155-164
     last[i] = D;
   }
   z0 = fmaf(1.0f, D, z0);  // sma.c:169-174

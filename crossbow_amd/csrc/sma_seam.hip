@@ -12,8 +12,8 @@
 // The context API (context.hip) owns an arena whose buffers are padded to
 // whole kernel trips; the reference's buffers hold exactly `elements` floats.
 // So every launch here runs the bulk of the buffers through the same float4
-// kernels (n4b float4s, a multiple of kPadFloat4) and the last < 4 *
-// kPadFloat4 elements on extra workgroups of the same launch, one float per
+// kernels (n4b float4s, a multiple of kTailQuantum4) and the last < 4 *
+// kTailQuantum4 elements on extra workgroups of the same launch, one float per
 // lane (the kernels' TAIL instantiations, sma_kernels.hip), with the same fma
 // sequence per element: the results equal the context path's and the
 // oracle's bit for bit.
@@ -46,8 +46,16 @@ int cus_of_current_device(int *cus) {
   return CBX_OK;
 }
 
-// Largest whole-trip prefix of an n-float buffer, in float4s.
-int64_t bulk_float4s(int64_t n) { return (n / 4) / cbx::kPadFloat4 * cbx::kPadFloat4; }
+// Largest prefix of an n-float buffer that the float4 kernels cover without
+// bounds checks, in float4s.  Their loops need whole waves' chunks (64 lanes
+// x unroll float4s, every launch shape here has unroll <= 4); bucket starts
+// stay on kPadFloat4.  A smaller tail is fewer scalar workgroups: ResNet-50's
+// n = 25,557,032 leaves 40 elements (2,088 at kPadFloat4 granularity, whose
+// tail workgroups cost ~7 us per fused step on separately allocated buffers:
+// scripts/seam_layout_ab.py, profiles/r02/seam_layout_trace/).
+constexpr int64_t kTailQuantum4 = 256;
+static_assert(cbx::kPadFloat4 % kTailQuantum4 == 0, "bucket starts must stay on whole chunks");
+int64_t bulk_float4s(int64_t n) { return (n / 4) / kTailQuantum4 * kTailQuantum4; }
 
 }  // namespace
 

@@ -48,6 +48,7 @@ ONE_GPU = [
     ("three-elements-no-momentum", 3, 2, 0.0, 2, 0, (), {}),
     ("ragged-4099", 4099, 4, 0.9, 3, 0, (), {1: 2}),
     ("whole-trips", 4096 * 3, 8, 0.9, 2, 0, (), {}),
+    ("quarter-chunk-bulk", 4096 + 1024 + 7, 3, 0.9, 2, 0, (), {1: 1}),  # bulk 1,280 float4s: not whole kPadFloat4s
     ("chunked-9-replicas", 65_541, 9, 0.9, 2, 0, (), {0: 3}),
     ("first-and-held", 300_007, 8, 0.9, 2, 2, (5,), {1: 6}),
     ("lenet-c2", 1_111_946, 4, 0.0, 2, 0, (), {}),
@@ -493,7 +494,7 @@ DEVICE_CASES = [
     ("plan-comms", 50_001, 2, 0.9, 3, {1: 3}, {0: (1,)}, 0, "rank", False, 0),
     ("plan-comms-in-order", 50_001, 2, 0.9, 3, {1: 3}, {0: (1,)}, 0, "rank", False, 1),
     ("caller-comms", 50_001, 2, 0.9, 2, {}, {}, 1, "rank", True, 0),
-    ("tail-only", 1031, 3, 0.9, 2, {1: 0}, {}, 0, "rank", False, 0),  # below one kernel trip: no bulk launch
+    ("tail-only", 1021, 3, 0.9, 2, {1: 0}, {}, 0, "rank", False, 0),  # below one kernel trip: no bulk launch
     ("no-momentum", 20_011, 1, 0.0, 2, {}, {}, 0, "rank", False, 3),
     ("many-buckets", 300_007, 2, 0.9, 4, {2: 1}, {1: (0,)}, 0, "rank", False, 37),  # more buckets than trips allow
     ("ring-order", 300_007, 2, 0.9, 3, {2: 1}, {}, 0, "ring", False, 0),
