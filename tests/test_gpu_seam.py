@@ -92,6 +92,30 @@ def test_seam_one_gpu_bitexact(name, n, R, mom, steps, first, held, copy_at):
         assert _bits_equal(s[i].cpu().numpy(), st.s[i]), f"s[{i}] must be untouched"
 
 
+def _random_cases(count=16, seed=20261017):
+    """Seeded sizes log-uniform in [1, 2^18) (every bulk/tail split the seam can
+    make: no bulk, bulk at any multiple of 1,024 floats, tails of 0..1,023),
+    1..10 replicas (above 8 the kernel walks them in register chunks), momentum 0 / 0.9,
+    a Phase-D request at step 1 half of the time."""
+    rng = np.random.default_rng(seed)
+    out = []
+    for k in range(count):
+        n = int(np.exp(rng.uniform(0.0, np.log(1 << 18))))
+        R = int(rng.integers(1, 11))
+        mom = float(rng.choice([0.0, 0.9]))
+        copy_at = {1: int(rng.integers(0, R))} if rng.random() < 0.5 else {}
+        out.append((f"random-{k}-n{n}-r{R}", n, R, mom, 2, 0, (), copy_at))
+    return out
+
+
+RANDOM = _random_cases()
+
+
+@pytest.mark.parametrize("name,n,R,mom,steps,first,held,copy_at", RANDOM, ids=[c[0] for c in RANDOM])
+def test_seam_random_sizes_bitexact(name, n, R, mom, steps, first, held, copy_at):
+    test_seam_one_gpu_bitexact(name, n, R, mom, steps, first, held, copy_at)
+
+
 def _golden(G):
     from tests.test_oracle import load_golden_cases
     return [c for c in load_golden_cases() if c["G"] == G]
@@ -127,7 +151,7 @@ def test_seam_golden_fixtures_one_gpu(gcase):
 
 def test_seam_resnet50_full_size_bitexact():
     """C3's buffers through the seam: n = 25,557,032 (not a multiple of the
-    kernels' 4096-float trip: a 2,088-element tail), 8 replicas, mu 0.9."""
+    seam's 1,024-float bulk granularity: a 40-element tail), 8 replicas, mu 0.9."""
     import torch
 
     from crossbow_amd.seam import SmaPlan
@@ -653,7 +677,7 @@ def test_seam_largest_model_windows_bitexact():
     last = torch.randn(n, device=dev, generator=gen) * 0.001
     s = [z + 0.01 * torch.randn(n, device=dev, generator=gen) for _ in range(R)]
     w = [si + 0.001 * torch.randn(n, device=dev, generator=gen) for si in s]
-    bulk = (n // 4) // 1024 * 1024 * 4
+    bulk = (n // 4) // 256 * 256 * 4  # the seam's bulk/tail boundary (kTailQuantum4)
     windows = [(0, 70_000), ((1 << 28) - 35_000, (1 << 28) + 35_000), (bulk - 40_000, n)]
     before = [[t[a:b].cpu().numpy().copy() for t in [z, last] + s + w] for a, b in windows]
     stream = torch.cuda.Stream()
