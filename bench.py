@@ -215,9 +215,10 @@ def bench_seam(torch, n, args, steps=20):
     """The sma.c seam (cbx_sma_plan_step): the same step
     over buffers the caller owns -- here one torch allocation per buffer,
     exactly n floats each, as the reference's model manager allocates them --
-    so the fused kernel runs the whole-trip bulk and a tail kernel the last
-    elements.  Timed with torch events around back-to-back steps on the
-    caller's stream (launch gaps included)."""
+    so one launch of the fused kernel runs the whole-trip bulk and, on extra
+    workgroups of the same launch, the last elements.  Timed with torch
+    events around back-to-back steps on the caller's stream (launch gaps
+    included)."""
     from crossbow_amd.seam import SmaPlan
     dev = torch.device("cuda:0")
     gen = torch.Generator(device=dev)

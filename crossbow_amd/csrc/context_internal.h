@@ -271,6 +271,8 @@ struct Device {
   std::vector<char> ring_split;
   // 1: this slot recorded no START; its step queued right behind the previous
   // slot's fused step, whose stop event stands in as its start (ring_start).
+  // 2: the same, but the previous slot has since been reused by a newer step
+  // (the ring wrapped), so this slot has no start any more (spans read -1).
   std::vector<char> ring_from_prev;
   bool start_chosen = false;  // step_start_event decided this slot's ring_from_prev
   unsigned long long start_foreign = ~0ull;  // foreign_ops at the last step_start_event
@@ -608,6 +610,7 @@ inline hipEvent_t step_start_event(cbx_context *c, Device &d, int kind) {
 // The event that opens ring slot `slot`: its START, or the previous slot's
 // stop when the step was enqueued behind it (step_start_event).
 inline hipEvent_t ring_start(Device &d, int slot) {
+  if (!d.ring_from_prev.empty() && d.ring_from_prev[slot] == 2) return nullptr;  // its stand-in was overwritten
   if (!d.ring_from_prev.empty() && d.ring_from_prev[slot])
     return ring_stop(d, (slot + Device::kRing - 1) % Device::kRing);
   return d.ring[(size_t)slot * 4 + EV_START];
@@ -633,7 +636,11 @@ inline void ring_advance(cbx_context *c, Device &d, int kind) {
   d.ring_split[d.ring_pos] = (char)kind;
   if (!d.start_chosen) d.ring_from_prev[d.ring_pos] = 0;  // a path that records START itself
   d.start_chosen = false;
-  d.ring_pos = (d.ring_pos + 1) % Device::kRing;
+  // The next slot (the oldest once the ring is full) borrowed the stop of the
+  // slot just written as its start: that stop now belongs to the newest step.
+  const int next = (d.ring_pos + 1) % Device::kRing;
+  if (d.ring_from_prev[next] == 1) d.ring_from_prev[next] = 2;
+  d.ring_pos = next;
   if (d.ring_count < Device::kRing) d.ring_count++;
 }
 
@@ -642,6 +649,7 @@ inline int ring_span(Device &d, int slot, int a, int b, float *out) {
   *out = -1.0f;
   HIP_TRY(hipEventSynchronize(d.ring[(size_t)slot * 4 + b]));
   hipEvent_t from = a == EV_START ? ring_start(d, slot) : d.ring[(size_t)slot * 4 + a];
+  if (!from) return CBX_OK;  // the slot's start was lost to the ring's wrap
   HIP_TRY(hipEventElapsedTime(out, from, d.ring[(size_t)slot * 4 + b]));
   return CBX_OK;
 }

@@ -471,7 +471,11 @@ int cbx_sma_plan_set_buckets (cbx_sma_plan *plan, int buckets);
  * (base->updated, synched[dev], replica->updated) are recorded on the same
  * streams after the call, as sma.c:115,177,204,222 do.  One step at a time
  * per plan (the reference's single ResultCollector thread): the scratch is
- * the plan's.  With a communicator that spans processes, each process
+ * the plan's.  streams[k] must be the same stream on every call of a plan
+ * (as dev->modelSynchronisationStream is): with buckets, the next step's
+ * all-reduce of bucket k is ordered after this step's last kernel B only
+ * through that stream, so a different stream would let it overwrite the
+ * plan's D while B still reads it.  With a communicator that spans processes, each process
  * passes only its own replicas as locked; a Phase-D request on any rank
  * reaches every rank through the all-reduced control block, so the return
  * value reports this process's requests only.                           */
@@ -495,7 +499,9 @@ int cbx_sma_optimise_buffers (void *stream, float *w, float *g, float *last, flo
  * (used iff momentum > 0: the base model's conf->momentum, NOT forced to
  * 0.9), the locked replicas from `first` on (set to their device's new base
  * model, common.c:198-220) and wpc = defaultBaseModel->wpc (D *= 1/wpc).
- * Buckets as cbx_sma_plan_set_buckets sets them.
+ * Buckets as cbx_sma_plan_set_buckets sets them at G > 1; one rank always
+ * runs one apply pass (no all-reduce to overlap), whatever the setting.
+ * streams[k] must be the same stream on every call, as for cbx_sma_plan_step.
  * crossbowKernelOptimiserSynchronousSGD (kernels/optimisers/synchronoussgd.cu:
  * 3-56) -> cbx_ssgd_accumulate_buffers: g += weight_decay * w, then
  * acc += -learning_rate * g, on `stream` = the device's model-synchronisation

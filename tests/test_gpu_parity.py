@@ -250,6 +250,30 @@ def test_pipelined_timing_spans():
         g.free()
 
 
+def test_timing_history_after_the_ring_wraps():
+    """More back-to-back fused steps than the timing ring holds (1024): a step
+    queued behind a busy GPU borrows the previous slot's stop as its start, and
+    once the ring wraps the oldest slot's stand-in belongs to the newest step.
+    That slot must read -1 (no start), never a negative or garbage span."""
+    from crossbow_amd import _lib
+    g = make_gpu(4_000_000, 2, 0.1, 0.9)
+    try:
+        g.fill_synthetic(3)
+        g.set_timing(True)
+        for c in range(1100):
+            g.lockAny()
+            g.synchronise(0, c, 0, False)
+            g.unlockAny()
+        g.wait()
+        for which in (_lib.T_KERNEL, _lib.T_STEP):
+            h = g.timing_history(which, max_steps=1024)
+            assert len(h) == 1024
+            assert h[0] > 0 or h[0] == -1, h[0]
+            assert all(x > 0 for x in h[1:]), min(h[1:])
+    finally:
+        g.free()
+
+
 def test_multiple_steps_drift():
     _run(50_000, 4, 0.1, 0.9, steps=3)
 

@@ -208,7 +208,10 @@ def test_seam_optimise_bitexact(n, mom, wd):
 def test_seam_ssgd_one_gpu_bitexact(n, R, mom, wd, buckets):
     """Synchronous SGD through the seam: task steps (cbx_ssgd_accumulate_buffers)
     into the caller's base gradient, then the barrier (cbx_ssgd_plan_step),
-    two clocks, against the oracle's synchronoussgd.cu / .c restatement."""
+    two clocks, against the oracle's synchronoussgd.cu / .c restatement.
+    One rank always runs one apply pass (include/crossbow_sma.h): `buckets`
+    must have no effect, which the bit-exact result at every setting shows;
+    bucketing itself is covered by the multi-rank seam tests."""
     import torch
 
     from crossbow_amd.seam import SmaPlan, ssgd_accumulate_buffers
