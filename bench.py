@@ -14,16 +14,27 @@ value = algorithmic bytes moved by all ranks / max-over-ranks wall time of
 exactly K steps ((12R+8+8m)n per step at G = 1, and
 (12R+8)n + (12+8m)n per GPU at G > 1; the all-reduce is reported apart).
 
+Process forms at N > 1:
+  per-rank  one process per GPU, launched by torch.distributed.run (each rank
+            its own RCCL communicator, ncclCommInitRank);
+  single    one process over N devices, the form Crossbow itself takes
+            (TheGPU.init -> ncclCommInitAll, executioncontext.c:185-201, grouped
+            all-reduces from one host thread, synch/common.c:14-54): --gpus N
+            without a torch.distributed.run environment, or --single-process.
+
 Run:  python bench.py [--gpus N --steps K --warmup W]
       python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+      python bench.py --gpus N [--single-process]
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import re
 import statistics
 import sys
+import tempfile
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -75,6 +86,14 @@ def parse():
                    help="N > 1 rehearsal on a one-GPU box: every rank on device 0, each its own RCCL 'host' "
                         "(NCCL_HOSTID), so real RCCL links the ranks by sockets over loopback; the numbers say "
                         "nothing about xGMI, the run checks the N > 1 code path end to end")
+    p.add_argument("--single-process", action="store_true",
+                   help="N > 1 in one process over N devices (cbx_init -> ncclCommInitAll, Crossbow's own form); "
+                        "the default when --gpus N > 1 runs without a torch.distributed.run environment. With "
+                        "--rehearse-one-gpu every device is device 0 and the all-reduce is the peer-read form "
+                        "(RCCL refuses a repeated device)")
+    p.add_argument("--no-rccl-tuning-log", action="store_true",
+                   help="N > 1 with RCCL: do not log RCCL's per-collective tuning choices (NCCL_DEBUG=INFO, "
+                        "NCCL_DEBUG_SUBSYS=TUNING into a file) for the allreduce.rccl_tuning field")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
                    help="PMC-derived HBM bytes per launch (written by scripts/pmc_traffic.py)")
     return p.parse_args()
@@ -252,6 +271,47 @@ def bench_seam(torch, n, args, steps=20):
             "timed": "torch events around back-to-back steps on the caller's stream (one launch per step: bulk + tail workgroups; gaps included)"}
 
 
+RCCL_TUNING_RE = re.compile(r"(\w+): (\d+) Bytes -> Algo (\S+) proto (\S+) channel\{Lo\.\.Hi\}=\{(\d+)\.\.(\d+)\}")
+
+
+def rccl_tuning(path):
+    """RCCL's per-collective tuning choices (NCCL_DEBUG=INFO,
+    NCCL_DEBUG_SUBSYS=TUNING): one entry per (collective, bytes) with the
+    algorithm, protocol and channel range RCCL picked and how often."""
+    seen = {}
+    try:
+        with open(path, errors="replace") as f:
+            for line in f:
+                m = RCCL_TUNING_RE.search(line)
+                if not m:
+                    continue
+                key = (m.group(1), int(m.group(2)), m.group(3), m.group(4), int(m.group(5)), int(m.group(6)))
+                seen[key] = seen.get(key, 0) + 1
+    except OSError:
+        return None
+    return [{"collective": k[0], "bytes": k[1], "algo": k[2], "proto": k[3], "channels": [k[4], k[5]], "calls": v}
+            for k, v in sorted(seen.items(), key=lambda kv: (kv[0][0], kv[0][1]))]
+
+
+def span_stats(gpu, _lib, locals_, steps):
+    """Per-step summed busy spans of kernels A, collectives and kernels B over
+    the last `steps` steps on every local device (cbx_timing_history: for a
+    pipelined step each dispatch's stop minus the latest event that bounded
+    its start; for a one-bucket step the exact START..A / A..AR / AR..B).
+    Returns (A, coll, B) lists of per-step ms (device-major), None if any
+    step kept no spans."""
+    out = []
+    for which in (_lib.T_KERNEL, _lib.T_ALLREDUCE, _lib.T_APPLY):
+        vals = []
+        for k in range(locals_):
+            h = list(gpu.timing_history(which, local=k)[-steps:])
+            if len(h) < steps or any(x <= 0 for x in h):
+                return None
+            vals += h
+        out.append(vals)
+    return tuple(out)
+
+
 def main():
     args = parse()
     # stdout carries the ONE JSON line and nothing else: native libraries
@@ -263,22 +323,43 @@ def main():
     os.dup2(2, 1)
     from crossbow_amd import dist as D
     rank, world, local_rank = D.env_rank()
-    if args.rehearse_one_gpu:
-        D.rehearsal_env(rank)
-        local_rank = 0
-    if world != args.gpus:
-        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: launch N>1 with torch.distributed.run")
+    G = args.gpus
+    single = G > 1 and (args.single_process or "WORLD_SIZE" not in os.environ)
+    if single:
+        if world != 1:
+            raise SystemExit("--single-process drives every GPU from one process: launch it without torch.distributed.run")
+        devices = [0] * G if args.rehearse_one_gpu else list(range(G))
+        local_rank = devices[0]
+    else:
+        if args.rehearse_one_gpu:
+            D.rehearsal_env(rank)
+            local_rank = 0
+        if world != G:
+            raise SystemExit(f"--gpus {G} but WORLD_SIZE={world}: launch N>1 with torch.distributed.run "
+                             "(one process per GPU) or without it (one process over N GPUs)")
+    nlocal = G if single else 1
+    peer_only = single and args.rehearse_one_gpu  # RCCL refuses a repeated device: the peer-read form only
+    rccl_log = None
+    if G > 1 and not peer_only and not args.no_rccl_tuning_log and "NCCL_DEBUG" not in os.environ:
+        # RCCL reads these once, at its first call: every collective then logs
+        # its algorithm / protocol / channels (one line each) to the file.
+        rccl_log = os.path.join(tempfile.gettempdir(), f"cbx_rccl_tuning.r{rank}.{os.getpid()}.log")
+        os.environ.update(NCCL_DEBUG="INFO", NCCL_DEBUG_SUBSYS="TUNING", NCCL_DEBUG_FILE=rccl_log)
 
     import torch
 
     from crossbow_amd import SYNC_BSP, UPDATE_SMA, TheGPU, _lib
+    ALLREDUCE_PEER = _lib.ALLREDUCE_PEER
     from crossbow_amd.variables import MODELS, register
 
     torch.cuda.set_device(local_rank)
-    D.init(world, rank)
     gpu = TheGPU()
-    uid = D.share_unique_id(rank, world, TheGPU.unique_id)
-    gpu.init_rank(local_rank, world, rank, uid)
+    if single:
+        gpu.init(devices)
+    else:
+        D.init(world, rank)
+        uid = D.share_unique_id(rank, world, TheGPU.unique_id)
+        gpu.init_rank(local_rank, world, rank, uid)
 
     shapes = MODELS[args.model]()
     n = register(gpu, shapes)
@@ -296,10 +377,13 @@ def main():
     bucket_elems = int(args.bucket_mb * (1 << 20) / 4) if args.bucket_mb > 0 else (one_bucket if args.bucket_mb < 0 else 0)
     if args.force_split:
         gpu.set_force_split(True)
+    if peer_only:
+        gpu.set_allreduce_algorithm(ALLREDUCE_PEER)
     gpu.fill_synthetic(SEED)
     gpu.set_timing(True)
 
     clock = 0
+    host_ms = []
 
     def step():
         nonlocal clock
@@ -308,15 +392,15 @@ def main():
         gpu.synchronise(0, clock, 0, False)
         gpu.unlockAny()
 
-    G = world
     split = G > 1 or args.force_split
     calib = None
     if rank == 0:
-        log(f"[bench] {world} rank(s), n = {n}, {args.replicas} replicas per GPU: "
-            f"{'calibration, tuning, ' if split else ''}warm-up, {args.steps} timed steps")
+        log(f"[bench] {G} GPU(s) in {'one process' if single or G == 1 else f'{world} processes'}, n = {n}, "
+            f"{args.replicas} replicas per GPU: {'calibration, tuning, ' if split else ''}warm-up, "
+            f"{args.steps} timed steps")
     if split:
         # Calibration: one bucket, everything in order on the sync stream, so
-        # HIP events separate kernel A, the RCCL all-reduce and kernel B.
+        # HIP events separate kernel A, the collective and kernel B.
         gpu.set_bucket_elements(one_bucket)
         for _ in range(args.calib_steps):
             step()
@@ -331,11 +415,12 @@ def main():
     pipeline_mode = 0
     wait_stride = 1
     ar_group = 1
-    ar_algo = 0
-    if split and args.bucket_mb == 0:
+    ar_algo = ALLREDUCE_PEER if peer_only else 0
+    if split and args.bucket_mb == 0 and not peer_only:
         # warm-up autotune of the bucket count on the live communicator (same choice on every rank)
         bucket_elems, pipeline_mode, wait_stride, ar_group, ar_algo, tuning = D.tune_buckets(
-            gpu, n, world, step, progress=(lambda m: log(f"[bench] {m}")) if rank == 0 else None)
+            gpu, n, world, step, progress=(lambda m: log(f"[bench] {m}")) if rank == 0 else None,
+            ndev=G, peer=single)
 
     for _ in range(args.warmup):
         step()
@@ -346,17 +431,20 @@ def main():
         log("[bench] timed region")
     t0 = time.perf_counter()
     for _ in range(args.steps):
+        h0 = time.perf_counter()
         step()
+        host_ms.append((time.perf_counter() - h0) * 1e3)
     gpu.wait()
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
     D.barrier(world)
     el = D.max_over_ranks(el, world)
+    spans = span_stats(gpu, _lib, nlocal, args.steps) if split else None
 
     step_bytes, kernel_bytes = alg_bytes(n, args.replicas, args.momentum, 2 if split else 1)
-    kern = calib["kernel"] if split else list(gpu.timing_history(_lib.T_KERNEL)[-args.steps:])
     steps_ms = gpu.timing_history(_lib.T_STEP)[-args.steps:]
-    kern_ms = statistics.mean(kern)
+    form = ("peer-read two-shot" if ar_algo == ALLREDUCE_PEER else
+            "reduce-scatter+all-gather" if ar_algo == 2 else "all-reduce")
     result = {
         "metric": METRIC,
         "value": round(step_bytes * G * args.steps / el / 1e9, 2),
@@ -384,20 +472,22 @@ def main():
                 step_bytes if not (split and ar_algo == 2) else
                 (12 * args.replicas + 8) * n + 12 * n + (12 * n // G if args.momentum > 0 else 0)),
             "parallelism": f"sma-dp{G}",
-            "pipeline": "fused" if not split else "accumulate+rccl-allreduce+apply, bucketed on two streams",
-            "buckets": (None if not split else int(min(tuning, key=lambda k: tuning[k]).split("/")[0]) if tuning
+            "process_form": None if G == 1 else ("single" if single else "per-rank"),
+            "pipeline": "fused" if not split else "accumulate+collective+apply, bucketed on two streams",
+            "buckets": (None if not split else 1 if ar_algo == ALLREDUCE_PEER else
+                        int(min(tuning, key=lambda k: tuning[k]).split("/")[0])
+                        if tuning and not min(tuning, key=lambda k: tuning[k]).startswith("peer")
                         else -(-n // min(bucket_elems, n)) if bucket_elems else "library default (8)"),
             "pipeline_mode": None if not split else pipeline_mode,
             "cross_wait_stride": None if not split else wait_stride,
             "allreduce_group": None if not split else ar_group,
-            "allreduce_algorithm": None if not split else ("reduce-scatter+all-gather" if ar_algo == 2 else "all-reduce"),
+            "allreduce_algorithm": None if not split else form,
             "bucket_tuning_ms_per_step": tuning,
             "kernel_config": dict(block=args.block, blocks_per_cu=args.blocks_per_cu, policy=args.policy,
                                   unroll=args.unroll, waves_per_cu=args.waves_per_cu, bucket_mb=args.bucket_mb),
         },
     }
     kname = "sma_fused_kernel" if not split else "sma_accumulate_kernel"
-    achieved = kernel_bytes / (kern_ms * 1e-3) / 1e9
     traffic, traffic_note = None, None
     try:
         from crossbow_amd.build import code_object_digest
@@ -418,21 +508,72 @@ def main():
                             f"({running[:12]}); traffic / alg = {traffic / kernel_bytes:.4f}")
     except (OSError, ValueError) as e:
         traffic_note = f"unavailable: {e}"
-    result["roofline"] = {"bound": "hbm", "kernel": kname, "achieved": round(achieved, 1),
-                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                          "traffic": traffic, "traffic_note": traffic_note, "alg_bytes_per_launch": kernel_bytes,
-                          "launch_ms_mean": round(kern_ms, 4), "launch_ms_median": round(statistics.median(kern), 4),
-                          "launches": len(kern),
-                          "timed_in": "timed region" if not split else "calibration steps (one bucket, in order)"}
+
+    def roofline(kern, timed_in, kbytes=kernel_bytes, kernel=kname):
+        kern_ms = statistics.mean(kern)
+        achieved = kbytes / (kern_ms * 1e-3) / 1e9
+        return {"bound": "hbm", "kernel": kernel, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "alg_bytes_per_launch": kbytes,
+                "launch_ms_mean": round(kern_ms, 4), "launch_ms_median": round(statistics.median(kern), 4),
+                "launches": len(kern), "timed_in": timed_in}
+
+    if not split:
+        result["roofline"] = roofline(list(gpu.timing_history(_lib.T_KERNEL)[-args.steps:]), "timed region")
+    else:
+        # N > 1: the kernels as they ran in the timed region, beside the
+        # collectives (per step: kernel A's dispatches' summed busy spans);
+        # the calibration's one-bucket, in-order figure is kept apart.
+        b_bytes = (12 + 8 * (1 if args.momentum > 0 else 0)) * n
+        unpiped = roofline(calib["kernel"], "calibration steps (one bucket, in order)")
+        if spans is not None:
+            a_ms, coll_ms, b_ms = spans
+            result["roofline"] = roofline(
+                a_ms, "timed region: per step, the summed busy spans of kernel A's dispatches (each its stop minus "
+                      "the latest event bounding its start: an upper bound incl. dispatch latency), beside the "
+                      f"collectives; {'every local device, ' if nlocal > 1 else ''}max over ranks via the slowest")
+            # max over ranks: the slowest rank's kernel time sets the roofline
+            worst = D.max_over_ranks(statistics.mean(a_ms), world)
+            if worst > statistics.mean(a_ms):
+                result["roofline"] = roofline([worst], result["roofline"]["timed_in"])
+            result["roofline"]["apply_kernel"] = roofline(b_ms, "timed region (summed busy spans of kernel B)",
+                                                          b_bytes, "sma_apply_kernel")
+            ab = [x + y for x, y in zip(a_ms, b_ms)]
+            result["roofline"]["a_plus_b"] = roofline(ab, "timed region (kernels A + B)", kernel_bytes + b_bytes,
+                                                      "sma_accumulate_kernel+sma_apply_kernel")
+            result["roofline"]["collective_busy_ms_mean"] = round(statistics.mean(coll_ms), 4)
+        else:
+            result["roofline"] = dict(unpiped, timed_in=unpiped["timed_in"] + " (the timed steps kept no spans)")
+        result["roofline_unpipelined"] = unpiped
+    result["roofline"]["traffic"] = traffic
+    result["roofline"]["traffic_note"] = traffic_note
     result["step_ms_device_median"] = round(statistics.median(steps_ms), 4)
+    if G > 1:
+        # Host side of the step (lockAny + synchronise + unlockAny, every local
+        # device's enqueue) against the device's step: the single-process form
+        # enqueues all G devices' kernels and collectives from one thread.
+        idle = []
+        for _ in range(5):
+            gpu.wait()
+            h0 = time.perf_counter()
+            step()
+            idle.append((time.perf_counter() - h0) * 1e3)
+        gpu.wait()
+        result["host"] = {"enqueue_ms_per_step_timed": round(statistics.median(host_ms), 4),
+                          "enqueue_ms_per_step_idle_gpu": round(statistics.median(idle), 4),
+                          "devices_per_process": nlocal,
+                          "note": "perf_counter around lockAny+synchronise+unlockAny; 'idle_gpu' after a wait, so "
+                                  "no queue back-pressure; host-bound when it exceeds ms_per_step"}
     if args.rehearse_one_gpu:
         result["rehearsal"] = (f"{G} ranks on ONE GPU over RCCL's socket transport (NCCL_HOSTID per rank): "
-                               "a check of the N > 1 code path, not an N-GPU measurement")
+                               "a check of the N > 1 code path, not an N-GPU measurement" if not single else
+                               f"{G} devices of one process that are all device 0, peer-read all-reduce (RCCL "
+                               "refuses a repeated device): the single-process form's host side and code path, "
+                               "not an N-GPU measurement")
     if split:
         ar_ms = statistics.median(calib["allreduce"])
         algbw = 4 * n / (ar_ms * 1e-3) / 1e9
         busbw = algbw * 2 * (G - 1) / G if G > 1 else 0.0
-        result["allreduce"] = {"ms_median": round(ar_ms, 4), "algbw_GBs": round(algbw, 1),
+        result["allreduce"] = {"form": form, "ms_median": round(ar_ms, 4), "algbw_GBs": round(algbw, 1),
                                "busbw_GBs": round(busbw, 1),
                                # a G-GPU all-reduce can use the G-1 links from each GPU to its peers
                                "xgmi_links": G - 1, "xgmi_peak_GBs": (G - 1) * XGMI_LINK_GBS,
@@ -440,11 +581,19 @@ def main():
                                "apply_ms_median": round(statistics.median(calib["apply"]), 4),
                                "unpipelined_step_ms_median": round(statistics.median(calib["step"]), 4),
                                "timed_in": "calibration steps (one bucket, in order)"}
+        if rccl_log:
+            gpu.wait()
+            result["allreduce"]["rccl_tuning"] = rccl_tuning(rccl_log)
+            result["allreduce"]["rccl_tuning_source"] = (
+                "RCCL's own log (NCCL_DEBUG=INFO, NCCL_DEBUG_SUBSYS=TUNING), this process, every collective of the "
+                "run (calibration, tuning, timed)")
 
-    if world > 1 and not args.no_staged:
+    if G > 1 and not args.no_staged and peer_only:
+        result["host_staged"] = {"skipped": "the host-staged step's collective is RCCL's, which refuses a repeated device"}
+    elif G > 1 and not args.no_staged:
         # Host-staged rate at N > 1 (north_star: the path starts and ends in
-        # host memory): each rank's replicas live in its own pinned mirror and
-        # cross its own GPU's PCIe link; zero-copy staging kernels, kernel A /
+        # host memory): each GPU's replicas live in its own pinned mirror and
+        # cross its own PCIe link; zero-copy staging kernels, kernel A /
         # all-reduce / kernel B per bucket.  Max over ranks of the median of 3.
         # The pinned mirror is allocated first (no collective); every rank
         # must have one before any rank enters the staged step's collectives.
@@ -466,20 +615,20 @@ def main():
                 gpu.synchronise_staged(0, clock, 0, args.staged_buckets)
                 gpu.unlockAny()
                 gpu.wait()
-                runs.append(gpu.last_timing(0)[_lib.T_STEP])
+                runs.append(max(gpu.last_timing(k)[_lib.T_STEP] for k in range(nlocal)))
             ms = D.max_over_ranks(sorted(runs)[1], world)
             result["host_staged"] = {"zerocopy": {
                 "buckets": args.staged_buckets, "step_ms": round(ms, 3),
                 "end_to_end_GBs": round(step_bytes * G / (ms * 1e-3) / 1e9, 2),
                 "per_gpu_GBs": round(step_bytes / (ms * 1e-3) / 1e9, 2),
-                "timed": "HIP events per rank (staged step: host in, host and device out), max over ranks"}}
+                "timed": "HIP events per device (staged step: host in, host and device out), max over devices"}}
 
-    if rank == 0 and world == 1 and not args.no_optimiser:
+    if rank == 0 and G == 1 and not args.no_optimiser:
         result["replica_optimiser"] = bench_optimiser(gpu, torch, n, args)
-    if rank == 0 and world == 1 and not args.no_seam:
+    if rank == 0 and G == 1 and not args.no_seam:
         result["seam"] = bench_seam(torch, n, args)
 
-    if rank == 0 and world == 1:
+    if rank == 0 and G == 1:
         if not args.no_copy_ceiling:
             result["copy_ceiling_GBs"] = round(gpu.bench_copy(1 << 30, 20), 1)
         if not args.no_staged:

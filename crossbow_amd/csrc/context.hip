@@ -116,7 +116,11 @@ int cbx_init(cbx_context **out, const int *devices, int ndevices) {
     for (int b = 0; b < a; ++b) repeated = repeated || devices[a] == devices[b];
   if (!repeated)
     for (Device &d : c->devs) d.file_id = d.hip_id;
-  if (ndevices > 1) {
+  // RCCL refuses a clique that repeats a device: such a selection (a one-GPU
+  // rehearsal of this form) creates its communicators on first use, which
+  // fails there unless the test harness's loopback collective stands in;
+  // the peer-read all-reduce needs none (ensure_comms, sync_steps.hip).
+  if (ndevices > 1 && !repeated) {
     // executioncontext.c:185-201: ncclCommInitAll over the selected devices;
     // communicators are indexed by rank (selected-device order).
     std::vector<ncclComm_t> comms(ndevices);
@@ -1014,12 +1018,7 @@ int cbx_average_batchnorm_stats(cbx_context *c, int layers, const int *elements,
   // :165-166: nothing to average with one device.
   const bool run = c->G > 1 || c->force_split;
   if (!run) return CBX_OK;
-  if (c->G == 1 && c->devs[0].comm == nullptr) {
-    Device &d = c->devs[0];
-    HIP_TRY(hipSetDevice(d.hip_id));
-    int dev = d.hip_id;
-    NCCL_TRY(ncclCommInitAll(&d.comm, 1, &dev));
-  }
+  TRY(ensure_comms(c));
   std::vector<BnDevice> devs;
   for (Device &d : c->devs)
     devs.push_back({d.hip_id, d.g, d.comm, d.stream, &d.bn_table, &d.bn_table_bytes, &d.bn_scratch, &d.bn_scratch_bytes});
@@ -1356,12 +1355,19 @@ int cbx_set_timing(cbx_context *c, int enable) {
     for (int k = 0; k < EV_COUNT; ++k) d.ev_valid[k] = false;
     d.ring_pos = 0;
     d.ring_count = 0;
+    d.span_pos = 0;
+    d.span_last = -1;
     if (c->timing && d.ring.empty()) {
       HIP_TRY(hipSetDevice(d.hip_id));
       d.ring.resize((size_t)Device::kRing * 4, nullptr);
       d.ring_split.assign(Device::kRing, 0);
       d.ring_from_prev.assign(Device::kRing, 0);
       for (hipEvent_t &e : d.ring) HIP_TRY(hipEventCreate(&e));
+      d.spans.resize(Device::kSpanRing);
+    }
+    if (!d.ring.empty()) {
+      d.ring_span.assign(Device::kRing, -1);
+      for (Device::SpanSlot &s : d.spans) s.ring_slot = -1;
     }
   }
   return CBX_OK;
@@ -1411,6 +1417,11 @@ int cbx_last_timing(cbx_context *c, int local, float *ms) {
       TRY(ring_span(d, slot, EV_A, EV_AR, &ms[CBX_T_ALLREDUCE]));
       TRY(ring_span(d, slot, EV_AR, EV_B, &ms[CBX_T_APPLY]));
     }
+    if (kind == 2) {  // pipelined: summed busy spans of the step's dispatches
+      TRY(span_sum(d, slot, Device::SPAN_A, &ms[CBX_T_KERNEL]));
+      TRY(span_sum(d, slot, Device::SPAN_COLL, &ms[CBX_T_ALLREDUCE]));
+      TRY(span_sum(d, slot, Device::SPAN_B, &ms[CBX_T_APPLY]));
+    }
     TRY(ring_span(d, slot, EV_START, kind == 0 ? EV_A : EV_B, &ms[CBX_T_STEP]));
   }
   auto span = [&](int a, int b, float *out) -> int {
@@ -1439,8 +1450,12 @@ int cbx_timing_history(cbx_context *c, int local, int which, float *ms, int max)
     if (which == CBX_T_APPLY) { a = EV_AR; b = EV_B; }
     const int kind = d.ring_split[slot];
     if (which == CBX_T_STEP) { a = EV_START; b = (kind == 0) ? EV_A : EV_B; }
-    if ((which == CBX_T_KERNEL && kind == 2) ||
-        ((which == CBX_T_ALLREDUCE || which == CBX_T_APPLY) && kind != 1)) {
+    if (kind == 2 && which != CBX_T_STEP) {  // pipelined: summed busy spans of the step's dispatches
+      const int sk = which == CBX_T_KERNEL ? Device::SPAN_A : which == CBX_T_APPLY ? Device::SPAN_B : Device::SPAN_COLL;
+      TRY(span_sum(d, slot, sk, &ms[k]));
+      continue;
+    }
+    if ((which == CBX_T_ALLREDUCE || which == CBX_T_APPLY) && kind != 1) {
       ms[k] = -1.0f;
       continue;
     }

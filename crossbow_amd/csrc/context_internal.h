@@ -278,6 +278,39 @@ struct Device {
   unsigned long long start_foreign = ~0ull;  // foreign_ops at the last step_start_event
   int ring_pos = 0;
   int ring_count = 0;
+  // Kernel spans of pipelined split steps (timing on, order check off): in
+  // the last kSpanRing such steps every kernel A and B dispatch stops an
+  // event of its own, and so does the collective of each bucket (an event
+  // recorded on the comm stream after it).  Each record also keeps the events
+  // that bound its start: the previous dispatch on its stream and the events
+  // its stream waited on since.  A dispatch starts when the last of them has
+  // completed, so stop - (latest of them) is its busy span, an upper bound
+  // that includes the dispatch latency (SplitStep, cbx_timing_history).
+  static constexpr int kSpanRing = 64;
+  static constexpr int64_t kSpanMaxBuckets = 64;
+  static constexpr int kSpanPreds = 4;
+  enum SpanKind { SPAN_A = 0, SPAN_B = 1, SPAN_COLL = 2 };
+  struct SpanRec {
+    hipEvent_t stop = nullptr;
+    hipEvent_t pred[kSpanPreds] = {};
+    int npred = 0;  // 0: start unknown
+    int kind = SPAN_A;
+  };
+  struct SpanSlot {
+    int ring_slot = -1;       // the timing-ring slot of the step it holds
+    bool preds_valid = true;  // false once the slot before it was reused (its records' predecessors are gone)
+    int64_t nb = 0;
+    std::vector<hipEvent_t> a, red, b;  // owned, timing-enabled, per bucket
+    hipEvent_t entry = nullptr;         // owned: the cross-step join point on the sync stream
+    std::vector<hipEvent_t> a_used, b_used;  // the stop events kernels A(k) / B(k) really carried
+    std::vector<SpanRec> recs;
+  };
+  std::vector<SpanSlot> spans;  // kSpanRing, created with the timing ring
+  std::vector<int> ring_span;   // timing-ring slot -> span slot, or -1
+  int span_pos = 0;
+  int span_last = -1;        // span slot of the last pipelined step
+  int pending_span = -1;     // span slot of the step ring_advance is about to close
+  bool cross_spans = false;  // the last cross-pipelined step ran with span events
 };
 
 }  // namespace cbx::host
@@ -535,6 +568,11 @@ inline void close_device(Device &d) {
   for (int k = 0; k < EV_COUNT; ++k)
     if (d.ev[k]) (void)hipEventDestroy(d.ev[k]);
   for (hipEvent_t e : d.ring) (void)hipEventDestroy(e);
+  for (Device::SpanSlot &s : d.spans) {
+    for (auto *v : {&s.a, &s.red, &s.b})
+      for (hipEvent_t e : *v) (void)hipEventDestroy(e);
+    if (s.entry) (void)hipEventDestroy(s.entry);
+  }
   for (hipEvent_t e : d.bucket_acc) (void)hipEventDestroy(e);
   for (hipEvent_t e : d.bucket_red) (void)hipEventDestroy(e);
   if (d.a_stream) (void)hipStreamSynchronize(d.a_stream);
@@ -634,6 +672,8 @@ inline int mark(cbx_context *c, Device &d, int ev) {
 inline void ring_advance(cbx_context *c, Device &d, int kind) {
   if (!c->timing || d.ring.empty()) return;
   d.ring_split[d.ring_pos] = (char)kind;
+  if (!d.ring_span.empty()) d.ring_span[d.ring_pos] = d.pending_span;
+  d.pending_span = -1;
   if (!d.start_chosen) d.ring_from_prev[d.ring_pos] = 0;  // a path that records START itself
   d.start_chosen = false;
   // The next slot (the oldest once the ring is full) borrowed the stop of the
@@ -651,6 +691,35 @@ inline int ring_span(Device &d, int slot, int a, int b, float *out) {
   hipEvent_t from = a == EV_START ? ring_start(d, slot) : d.ring[(size_t)slot * 4 + a];
   if (!from) return CBX_OK;  // the slot's start was lost to the ring's wrap
   HIP_TRY(hipEventElapsedTime(out, from, d.ring[(size_t)slot * 4 + b]));
+  return CBX_OK;
+}
+
+// Summed busy ms of the `kind` dispatches (Device::SpanKind) of the pipelined
+// step in ring slot `slot`: for each, stop - the latest event that bounded
+// its start, i.e. the minimum over those events of elapsed(event, stop).
+// -1 when the step kept no span records (another form, or overwritten).
+inline int span_sum(Device &d, int slot, int kind, float *out) {
+  *out = -1.0f;
+  if (d.ring_span.empty() || d.ring_span[slot] < 0) return CBX_OK;
+  Device::SpanSlot &sp = d.spans[d.ring_span[slot]];
+  if (sp.ring_slot != slot || !sp.preds_valid) return CBX_OK;
+  float sum = 0.0f;
+  int n = 0;
+  for (const Device::SpanRec &r : sp.recs) {
+    if (r.kind != kind) continue;
+    if (r.npred <= 0) return CBX_OK;
+    HIP_TRY(hipEventSynchronize(r.stop));
+    float best = 1e30f;
+    for (int i = 0; i < r.npred; ++i) {
+      float ms = 0.0f;
+      HIP_TRY(hipEventElapsedTime(&ms, r.pred[i], r.stop));
+      best = std::min(best, ms);
+    }
+    if (best < 0.0f) return CBX_OK;
+    sum += best;
+    ++n;
+  }
+  if (n > 0) *out = sum;
   return CBX_OK;
 }
 
@@ -682,6 +751,8 @@ int sma_step(cbx_context *c, int first);
 int sma_step_staged(cbx_context *c, int first, int buckets);
 // Synchronous SGD, update model WORKER (synch/synchronoussgd.c:13-106).
 int ssgd_step(cbx_context *c, int first);
+// RCCL communicators on first use (one-rank, or a clique that repeats a device).
+int ensure_comms(cbx_context *c);
 // The step event of every device (cbx_step_event), after a step's last dispatch.
 int finish_step(cbx_context *c);
 // The stop event for a step's LAST dispatch (see sync_steps.hip).

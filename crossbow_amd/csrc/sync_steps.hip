@@ -84,14 +84,23 @@ hipEvent_t step_stop_event(cbx_context *c, Device &d, int ev) {
   return d.synched;
 }
 
-// cbx_set_force_split at G = 1: the split pipeline runs over a one-rank
-// communicator so a single-GPU host exercises kernel A + RCCL + kernel B.
-int ensure_one_rank_comm(cbx_context *c) {
-  if (c->G != 1 || !c->force_split || c->devs[0].comm != nullptr) return CBX_OK;
-  Device &d = c->devs[0];
-  HIP_TRY(hipSetDevice(d.hip_id));
-  int dev = d.hip_id;
-  NCCL_TRY(ncclCommInitAll(&d.comm, 1, &dev));
+// The communicators, created on first use where cbx_init did not create them:
+// a one-rank communicator at G = 1 (cbx_set_force_split, S-SGD's split path,
+// BN averaging), so a single-GPU host exercises kernel A + RCCL + kernel B;
+// and the ncclCommInitAll clique of a device selection that repeats a device
+// (a one-GPU rehearsal of the single-process form), which real RCCL refuses:
+// there only the peer-read form (no communicator) runs.
+int ensure_comms(cbx_context *c) {
+  if (c->devs[0].comm != nullptr || (c->per_rank && c->G > 1)) return CBX_OK;
+  std::vector<ncclComm_t> comms(c->devs.size());
+  std::vector<int> ids;
+  for (Device &d : c->devs) ids.push_back(d.hip_id);
+  HIP_TRY(hipSetDevice(ids[0]));
+  ncclResult_t r = ncclCommInitAll(comms.data(), (int)ids.size(), ids.data());
+  if (r != ncclSuccess)
+    return fail(CBX_ERR_RCCL, "ncclCommInitAll over %d device(s): %s%s", (int)ids.size(), ncclGetErrorString(r),
+                ids.size() > 1 ? " (RCCL takes each device once; the peer-read all-reduce needs no communicator)" : "");
+  for (size_t k = 0; k < comms.size(); ++k) c->devs[k].comm = comms[k];
   return CBX_OK;
 }
 
@@ -211,14 +220,97 @@ struct SplitStep {
   std::vector<cbx::SmaArgs> &args;
   bool mom;
   int64_t b4 = 0, nb = 0, wait_stride = 1;
-  bool pipelined = false, cross = false, rsag = false, ocheck = false;
+  bool pipelined = false, cross = false, rsag = false, ocheck = false, spans = false;
   unsigned long long foreign = 0;
   std::vector<char> join;
+  // Kernel spans (Device::SpanSlot), per device: the step's slot, the
+  // previous pipelined step's, the last stop event on each stream the step
+  // uses (0 sync stream, 1 a_stream, 2 comm_stream) and the events each of
+  // those streams waited on since.
+  struct Track {
+    Device::SpanSlot *slot = nullptr, *prev = nullptr;
+    hipEvent_t last[3] = {};
+    std::vector<hipEvent_t> pending[3];
+  };
+  std::vector<Track> tr;
 
   SplitStep(cbx_context *ctx, std::vector<cbx::SmaArgs> &a, bool momentum) : c(ctx), args(a), mom(momentum) {}
 
   int64_t start_of(int64_t b) const { return b * b4; }
   int64_t len_of(int64_t b) const { return std::min(b4, c->n4 - b * b4); }
+
+  // The event kernel A(b) of this step stops (the collective of b waits on it).
+  hipEvent_t ev_a(size_t k, int64_t b) {
+    Device &d = c->devs[k];
+    return ocheck ? d.ord[d.ord_cur].a1[b] : spans ? tr[k].slot->a[b] : d.bucket_acc[b];
+  }
+  // The event recorded on the comm stream after the collective of bucket b.
+  hipEvent_t ev_red(size_t k, int64_t b) { return spans ? tr[k].slot->red[b] : c->devs[k].bucket_red[b]; }
+
+  void note_wait(size_t k, int s, hipEvent_t e) {
+    if (spans) tr[k].pending[s].push_back(e);
+  }
+  // A dispatch on stream s stopping `stop`: its start is bounded by the last
+  // stop on s and by every event s waited on since (or known exactly).
+  void note_dispatch(size_t k, int s, int kind, hipEvent_t stop, hipEvent_t exact_start) {
+    if (!spans) return;
+    Track &t = tr[k];
+    Device::SpanRec r;
+    r.stop = stop;
+    r.kind = kind;
+    if (exact_start) {
+      r.pred[r.npred++] = exact_start;
+    } else {
+      if (t.last[s]) r.pred[r.npred++] = t.last[s];
+      for (hipEvent_t e : t.pending[s]) {
+        if (r.npred == Device::kSpanPreds) {
+          r.npred = 0;  // more than it keeps: start unknown
+          break;
+        }
+        r.pred[r.npred++] = e;
+      }
+    }
+    t.slot->recs.push_back(r);
+    t.last[s] = stop;
+    t.pending[s].clear();
+  }
+
+  // This step's span slot on device k, and where each stream left off.
+  int prepare_spans(size_t k) {
+    Device &d = c->devs[k];
+    Track &t = tr[k];
+    const int p = d.span_pos;
+    Device::SpanSlot &sl = d.spans[p];
+    if (sl.ring_slot >= 0 && d.ring_span[sl.ring_slot] == p) d.ring_span[sl.ring_slot] = -1;
+    d.spans[(p + 1) % Device::kSpanRing].preds_valid = false;  // its records may point into this slot
+    sl.ring_slot = d.ring_pos;
+    sl.preds_valid = true;
+    sl.nb = nb;
+    sl.recs.clear();
+    for (auto *v : {&sl.a, &sl.red, &sl.b})
+      while ((int64_t)v->size() < nb) {
+        hipEvent_t e;
+        HIP_TRY(hipEventCreate(&e));
+        v->push_back(e);
+      }
+    if (!sl.entry) HIP_TRY(hipEventCreate(&sl.entry));
+    sl.a_used.assign(nb, nullptr);
+    sl.b_used.assign(nb, nullptr);
+    t.slot = &sl;
+    const int prev_ring = (d.ring_pos + Device::kRing - 1) % Device::kRing;
+    t.prev = nullptr;
+    if (d.span_last >= 0 && d.spans[d.span_last].ring_slot == prev_ring && d.ring_count > 0)
+      t.prev = &d.spans[d.span_last];
+    if (t.prev) t.last[2] = t.prev->red[t.prev->nb - 1];
+    if (!cross) {
+      if (d.ring_count > 0) t.last[0] = ring_stop(d, prev_ring);
+    } else if (!join[k]) {  // continues the previous cross step bucket by bucket (same nb, spans on)
+      if (!t.prev) return fail(CBX_ERR_STATE, "span records of the previous step are missing");
+      t.last[1] = t.prev->a_used[nb - 1];
+      t.last[0] = t.prev->b_used[nb - 1];
+    }
+    return CBX_OK;
+  }
 
   // Bucket geometry, per-bucket events, the cross-step join decision, and a
   // fresh set of stream-order timestamps when the check is on.
@@ -236,9 +328,12 @@ struct SplitStep {
     cross = pipelined && c->pipeline_mode == 1;
     rsag = c->allreduce_algo == CBX_ALLREDUCE_RSAG;
     ocheck = c->order_check && c->timing;
+    spans = c->timing && !ocheck && pipelined && nb <= Device::kSpanMaxBuckets;
+    for (Device &d : c->devs) spans = spans && !d.spans.empty();
     wait_stride = std::max(1, c->cross_wait_stride);
     foreign = c->foreign_ops.load(std::memory_order_acquire);
     join.assign(c->devs.size(), 1);
+    tr.assign(c->devs.size(), Track());
     for (size_t k = 0; k < c->devs.size(); ++k) {
       Device &d = c->devs[k];
       HIP_TRY(hipSetDevice(d.hip_id));
@@ -262,11 +357,15 @@ struct SplitStep {
           HIP_TRY(hipMemsetAsync(d.decision, 0, 256, d.stream));
           d.cross_valid = false;
         }
-        join[k] = !d.cross_valid || d.cross_nb != nb || d.cross_foreign != foreign;
-        if (join[k]) {
-          HIP_TRY(hipEventRecord(d.cross_entry, d.stream));
-          HIP_TRY(hipStreamWaitEvent(d.a_stream, d.cross_entry, 0));
-        }
+        join[k] = !d.cross_valid || d.cross_nb != nb || d.cross_foreign != foreign || d.cross_spans != spans;
+      }
+      if (spans) TRY(prepare_spans(k));
+      if (cross && join[k]) {
+        hipEvent_t e = spans ? tr[k].slot->entry : d.cross_entry;
+        HIP_TRY(hipEventRecord(e, d.stream));
+        HIP_TRY(hipStreamWaitEvent(d.a_stream, e, 0));
+        note_wait(k, 1, e);
+        if (spans) tr[k].last[0] = e;  // everything before it on the sync stream
       }
       if (ocheck) {
         d.ord_cur ^= 1u;
@@ -302,17 +401,22 @@ struct SplitStep {
       if (b == 0) t.start = pipelined ? step_start_event(c, d, 2) : ring_event(c, d, EV_START);
       if (!pipelined) t.stop = ring_event(c, d, EV_A);
       hipStream_t st = cross ? d.a_stream : d.stream;
+      const int si = cross ? 1 : 0;
       if (cross && !join[k] && b % wait_stride == 0) {  // B(b .. b+stride-1) of the last step
         const int64_t w = std::min<int64_t>(b + wait_stride - 1, nb - 1);
-        HIP_TRY(hipStreamWaitEvent(st, ocheck ? d.ord[d.ord_cur ^ 1u].b1[w] : d.bucket_b[w], 0));
+        hipEvent_t e = ocheck ? d.ord[d.ord_cur ^ 1u].b1[w] : spans ? tr[k].prev->b_used[w] : d.bucket_b[w];
+        HIP_TRY(hipStreamWaitEvent(st, e, 0));
+        note_wait(k, si, e);
       }
-      if (pipelined) t.stop = ocheck ? d.ord[d.ord_cur].a1[b] : d.bucket_acc[b];
+      if (pipelined) t.stop = ev_a(k, b);
       if (ocheck) {
         Device::OrderStep &o = d.ord[d.ord_cur];
         HIP_TRY(cbx::launch_order_probe(st, {nullptr, o.pa[b]}));
         o.a1[b] = t.stop;  // with timing on, A always carries a stop event (the pool's or the ring's)
       }
       HIP_TRY(cbx::launch_sma_accumulate(offset_args(args[k], start_of(b), len_of(b)), b == 0, cfg, st, t));
+      if (spans) tr[k].slot->a_used[b] = t.stop;
+      note_dispatch(k, si, Device::SPAN_A, t.stop, b == 0 ? t.start : nullptr);
     }
     return CBX_OK;
   }
@@ -328,7 +432,9 @@ struct SplitStep {
       for (size_t k = 0; k < c->devs.size(); ++k) {
         Device &d = c->devs[k];
         HIP_TRY(hipSetDevice(d.hip_id));
-        HIP_TRY(hipStreamWaitEvent(d.comm_stream, ocheck ? d.ord[d.ord_cur].a1[wait_acc] : d.bucket_acc[wait_acc], 0));
+        hipEvent_t e = ev_a(k, wait_acc);
+        HIP_TRY(hipStreamWaitEvent(d.comm_stream, e, 0));
+        note_wait(k, 2, e);
       }
     }
     for (size_t k = 0; ocheck && k < c->devs.size(); ++k) {
@@ -400,7 +506,8 @@ struct SplitStep {
       for (size_t k = 0; k < c->devs.size(); ++k) {
         Device &d = c->devs[k];
         HIP_TRY(hipSetDevice(d.hip_id));
-        HIP_TRY(hipEventRecord(d.bucket_red[b], d.comm_stream));
+        HIP_TRY(hipEventRecord(ev_red(k, b), d.comm_stream));
+        note_dispatch(k, 2, Device::SPAN_COLL, ev_red(k, b), nullptr);
       }
     }
     return CBX_OK;
@@ -411,7 +518,10 @@ struct SplitStep {
     for (size_t k = 0; k < c->devs.size(); ++k) {
       Device &d = c->devs[k];
       HIP_TRY(hipSetDevice(d.hip_id));
-      if (pipelined) HIP_TRY(hipStreamWaitEvent(d.stream, d.bucket_red[b], 0));
+      if (pipelined) {
+        HIP_TRY(hipStreamWaitEvent(d.stream, ev_red(k, b), 0));
+        note_wait(k, 0, ev_red(k, b));
+      }
       cbx::LaunchConfig cfg = c->apply_cfg;
       cfg.num_cus = d.num_cus;
       cbx::Timing t;
@@ -426,7 +536,8 @@ struct SplitStep {
         a.decision = d.decision + (d.cross_parity & 1u);
       }
       const bool in_dispatch = cross && !t.stop;
-      if (in_dispatch) t.stop = ocheck ? d.ord[d.ord_cur].b1[b] : d.bucket_b[b];
+      if (in_dispatch) t.stop = ocheck ? d.ord[d.ord_cur].b1[b] : spans ? tr[k].slot->b[b] : d.bucket_b[b];
+      if (spans && !t.stop) t.stop = tr[k].slot->b[b];  // every B stops an event of its own for its span
       if (ocheck) {
         Device::OrderStep &o = d.ord[d.ord_cur];
         HIP_TRY(cbx::launch_order_probe(d.stream, {nullptr, o.pb[b]}));
@@ -434,7 +545,9 @@ struct SplitStep {
         o.b1[b] = t.stop;
       }
       HIP_TRY(cbx::launch_sma_apply(a, mom && !rsag, cfg, d.stream, t));
-      if (cross && !in_dispatch) HIP_TRY(hipEventRecord(d.bucket_b[b], d.stream));
+      if (cross && !in_dispatch && !spans) HIP_TRY(hipEventRecord(d.bucket_b[b], d.stream));
+      if (spans) tr[k].slot->b_used[b] = t.stop;  // the last B's is the ring's stop event
+      note_dispatch(k, 0, Device::SPAN_B, t.stop, nullptr);
     }
     return CBX_OK;
   }
@@ -472,12 +585,20 @@ struct SplitStep {
       for (; applied < nb; ++applied) TRY(apply(applied));
     }
     for (Device &d : c->devs) {
+      if (spans) {
+        d.pending_span = d.span_pos;
+        d.span_last = d.span_pos;
+        d.span_pos = (d.span_pos + 1) % Device::kSpanRing;
+      } else {
+        d.span_last = -1;
+      }
       ring_advance(c, d, pipelined ? 2 : 1);
       d.cross_valid = cross;
       if (cross) {
         d.cross_nb = nb;
         d.cross_foreign = foreign;
         d.cross_parity ^= 1u;
+        d.cross_spans = spans;
       }
     }
     c->last_step_split = true;
@@ -495,7 +616,7 @@ int sma_step(cbx_context *c, int first) {
     copies_total += cp;
   }
 
-  TRY(ensure_one_rank_comm(c));
+  if (c->G > 1 ? c->allreduce_algo != CBX_ALLREDUCE_PEER : c->force_split) TRY(ensure_comms(c));
   if (c->allreduce_algo == CBX_ALLREDUCE_PEER && c->G > 1) {
     TRY(sma_step_peer(c, args, mom));
   } else if (c->G == 1 && !c->force_split) {
@@ -738,7 +859,7 @@ int sma_step_staged(cbx_context *c, int first, int buckets) {
     TRY(build_args(c, c->devs[k], first, args[k], &cp));
     copies_total += cp;
   }
-  TRY(ensure_one_rank_comm(c));
+  if (c->G > 1 || c->force_split) TRY(ensure_comms(c));
   TRY(alloc_host_mirror(c));
   if (c->staging_mode == CBX_STAGING_ZEROCOPY) {
     TRY(sma_step_staged_zerocopy(c, first, buckets, args, copies_total, mom));
@@ -869,12 +990,7 @@ int ssgd_step(cbx_context *c, int first) {
   const float ratio = (float)(1.0 / (double)(float)c->model.wpc);  // synchronoussgd.c:55
   const bool mom = c->has_last && c->model.conf.momentum > 0;        // :64
   const bool split = c->G > 1 || c->force_split;
-  if (split && c->G == 1 && c->devs[0].comm == nullptr) {
-    Device &d = c->devs[0];
-    HIP_TRY(hipSetDevice(d.hip_id));
-    int dev = d.hip_id;
-    NCCL_TRY(ncclCommInitAll(&d.comm, 1, &dev));
-  }
+  if (split) TRY(ensure_comms(c));
   std::vector<cbx::SsgdArgs> args(c->devs.size());
   for (size_t k = 0; k < c->devs.size(); ++k) {
     Device &d = c->devs[k];

@@ -14,7 +14,7 @@ from __future__ import annotations
 import os
 from typing import Callable, Optional, Tuple
 
-from ._abi import ALLREDUCE_RCCL, ALLREDUCE_RSAG
+from ._abi import ALLREDUCE_PEER, ALLREDUCE_RCCL, ALLREDUCE_RSAG
 
 
 def env_rank() -> Tuple[int, int, int]:
@@ -71,7 +71,8 @@ def max_over_ranks(value: float, world: int) -> float:
 
 def tune_buckets(gpu, n: int, world: int, step: Callable[[], None], candidates=(1, 2, 4, 8),
                  steps: int = 10, warmup: int = 2, modes=(0, 1), strides=(1, 2, 4), passes: int = 2,
-                 group_candidates=(2, 4), progress: Optional[Callable[[str], None]] = None):
+                 group_candidates=(2, 4), progress: Optional[Callable[[str], None]] = None,
+                 ndev: Optional[int] = None, peer: bool = False):
     """Pick the configuration of the G > 1 pipeline (kernel A / collective /
     kernel B per bucket) by timing each candidate on the live communicator,
     the way a runtime tunes itself in its warm-up.
@@ -102,6 +103,10 @@ def tune_buckets(gpu, n: int, world: int, step: Callable[[], None], candidates=(
     best pass, so one noisy sample (a few percent on one GPU) does not decide.
 
     ``progress`` (if given) receives one line per timed candidate.
+    ``ndev`` is the number of GPUs (default ``world``: one process per GPU);
+    with one process over every GPU (``peer``), the peer-read form
+    (``ALLREDUCE_PEER``: no RCCL pass, no buckets) is timed as one more
+    candidate, key "peer".
 
     Returns (bucket_elements, mode, stride, group, algorithm, {key: ms_per_step})
     with keys "<buckets>/<mode>" for stride 1, "<buckets>/<mode>/s<stride>",
@@ -129,12 +134,20 @@ def tune_buckets(gpu, n: int, world: int, step: Callable[[], None], candidates=(
     def elems_of(nb):
         return (1 << 62) if nb <= 1 else max(1, -(-n // nb))
 
+    G = world if ndev is None else ndev
     algos = [ALLREDUCE_RCCL]
-    if 1 < world <= 16 and 1024 % world == 0:
+    if 1 < G <= 16 and 1024 % G == 0:
         algos.append(ALLREDUCE_RSAG)
     gpu.set_allreduce_group(1)
     results = {}
     for _ in range(max(1, passes)):
+        if peer and 1 < G <= 16:
+            gpu.set_allreduce_algorithm(ALLREDUCE_PEER)
+            ms = timed_steps()
+            key = (1, 0, 1, ALLREDUCE_PEER)
+            results[key] = min(ms, results.get(key, ms))
+            if progress:
+                progress(f"tune {tuning_key(*key)}: {ms:.4f} ms/step")
         for algo in algos:
             gpu.set_allreduce_algorithm(algo)
             for nb in candidates:
@@ -158,7 +171,7 @@ def tune_buckets(gpu, n: int, world: int, step: Callable[[], None], candidates=(
     # later collective starts.  Over xGMI the later start may cost more than
     # the waits save, so it is timed, not assumed.
     group = 1
-    groups = [grp for grp in group_candidates if 1 < grp < nb]
+    groups = [grp for grp in group_candidates if 1 < grp < nb and algorithm != ALLREDUCE_PEER]
     if groups:
         timed = {1: results[best]}
         for _ in range(max(1, passes)):
@@ -176,6 +189,8 @@ def tune_buckets(gpu, n: int, world: int, step: Callable[[], None], candidates=(
 
 
 def tuning_key(nb: int, mode: int, stride: int = 1, algo: int = ALLREDUCE_RCCL) -> str:
+    if algo == ALLREDUCE_PEER:
+        return "peer"
     key = f"{nb}/{mode}" if stride == 1 else f"{nb}/{mode}/s{stride}"
     return key + ("/rsag" if algo == ALLREDUCE_RSAG else "")
 

@@ -321,7 +321,14 @@ int cbx_check_order (cbx_context *ctx);
 int cbx_last_timing (cbx_context *ctx, int local, float *ms);
 /* Per-launch history of the last steps (up to 1024) on local device `local`:
  * `which` is CBX_T_KERNEL, CBX_T_ALLREDUCE, CBX_T_APPLY or CBX_T_STEP; fills
- * ms[0..count) oldest first and returns count.                             */
+ * ms[0..count) oldest first and returns count.  For a pipelined split step
+ * (2..64 buckets, order check off; the last 64 such steps) KERNEL, ALLREDUCE
+ * and APPLY are the step's summed busy spans of kernels A, collectives and
+ * kernels B: each dispatch's stop minus the latest event that bounded its
+ * start (the previous dispatch on its stream, the events the stream waited
+ * on), so each includes its dispatch latency and any sharing of the GPU
+ * with the other streams' work.  Both this and cbx_last_timing report -1
+ * for a span a step did not keep.                                         */
 int cbx_timing_history (cbx_context *ctx, int local, int which, float *ms, int max);
 /* Launch geometry for the SMA kernels: threads per block (multiple of 64),
  * workgroups per CU for the grid-stride loop (0 = one float4 per thread),
@@ -349,7 +356,8 @@ int cbx_set_apply_kernel_config (cbx_context *ctx, int block, int unroll, int wa
  * of `bucket_elements` floats; 0 (default) = 8 buckets when G > 1, one at
  * G = 1; a value >= n = one bucket, all in order on the sync stream.  With
  * more than one bucket the all-reduce of bucket k runs on a second stream
- * beside kernel A of bucket k+1, and only CBX_T_STEP is timed per step.  */
+ * beside kernel A of bucket k+1, and the kernels are timed as summed busy
+ * spans (cbx_timing_history).                                             */
 int cbx_set_bucket_elements (cbx_context *ctx, long long bucket_elements);
 /* How the bucketed pipeline overlaps (G > 1, or forced split): 0 (default)
  * within a step only; 1 also across steps: kernels A run on their own

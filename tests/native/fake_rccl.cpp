@@ -31,6 +31,11 @@
 //                     the stated G > 1 tolerance and the
 //                     cross-rank identity of z (sma.c:168-174).
 //
+// $FAKE_RCCL_NOOP=1 (read when the communicator is created): every
+// collective returns at once and moves nothing -- results are wrong.  Only
+// for timing the host side of the library's enqueue without a collective's
+// own cost (scripts/host_enqueue_multidev.py); no parity test sets it.
+//
 // Built by scripts/build_fake_rccl.sh as tests/native/libfakerccl.so; a
 // variant of the library linked against it (libcrossbow_sma_fakerccl.so) is
 // what tests/test_gpu_multirank.py and tests/test_gpu_multidevice.py load.
@@ -58,6 +63,7 @@ struct ncclComm {
   int rank = 0;
   int device = 0;
   bool ring = false;
+  bool noop = false;  // $FAKE_RCCL_NOOP: collectives move nothing (host-side timing only)
   std::string tag;  // hex of the unique id
   unsigned long long seq = 0;
   Clique *clique = nullptr;  // single-process communicators (ncclCommInitAll, ndev > 1)
@@ -73,6 +79,11 @@ namespace {
 // Elements per ring chunk: small enough that a few-thousand-element test
 // buffer spans several chunks, so every start rank occurs.
 constexpr size_t kRingChunk = 1024;
+
+bool noop_from_env() {
+  const char *o = std::getenv("FAKE_RCCL_NOOP");
+  return o && std::strcmp(o, "1") == 0;
+}
 
 bool ring_order_from_env() {
   const char *o = std::getenv("FAKE_RCCL_ORDER");
@@ -238,6 +249,7 @@ ncclResult_t run_ranked(int kind, const void *send, void *recv, size_t count, nc
 ncclResult_t enqueue(int kind, const void *send, void *recv, size_t count, ncclDataType_t type, ncclComm_t c,
                      hipStream_t stream) {
   if (!c || type != ncclFloat) return ncclInvalidArgument;
+  if (c->noop) return ncclSuccess;
   if (c->clique) {
     if (g_depth == 0) return ncclInvalidUsage;
     g_ops.push_back(PendingOp{kind, send, recv, count, c, stream});
@@ -269,6 +281,7 @@ ncclResult_t ncclCommInitRank(ncclComm_t *comm, int nranks, ncclUniqueId id, int
   c->nranks = nranks;
   c->rank = rank;
   c->ring = ring_order_from_env();
+  c->noop = noop_from_env();
   (void)hipGetDevice(&c->device);
   c->tag = hex_tag(id);
   *comm = c;
@@ -284,6 +297,7 @@ ncclResult_t ncclCommInitAll(ncclComm_t *comm, int ndev, const int *devlist) {
     c->rank = r;
     c->device = devlist ? devlist[r] : r;
     c->ring = ring_order_from_env();
+    c->noop = noop_from_env();
     c->tag = "local";
     c->clique = q;
     if (q) q->comms.push_back(c);

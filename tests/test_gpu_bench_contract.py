@@ -54,6 +54,35 @@ def test_bench_two_ranks_through_the_launcher_prints_one_json_line():
     d = _one_line(p.stdout)
     _check(d, 2)
     assert d["config"]["parallelism"] == "sma-dp2" and "allreduce" in d and "rehearsal" in d
+    assert d["config"]["process_form"] == "per-rank"
+    # N > 1: the roofline of the kernels as they ran in the timed region
+    # (summed busy spans beside the collectives), the calibration's apart
+    r = d["roofline"]
+    assert r["timed_in"].startswith("timed region") and r["launches"] >= 3
+    assert 0 < r["apply_kernel"]["frac"] < 1 and 0 < r["a_plus_b"]["frac"] < 1
+    assert r["collective_busy_ms_mean"] > 0
+    assert d["roofline_unpipelined"]["timed_in"].startswith("calibration")
+    # RCCL's own tuning choices, parsed from its TUNING log
+    t = d["allreduce"]["rccl_tuning"]
+    assert isinstance(t, list) and t, d["allreduce"]
+    assert all(e["collective"] and e["algo"] and e["proto"] and e["bytes"] > 0 and e["calls"] > 0 for e in t)
+    assert d["host"]["enqueue_ms_per_step_timed"] > 0 and d["host"]["devices_per_process"] == 1
+
+
+@pytest.mark.timeout(300)
+def test_bench_single_process_two_devices_one_gpu():
+    """The reference's own multi-GPU topology: one process over N devices
+    (cbx_init -> ncclCommInitAll), here two devices that are both device 0,
+    so the all-reduce is the peer-read form (RCCL refuses a repeated device)."""
+    cmd = [sys.executable, "bench.py", "--gpus", "2", "--single-process", "--rehearse-one-gpu"] + QUICK
+    p = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=280)
+    assert p.returncode == 0, p.stderr[-2000:]
+    d = _one_line(p.stdout)
+    _check(d, 2)
+    assert d["config"]["process_form"] == "single" and d["config"]["allreduce_algorithm"] == "peer-read two-shot"
+    assert d["host"]["devices_per_process"] == 2 and d["host"]["enqueue_ms_per_step_idle_gpu"] > 0
+    assert d["roofline"]["timed_in"].startswith("timed region") and "roofline_unpipelined" in d
+    assert "rehearsal" in d
 
 
 @pytest.mark.timeout(300)

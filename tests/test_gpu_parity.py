@@ -222,24 +222,42 @@ def test_split_pipeline_many_buckets_two_streams(bucket):
     _run(1_000_003, 2, 0.5, 0.9, split=True, bucket=bucket, steps=3)
 
 
-def test_pipelined_timing_spans():
+@pytest.mark.parametrize("mode", [0, 1])
+def test_pipelined_timing_spans(mode):
+    """Pipelined steps time their kernels A, collectives and kernels B as
+    summed busy spans (each dispatch: its stop minus the latest event that
+    bounded its start), so N > 1 benches report the kernels as they ran in
+    the timed region; beyond 64 buckets the step keeps no spans (-1)."""
     from crossbow_amd import _lib
     n, R = 200_000, 2
     g = make_gpu(n, R, 0.1, 0.9)
     try:
         g.set_force_split(True)
-        g.set_bucket_elements(16_384)
+        g.set_bucket_elements(16_384)  # 13 buckets
+        g.set_pipeline_mode(mode)
         g.fill_synthetic(7)
         g.set_timing(True)
-        for c in range(3):
+        for c in range(6):
             g.lockAny()
             g.synchronise(0, c, 0, False)
             g.unlockAny()
         g.wait()
         t = g.last_timing(0)
-        assert t[_lib.T_KERNEL] == -1 and t[_lib.T_ALLREDUCE] == -1 and t[_lib.T_STEP] > 0
-        assert all(x == -1 for x in g.timing_history(_lib.T_KERNEL))
-        assert all(x > 0 for x in g.timing_history(_lib.T_STEP))
+        assert t[_lib.T_KERNEL] > 0 and t[_lib.T_ALLREDUCE] > 0 and t[_lib.T_APPLY] > 0 and t[_lib.T_STEP] > 0
+        hk = g.timing_history(_lib.T_KERNEL)
+        hb = g.timing_history(_lib.T_APPLY)
+        hs = g.timing_history(_lib.T_STEP)
+        assert len(hk) == 6 and all(x > 0 for x in hk) and all(x > 0 for x in hb) and all(x > 0 for x in hs)
+        if mode == 0:  # one stream: A and B never overlap, so their busy time fits in the step
+            assert all(k + b <= s * 1.001 + 0.002 for k, b, s in zip(hk, hb, hs)), (hk, hb, hs)
+        g.set_bucket_elements(1024)  # 196 buckets: more than the span records keep
+        for c in range(6, 8):
+            g.lockAny()
+            g.synchronise(0, c, 0, False)
+            g.unlockAny()
+        g.wait()
+        t = g.last_timing(0)
+        assert t[_lib.T_KERNEL] == -1 and t[_lib.T_APPLY] == -1 and t[_lib.T_STEP] > 0
         g.set_bucket_elements(1 << 40)
         g.lockAny()
         g.synchronise(0, 4, 0, False)
