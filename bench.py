@@ -509,8 +509,8 @@ def main():
     except (OSError, ValueError) as e:
         traffic_note = f"unavailable: {e}"
 
-    def roofline(kern, timed_in, kbytes=kernel_bytes, kernel=kname):
-        kern_ms = statistics.mean(kern)
+    def roofline(kern, timed_in, kbytes=kernel_bytes, kernel=kname, mean_ms=None):
+        kern_ms = statistics.mean(kern) if mean_ms is None else mean_ms
         achieved = kbytes / (kern_ms * 1e-3) / 1e9
         return {"bound": "hbm", "kernel": kernel, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "alg_bytes_per_launch": kbytes,
@@ -527,14 +527,12 @@ def main():
         unpiped = roofline(calib["kernel"], "calibration steps (one bucket, in order)")
         if spans is not None:
             a_ms, coll_ms, b_ms = spans
+            # the slowest rank's mean kernel time sets the roofline (max over ranks)
             result["roofline"] = roofline(
                 a_ms, "timed region: per step, the summed busy spans of kernel A's dispatches (each its stop minus "
                       "the latest event bounding its start: an upper bound incl. dispatch latency), beside the "
-                      f"collectives; {'every local device, ' if nlocal > 1 else ''}max over ranks via the slowest")
-            # max over ranks: the slowest rank's kernel time sets the roofline
-            worst = D.max_over_ranks(statistics.mean(a_ms), world)
-            if worst > statistics.mean(a_ms):
-                result["roofline"] = roofline([worst], result["roofline"]["timed_in"])
+                      f"collectives; {'mean over the local devices, ' if nlocal > 1 else ''}slowest rank",
+                mean_ms=D.max_over_ranks(statistics.mean(a_ms), world))
             result["roofline"]["apply_kernel"] = roofline(b_ms, "timed region (summed busy spans of kernel B)",
                                                           b_bytes, "sma_apply_kernel")
             ab = [x + y for x, y in zip(a_ms, b_ms)]

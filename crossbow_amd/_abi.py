@@ -137,6 +137,7 @@ SIGNATURES = {
     "cbx_set_staging_mode": (_I, [_P, _I]),
     "cbx_set_bucket_elements": (_I, [_P, _c.c_longlong]),
     "cbx_set_force_split": (_I, [_P, _I]),
+    "cbx_set_enqueue_threads": (_I, [_P, _I]),
     "cbx_set_order_check": (_I, [_P, _I]),
     "cbx_check_order": (_I, [_P]),
     "cbx_fill_synthetic": (_I, [_P, _c.c_ulonglong]),

@@ -176,6 +176,7 @@ int cbx_init_rank(cbx_context **out, int device, int nranks, int rank, const uns
 
 int cbx_free(cbx_context *c) {
   if (!c) return CBX_OK;
+  c->pool.reset();  // the enqueue threads are idle between calls
   for (Replica *r : c->replicas) {
     if (r && r->client && r->local >= 0) {
       (void)hipSetDevice(c->devs[r->local].hip_id);
@@ -1563,6 +1564,13 @@ int cbx_set_allreduce_algorithm(cbx_context *c, int algorithm) {
   if (algorithm == CBX_ALLREDUCE_PEER && c->G > cbx::kMaxDevices)
     return fail(CBX_ERR_UNSUPPORTED, "the peer-read all-reduce takes at most %d devices", cbx::kMaxDevices);
   c->allreduce_algo = algorithm;
+  return CBX_OK;
+}
+
+int cbx_set_enqueue_threads(cbx_context *c, int mode) {
+  TRY(check_ctx(c));
+  if (mode < -1 || mode > 1) return fail(CBX_ERR_INVALID, "enqueue threads must be -1 (auto), 0 or 1");
+  c->enqueue_threads = mode;
   return CBX_OK;
 }
 

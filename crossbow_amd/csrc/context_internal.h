@@ -19,12 +19,16 @@
 #include <algorithm>
 #include <atomic>
 #include <cmath>
+#include <condition_variable>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
+#include <functional>
 #include <map>
 #include <memory>
+#include <mutex>
 #include <string>
+#include <thread>
 #include <utility>
 #include <vector>
 
@@ -75,6 +79,113 @@ struct TraceRange {
     int rc_ = (expr);        \
     if (rc_ < 0) return rc_; \
   } while (0)
+
+// ---------------------------------------------------------------------------
+// One enqueue thread per local device (cbx_set_enqueue_threads).  The
+// reference drives every GPU's sync step from its one ResultCollector thread
+// (sma.c:42-128, common.c:14-54); at 8 devices and 8 buckets the HIP and RCCL
+// calls of a step then take the host longer than the GPUs take to run them
+// (profiles/r03/host_enqueue_single_thread.jsonl: 1.1 ms before RCCL's own
+// enqueue cost, against ~0.6 ms of device time).  run(n, fn) calls fn(k) for
+// every k < n, k = 0 on the calling thread and the others on workers that
+// live as long as the context, and returns when all have finished (the first
+// failure's code and message, in device order).  NCCL / RCCL take one thread
+// per device with ncclCommInitAll's communicators: each thread issues its own
+// device's collectives.
+// ---------------------------------------------------------------------------
+class EnqueuePool {
+ public:
+  EnqueuePool() = default;
+  EnqueuePool(const EnqueuePool &) = delete;
+  EnqueuePool &operator=(const EnqueuePool &) = delete;
+  ~EnqueuePool() {
+    {
+      std::lock_guard<std::mutex> l(m_);
+      stop_ = true;
+      gen_.fetch_add(1, std::memory_order_release);
+    }
+    cv_start_.notify_all();
+    for (std::thread &t : threads_) t.join();
+  }
+
+  int run(int n, const std::function<int(int)> &fn) {
+    while ((int)threads_.size() < n - 1) {
+      const int k = (int)threads_.size() + 1;
+      threads_.emplace_back([this, k] { worker(k); });
+    }
+    rc_.assign(n, 0);
+    err_.assign(n, std::string());
+    {
+      std::lock_guard<std::mutex> l(m_);
+      job_ = &fn;
+      n_ = n;
+      pending_.store(n - 1, std::memory_order_relaxed);
+      gen_.fetch_add(1, std::memory_order_release);
+    }
+    cv_start_.notify_all();
+    rc_[0] = fn(0);
+    if (rc_[0] < 0) err_[0] = g_last_error;
+    // Wait for the workers: spin a little (a step's enqueue is ~0.1 ms), then sleep.
+    for (int spin = 0; pending_.load(std::memory_order_acquire) != 0; ++spin) {
+      if (spin < 4000) {
+        sched_yield();
+        continue;
+      }
+      std::unique_lock<std::mutex> l(m_);
+      cv_done_.wait(l, [this] { return pending_.load(std::memory_order_acquire) == 0; });
+    }
+    job_ = nullptr;
+    for (int k = 0; k < n; ++k)
+      if (rc_[k] < 0) {
+        g_last_error = err_[k];
+        return rc_[k];
+      }
+    return CBX_OK;
+  }
+
+ private:
+  void worker(int k) {
+    uint64_t seen = 0;
+    for (;;) {
+      // Spin briefly on the generation (steps come back to back), then sleep.
+      uint64_t g = gen_.load(std::memory_order_acquire);
+      for (int spin = 0; g == seen && spin < 2000; ++spin) {
+        sched_yield();
+        g = gen_.load(std::memory_order_acquire);
+      }
+      const std::function<int(int)> *job;
+      int n;
+      {
+        std::unique_lock<std::mutex> l(m_);
+        if (g == seen) cv_start_.wait(l, [&] { return gen_.load(std::memory_order_acquire) != seen; });
+        if (stop_) return;
+        // generation, job and count change together under the lock
+        seen = gen_.load(std::memory_order_acquire);
+        job = job_;
+        n = n_;
+      }
+      if (job && k < n) {
+        rc_[k] = (*job)(k);
+        if (rc_[k] < 0) err_[k] = g_last_error;
+        if (pending_.fetch_sub(1, std::memory_order_acq_rel) == 1) {
+          std::lock_guard<std::mutex> l(m_);
+          cv_done_.notify_all();
+        }
+      }
+    }
+  }
+
+  std::vector<std::thread> threads_;
+  std::mutex m_;
+  std::condition_variable cv_start_, cv_done_;
+  std::atomic<uint64_t> gen_{0};
+  std::atomic<int> pending_{0};
+  bool stop_ = false;
+  const std::function<int(int)> *job_ = nullptr;
+  int n_ = 0;
+  std::vector<int> rc_;
+  std::vector<std::string> err_;
+};
 
 // ---------------------------------------------------------------------------
 // Solver configuration, clib-multigpu/solverconfiguration.{h,c}
@@ -377,9 +488,28 @@ struct cbx_context {
   // than the barrier path itself: a cross-step pipelined step then joins the
   // whole sync stream instead of waiting bucket by bucket.
   std::atomic<unsigned long long> foreign_ops{0};
+  // One process over several local devices: each device's share of a barrier
+  // step is enqueued by a thread of its own (cbx_set_enqueue_threads; -1 auto
+  // = on with two or more local devices, 0 = the reference's one thread).
+  int enqueue_threads = -1;
+  std::unique_ptr<cbx::host::EnqueuePool> pool;
 };
 
 namespace cbx::host {
+
+// Whether a barrier step enqueues each local device's work on its own thread.
+inline bool threaded(const cbx_context *c) { return c->devs.size() > 1 && c->enqueue_threads != 0; }
+
+// Runs fn(k) for every local device k, on one thread per device when the
+// context enqueues threaded, else in device order on this thread.
+inline int for_devices(cbx_context *c, const std::function<int(int)> &fn) {
+  if (!threaded(c)) {
+    for (int k = 0; k < (int)c->devs.size(); ++k) TRY(fn(k));
+    return CBX_OK;
+  }
+  if (!c->pool) c->pool.reset(new EnqueuePool());
+  return c->pool->run((int)c->devs.size(), fn);
+}
 
 // ---------------------------------------------------------------------------
 // Arena layout helpers

@@ -48,6 +48,7 @@ static jint fatal_or (int rc) {
  *   CBX_CROSS_WAIT_STRIDE  1..4096              (cbx_set_cross_wait_stride)
  *   CBX_ALLREDUCE_GROUP    1..4096              (cbx_set_allreduce_group)
  *   CBX_STAGING            zerocopy | dma       (cbx_set_staging_mode)
+ *   CBX_ENQUEUE_THREADS    -1 | 0 | 1           (cbx_set_enqueue_threads)
  * bench.py's warm-up tuner (crossbow_amd/dist.py) prints the values it
  * chose for a node in its JSON config. */
 static long long env_int (const char *name, int *present) {
@@ -94,6 +95,8 @@ static void configure_from_env (void) {
 	if (on) fatal_or (cbx_set_cross_wait_stride (theGPU, v < 0 || v > 4096 ? -1 : (int) v));
 	v = env_int ("CBX_ALLREDUCE_GROUP", &on);
 	if (on) fatal_or (cbx_set_allreduce_group (theGPU, v < 0 || v > 4096 ? -1 : (int) v));
+	v = env_int ("CBX_ENQUEUE_THREADS", &on);
+	if (on) fatal_or (cbx_set_enqueue_threads (theGPU, v < -1 || v > 1 ? -2 : (int) v));
 }
 
 /* GPU.c:21-63.  Thread-count / core-offset arguments configure the reference's

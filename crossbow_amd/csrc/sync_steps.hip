@@ -149,15 +149,19 @@ int sma_step_peer(cbx_context *c, std::vector<cbx::SmaArgs> &args, bool mom) {
     p.ctrl_in[h] = base_ctrl(c->devs[h], CBX_BUF_GRADIENT);
     p.D[h] = reinterpret_cast<const cbx::v4f *>(base_dev(c, c->devs[h], CBX_BUF_DIFF));
   }
-  for (int k = 0; k < G; ++k) {
+  // Three phases, each on every device before the next (a device waits on
+  // the others' events, which must be recorded first); with enqueue threads
+  // each phase runs one thread per device.
+  TRY(for_devices(c, [&](int k) -> int {
     Device &d = c->devs[k];
     HIP_TRY(hipSetDevice(d.hip_id));
     cbx::LaunchConfig cfg = c->cfg;
     cfg.num_cus = d.num_cus;
     HIP_TRY(cbx::launch_sma_accumulate(args[k], true, cfg, d.stream, {ring_event(c, d, EV_START), ring_event(c, d, EV_A)}));
     HIP_TRY(hipEventRecord(d.peer_a, d.stream));
-  }
-  for (int k = 0; k < G; ++k) {
+    return CBX_OK;
+  }));
+  TRY(for_devices(c, [&](int k) -> int {
     Device &d = c->devs[k];
     HIP_TRY(hipSetDevice(d.hip_id));
     for (int h = 0; h < G; ++h)
@@ -173,8 +177,9 @@ int sma_step_peer(cbx_context *c, std::vector<cbx::SmaArgs> &args, bool mom) {
     cfg.num_cus = d.num_cus;
     HIP_TRY(cbx::launch_sma_peer_reduce(r, cfg, d.stream, {nullptr, ring_event(c, d, EV_AR)}));
     HIP_TRY(hipEventRecord(d.peer_r, d.stream));
-  }
-  for (int k = 0; k < G; ++k) {
+    return CBX_OK;
+  }));
+  TRY(for_devices(c, [&](int k) -> int {
     Device &d = c->devs[k];
     HIP_TRY(hipSetDevice(d.hip_id));
     for (int h = 0; h < G; ++h)
@@ -182,9 +187,11 @@ int sma_step_peer(cbx_context *c, std::vector<cbx::SmaArgs> &args, bool mom) {
     cbx::LaunchConfig cfg = c->apply_cfg;
     cfg.num_cus = d.num_cus;
     HIP_TRY(cbx::launch_sma_peer_apply(args[k], p, mom, cfg, d.stream, {nullptr, step_stop_event(c, d, EV_B)}));
+    d.span_last = -1;
     ring_advance(c, d, 1);
     d.cross_valid = false;
-  }
+    return CBX_OK;
+  }));
   c->last_step_split = true;
   return CBX_OK;
 }
@@ -312,9 +319,8 @@ struct SplitStep {
     return CBX_OK;
   }
 
-  // Bucket geometry, per-bucket events, the cross-step join decision, and a
-  // fresh set of stream-order timestamps when the check is on.
-  int prepare() {
+  // Bucket geometry and the step's modes, for every device.
+  int prepare_common() {
     const int64_t pad = cbx::kPadFloat4;
     b4 = c->n4;
     if (c->bucket_elems > 0) {
@@ -334,7 +340,13 @@ struct SplitStep {
     foreign = c->foreign_ops.load(std::memory_order_acquire);
     join.assign(c->devs.size(), 1);
     tr.assign(c->devs.size(), Track());
-    for (size_t k = 0; k < c->devs.size(); ++k) {
+    return CBX_OK;
+  }
+
+  // Device k's per-bucket events, its cross-step join decision, its span
+  // slot, and a fresh set of stream-order timestamps when the check is on.
+  int prepare_device(size_t k) {
+    {
       Device &d = c->devs[k];
       HIP_TRY(hipSetDevice(d.hip_id));
       if (pipelined) {
@@ -390,9 +402,9 @@ struct SplitStep {
     return CBX_OK;
   }
 
-  // Kernel A (Phase A) of bucket b on every device.
-  int accumulate(int64_t b) {
-    for (size_t k = 0; k < c->devs.size(); ++k) {
+  // Kernel A (Phase A) of bucket b on devices [k0, k1).
+  int accumulate(int64_t b, size_t k0, size_t k1) {
+    for (size_t k = k0; k < k1; ++k) {
       Device &d = c->devs[k];
       HIP_TRY(hipSetDevice(d.hip_id));
       cbx::LaunchConfig cfg = c->cfg;
@@ -426,10 +438,10 @@ struct SplitStep {
   // the comm stream first waits for kernel A of that bucket (-1: no wait; an
   // earlier collective of the same group already waited on a later bucket,
   // which implies this one: A runs in order).
-  int collective(int64_t b, bool on_comm, int64_t wait_acc) {
+  int collective(int64_t b, bool on_comm, int64_t wait_acc, size_t k0, size_t k1) {
     const int64_t start = start_of(b), len = len_of(b);
     if (on_comm && wait_acc >= 0 && !c->fault_skip_comm_wait) {
-      for (size_t k = 0; k < c->devs.size(); ++k) {
+      for (size_t k = k0; k < k1; ++k) {
         Device &d = c->devs[k];
         HIP_TRY(hipSetDevice(d.hip_id));
         hipEvent_t e = ev_a(k, wait_acc);
@@ -437,7 +449,7 @@ struct SplitStep {
         note_wait(k, 2, e);
       }
     }
-    for (size_t k = 0; ocheck && k < c->devs.size(); ++k) {
+    for (size_t k = k0; ocheck && k < k1; ++k) {
       Device &d = c->devs[k];
       HIP_TRY(hipSetDevice(d.hip_id));
       HIP_TRY(cbx::launch_order_probe(on_comm ? d.comm_stream : d.stream, {nullptr, d.ord[d.ord_cur].c0[b]}));
@@ -450,7 +462,7 @@ struct SplitStep {
       // rides a 64-float all-reduce grouped with bucket 0's reduce-scatter.
       const int64_t sh4 = len / c->G;
       NCCL_TRY(ncclGroupStart());
-      for (size_t k = 0; k < c->devs.size(); ++k) {
+      for (size_t k = k0; k < k1; ++k) {
         Device &d = c->devs[k];
         HIP_TRY(hipSetDevice(d.hip_id));
         hipStream_t st = on_comm ? d.comm_stream : d.stream;
@@ -463,7 +475,7 @@ struct SplitStep {
       }
       NCCL_TRY(ncclGroupEnd());
       const int gather = mom ? CBX_BUF_LAST : CBX_BUF_DIFF;
-      for (size_t k = 0; mom && k < c->devs.size(); ++k) {
+      for (size_t k = k0; mom && k < k1; ++k) {
         Device &d = c->devs[k];
         HIP_TRY(hipSetDevice(d.hip_id));
         cbx::SmaArgs a = offset_args(args[k], start + d.g * sh4, sh4);
@@ -472,7 +484,7 @@ struct SplitStep {
         HIP_TRY(cbx::launch_sma_shard_momentum(a, cfg, on_comm ? d.comm_stream : d.stream));
       }
       NCCL_TRY(ncclGroupStart());
-      for (size_t k = 0; k < c->devs.size(); ++k) {
+      for (size_t k = k0; k < k1; ++k) {
         Device &d = c->devs[k];
         HIP_TRY(hipSetDevice(d.hip_id));
         float *buf = base_dev(c, d, gather) + start * 4;
@@ -482,7 +494,7 @@ struct SplitStep {
       NCCL_TRY(ncclGroupEnd());
     } else {
       NCCL_TRY(ncclGroupStart());
-      for (size_t k = 0; k < c->devs.size(); ++k) {
+      for (size_t k = k0; k < k1; ++k) {
         Device &d = c->devs[k];
         HIP_TRY(hipSetDevice(d.hip_id));
         const float *src = base_dev(c, d, CBX_BUF_GRADIENT) + start * 4;
@@ -497,13 +509,13 @@ struct SplitStep {
       }
       NCCL_TRY(ncclGroupEnd());
     }
-    for (size_t k = 0; ocheck && k < c->devs.size(); ++k) {
+    for (size_t k = k0; ocheck && k < k1; ++k) {
       Device &d = c->devs[k];
       HIP_TRY(hipSetDevice(d.hip_id));
       HIP_TRY(cbx::launch_order_probe(on_comm ? d.comm_stream : d.stream, {nullptr, d.ord[d.ord_cur].c1[b]}));
     }
     if (on_comm) {
-      for (size_t k = 0; k < c->devs.size(); ++k) {
+      for (size_t k = k0; k < k1; ++k) {
         Device &d = c->devs[k];
         HIP_TRY(hipSetDevice(d.hip_id));
         HIP_TRY(hipEventRecord(ev_red(k, b), d.comm_stream));
@@ -513,9 +525,9 @@ struct SplitStep {
     return CBX_OK;
   }
 
-  // Kernel B (Phase C, + D on copy) of bucket b on every device.
-  int apply(int64_t b) {
-    for (size_t k = 0; k < c->devs.size(); ++k) {
+  // Kernel B (Phase C, + D on copy) of bucket b on devices [k0, k1).
+  int apply(int64_t b, size_t k0, size_t k1) {
+    for (size_t k = k0; k < k1; ++k) {
       Device &d = c->devs[k];
       HIP_TRY(hipSetDevice(d.hip_id));
       if (pipelined) {
@@ -552,16 +564,20 @@ struct SplitStep {
     return CBX_OK;
   }
 
-  int run() {
-    TRY(prepare());
+  // The whole step on devices [k0, k1): every device at once from one
+  // thread (the reference's order, each collective grouped over the range),
+  // or one device per enqueue thread.
+  int run_devices(size_t k0, size_t k1) {
+    for (size_t k = k0; k < k1; ++k) TRY(prepare_device(k));
     if (!pipelined) {
-      TRY(accumulate(0));
-      TRY(collective(0, false, -1));
-      for (Device &d : c->devs) {
+      TRY(accumulate(0, k0, k1));
+      TRY(collective(0, false, -1, k0, k1));
+      for (size_t k = k0; k < k1; ++k) {
+        Device &d = c->devs[k];
         HIP_TRY(hipSetDevice(d.hip_id));
         TRY(mark(c, d, EV_AR));
       }
-      TRY(apply(0));
+      TRY(apply(0, k0, k1));
     } else {
       // Collectives go out in groups of `ar_group` buckets behind a single
       // comm-stream wait on the group's last kernel A (cbx_set_allreduce_group).
@@ -573,18 +589,19 @@ struct SplitStep {
       const int64_t ar_group = std::max(1, c->allreduce_group);
       int64_t applied = 0;
       for (int64_t b = 0; b < nb; ++b) {
-        TRY(accumulate(b));
+        TRY(accumulate(b, k0, k1));
         if ((b + 1) % ar_group != 0 && b != nb - 1) continue;
         const int64_t g0 = b - b % ar_group;
-        for (int64_t j = g0; j <= b; ++j) TRY(collective(j, true, j == g0 ? b : -1));
+        for (int64_t j = g0; j <= b; ++j) TRY(collective(j, true, j == g0 ? b : -1, k0, k1));
         const int64_t upto = cross ? b + 1 : g0;
-        for (; applied < upto; ++applied) TRY(apply(applied));
+        for (; applied < upto; ++applied) TRY(apply(applied, k0, k1));
       }
       // The wait inside apply(nb-1) also joins every earlier collective
       // (comm_stream is in order) back into the sync stream.
-      for (; applied < nb; ++applied) TRY(apply(applied));
+      for (; applied < nb; ++applied) TRY(apply(applied, k0, k1));
     }
-    for (Device &d : c->devs) {
+    for (size_t k = k0; k < k1; ++k) {
+      Device &d = c->devs[k];
       if (spans) {
         d.pending_span = d.span_pos;
         d.span_last = d.span_pos;
@@ -601,6 +618,13 @@ struct SplitStep {
         d.cross_spans = spans;
       }
     }
+    return CBX_OK;
+  }
+
+  int run() {
+    TRY(prepare_common());
+    if (threaded(c)) TRY(for_devices(c, [this](int k) { return run_devices((size_t)k, (size_t)k + 1); }));
+    else TRY(run_devices(0, c->devs.size()));
     c->last_step_split = true;
     return CBX_OK;
   }

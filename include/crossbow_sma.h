@@ -419,6 +419,19 @@ int cbx_set_allreduce_algorithm (cbx_context *ctx, int algorithm);
 #define CBX_STAGING_ZEROCOPY 0
 #define CBX_STAGING_DMA 1
 int cbx_set_staging_mode (cbx_context *ctx, int mode);
+/* One process over several local devices (cbx_init): who enqueues each
+ * device's share of a barrier step (the SMA split and peer-read steps).
+ *   0   one thread, every device in turn, collectives grouped across the
+ *       devices (the reference's ResultCollector thread, common.c:14-54);
+ *   1   one thread per local device, each issuing its own device's kernels
+ *       and collectives (NCCL's thread-per-device use of ncclCommInitAll's
+ *       communicators); the call returns once every device's work is
+ *       enqueued, as before;
+ *  -1   (default) 1 with two or more local devices.
+ * Same work on the same streams in the same per-device order: results are
+ * identical.  At 8 devices and 8 buckets one thread spends longer enqueuing
+ * a step than the GPUs spend running it.          */
+int cbx_set_enqueue_threads (cbx_context *ctx, int mode);
 /* Force the multi-GPU pipeline (kernel A + RCCL all-reduce + kernel B) even
  * at G = 1 (a one-rank communicator), so a single-GPU host exercises it.  */
 int cbx_set_force_split (cbx_context *ctx, int force);

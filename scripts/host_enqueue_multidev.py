@@ -13,7 +13,8 @@ Two library builds, one per process (pass one):
                        cost of everything BUT RCCL's own enqueue (which the
                        per-rank real-RCCL rehearsal measures); G = 1 (forced
                        split), 2, 4, 8 at 1 and 8 buckets, pipeline modes 0/1.
-Per configuration: the median host time of one step (lockAny + synchronise +
+Each at enqueue_threads 0 (one thread, the reference's) and 1 (one thread per
+device, cbx_set_enqueue_threads).  Per configuration: the median host time of one step (lockAny + synchronise +
 unlockAny) enqueued on an idle GPU, the same back to back over the timed
 steps, and the device's step (HIP events; on one GPU every device's work
 shares the card, so it is G x a real GPU's).  JSON lines on stdout.
@@ -31,7 +32,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
-def run(G, buckets, mode, peer, steps=20, warmup=5, force_split=False):
+def run(G, buckets, mode, peer, threads, steps=20, warmup=5, force_split=False):
     from crossbow_amd import SYNC_BSP, UPDATE_SMA, TheGPU, _lib
     from crossbow_amd.variables import MODELS, register
     g = TheGPU()
@@ -46,6 +47,7 @@ def run(G, buckets, mode, peer, steps=20, warmup=5, force_split=False):
     if peer:
         g.set_allreduce_algorithm(_lib.ALLREDUCE_PEER)
     g.set_bucket_elements((1 << 62) if buckets == 1 else -(-n // buckets))
+    g.set_enqueue_threads(threads)
     g.set_pipeline_mode(mode)
     g.fill_synthetic(1)
     g.set_timing(True)
@@ -79,7 +81,7 @@ def run(G, buckets, mode, peer, steps=20, warmup=5, force_split=False):
     dev = statistics.median(g.timing_history(_lib.T_STEP)[-steps:])
     kern = [x for x in g.timing_history(_lib.T_KERNEL)[-steps:] if x > 0]
     g.free()
-    return {"G": G, "buckets": buckets if not peer else None, "pipeline_mode": mode if not peer else None,
+    return {"G": G, "enqueue_threads": threads, "buckets": buckets if not peer else None, "pipeline_mode": mode if not peer else None,
             "form": "peer" if peer else "rccl-noop", "host_enqueue_ms_idle_gpu": round(statistics.median(idle), 4),
             "host_enqueue_ms_back_to_back": round(statistics.median(timed), 4),
             "device_step_ms_one_gpu": round(dev, 4), "wall_ms_per_step": round(wall, 4),
@@ -96,13 +98,14 @@ def main():
         from crossbow_amd import _lib
         _lib.load(os.path.join(ROOT, "tests", "native", "libcrossbow_sma_fakerccl.so"))
     for G in (int(x) for x in a.gs.split(",")):
-        if a.variant == "peer":
-            if G > 1:
-                print(json.dumps(run(G, 1, 0, True)), flush=True)
-            continue
-        for buckets in (1, 8):
-            for mode in ((0,) if buckets == 1 else (0, 1)):
-                print(json.dumps(run(G, buckets, mode, False, force_split=G == 1)), flush=True)
+        for threads in ((0,) if G == 1 else (0, 1)):
+            if a.variant == "peer":
+                if G > 1:
+                    print(json.dumps(run(G, 1, 0, True, threads)), flush=True)
+                continue
+            for buckets in (1, 8):
+                for mode in ((0,) if buckets == 1 else (0, 1)):
+                    print(json.dumps(run(G, buckets, mode, False, threads, force_split=G == 1)), flush=True)
 
 
 if __name__ == "__main__":

@@ -10,7 +10,12 @@
 //    executioncontext.c:185-201): the all-reduces issued between
 //    ncclGroupStart and ncclGroupEnd are matched by their order on each
 //    communicator, as in NCCL, and run at ncclGroupEnd.  An ungrouped call on
-//    such a communicator is an error (real NCCL would deadlock on it).
+//    such a communicator is an error (real NCCL would deadlock on it).  A
+//    group that holds only some ranks' calls (one thread per device, each
+//    issuing its own communicator's collectives: cbx_set_enqueue_threads)
+//    meets the other ranks' k-th calls at a rendezvous; the last to arrive
+//    runs the collective for all, the others wait for it (60 s, then
+//    ncclSystemError).
 //
 // Calls: ncclAllReduce, ncclReduceScatter and ncclAllGather (fp32; sum).
 // Each collective synchronises the stream it was given (so every kernel the
@@ -47,8 +52,12 @@
 #include <sys/stat.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <chrono>
+#include <condition_variable>
 #include <cstdio>
+#include <map>
+#include <mutex>
 #include <cstdlib>
 #include <cstring>
 #include <random>
@@ -66,12 +75,23 @@ struct ncclComm {
   bool noop = false;  // $FAKE_RCCL_NOOP: collectives move nothing (host-side timing only)
   std::string tag;  // hex of the unique id
   unsigned long long seq = 0;
+  unsigned long long rv_seq = 0;  // rendezvous calls on this communicator
   Clique *clique = nullptr;  // single-process communicators (ncclCommInitAll, ndev > 1)
 };
 
 struct Clique {
   std::vector<ncclComm *> comms;
   int live = 0;
+  // Rendezvous of per-thread groups: the k-th call of every rank.
+  struct Slot {
+    std::vector<const void *> ops;  // PendingOp of each rank
+    int have = 0, left = 0;
+    bool done = false;
+    int rc = 0;
+  };
+  std::mutex m;
+  std::condition_variable cv;
+  std::map<unsigned long long, Slot> rv;
 };
 
 namespace {
@@ -212,6 +232,33 @@ ncclResult_t run_clique(const std::vector<PendingOp *> &ops) {
   return ncclSuccess;
 }
 
+// One rank's call of a clique collective whose other ranks' calls come from
+// other threads: wait for all of them, the last one runs it.
+ncclResult_t rendezvous(const PendingOp &op) {
+  Clique *q = op.comm->clique;
+  const int G = (int)q->comms.size();
+  std::unique_lock<std::mutex> l(q->m);
+  const unsigned long long key = op.comm->rv_seq++;
+  Clique::Slot &s = q->rv[key];
+  if (s.ops.empty()) s.ops.assign(G, nullptr);
+  s.ops[op.comm->rank] = &op;
+  if (++s.have == G) {
+    std::vector<PendingOp *> coll(G);
+    for (int r = 0; r < G; ++r) coll[r] = const_cast<PendingOp *>(static_cast<const PendingOp *>(s.ops[r]));
+    l.unlock();
+    const ncclResult_t rc = run_clique(coll);
+    l.lock();
+    s.rc = (int)rc;
+    s.done = true;
+    q->cv.notify_all();
+  } else if (!q->cv.wait_for(l, std::chrono::seconds(60), [&] { return s.done; })) {
+    return ncclSystemError;  // a rank never arrived
+  }
+  const ncclResult_t rc = (ncclResult_t)s.rc;
+  if (++s.left == G) q->rv.erase(key);
+  return rc;
+}
+
 // The per-rank (multi-process) collective through files.
 ncclResult_t run_ranked(int kind, const void *send, void *recv, size_t count, ncclComm *c, hipStream_t stream) {
   if (hipStreamSynchronize(stream) != hipSuccess) return ncclSystemError;
@@ -340,6 +387,21 @@ ncclResult_t ncclGroupEnd() {
   // NCCL matches the grouped calls of a clique by their order on each
   // communicator: the k-th call on every rank forms the k-th collective.
   std::vector<bool> done(ops.size(), false);
+  // A clique only some of whose ranks are in this group: per-thread groups,
+  // every call goes to the rendezvous in order.
+  std::map<Clique *, std::vector<bool>> ranks;
+  for (const PendingOp &op : ops) {
+    auto &v = ranks[op.comm->clique];
+    v.resize(op.comm->clique->comms.size(), false);
+    v[op.comm->rank] = true;
+  }
+  for (size_t a = 0; a < ops.size(); ++a) {
+    const auto &v = ranks[ops[a].comm->clique];
+    if (std::find(v.begin(), v.end(), false) == v.end()) continue;
+    const ncclResult_t r = rendezvous(ops[a]);
+    if (r != ncclSuccess) return r;
+    done[a] = true;
+  }
   for (size_t a = 0; a < ops.size(); ++a) {
     if (done[a]) continue;
     Clique *q = ops[a].comm->clique;

@@ -91,7 +91,7 @@ def _jobs(G):
     return jobs + [("bn", "bn"), ("autotune", "autotune")]
 
 
-def _worker(G, jobs, ckdir, q):
+def _worker(G, jobs, ckdir, q, threads=-1):
     try:
         L, A = C.load_variant()
         cases = {c.name: c for c in CASES}
@@ -102,6 +102,7 @@ def _worker(G, jobs, ckdir, q):
             os.environ["FAKE_RCCL_ORDER"] = cases[name].order if kind == "case" else "rank"
             g = C.init_local(L, A, G)
             try:
+                assert L.cbx_set_enqueue_threads(g.c, threads) == 0
                 if G == 3:  # the reduce-scatter form needs G dividing the bucket padding
                     assert L.cbx_set_allreduce_algorithm(g.c, A.ALLREDUCE_RSAG) == A.CBX_ERR_UNSUPPORTED
                 if kind == "case":
@@ -123,14 +124,18 @@ def _worker(G, jobs, ckdir, q):
 
 
 @pytest.mark.skipif(not os.path.exists(C.VARIANT), reason="run scripts/build_fake_rccl.sh first")
-@pytest.mark.parametrize("G", [2, 3, 4, 8, 16])
-def test_one_process_many_devices_vs_oracle(G):
+@pytest.mark.parametrize("G,threads", [(2, -1), (3, -1), (4, -1), (8, -1), (16, -1), (2, 0), (8, 0)])
+def test_one_process_many_devices_vs_oracle(G, threads):
+    """threads -1 (the default): one enqueue thread per device, each issuing
+    its own communicator's collectives (the loopback meets them at a
+    rendezvous); 0: the reference's single thread, collectives grouped
+    across the devices."""
     import multiprocessing as mp
     jobs = _jobs(G)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     with tempfile.TemporaryDirectory() as ckdir:
-        p = ctx.Process(target=_worker, args=(G, jobs, os.path.join(ckdir, "ckpt"), q))
+        p = ctx.Process(target=_worker, args=(G, jobs, os.path.join(ckdir, "ckpt"), q, threads))
         p.start()
         try:
             res, err = q.get(timeout=110)
