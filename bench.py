@@ -339,12 +339,17 @@ def main():
                              "(one process per GPU) or without it (one process over N GPUs)")
     nlocal = G if single else 1
     peer_only = single and args.rehearse_one_gpu  # RCCL refuses a repeated device: the peer-read form only
-    rccl_log = None
-    if G > 1 and not peer_only and not args.no_rccl_tuning_log and "NCCL_DEBUG" not in os.environ:
-        # RCCL reads these once, at its first call: every collective then logs
-        # its algorithm / protocol / channels (one line each) to the file.
-        rccl_log = os.path.join(tempfile.gettempdir(), f"cbx_rccl_tuning.r{rank}.{os.getpid()}.log")
-        os.environ.update(NCCL_DEBUG="INFO", NCCL_DEBUG_SUBSYS="TUNING", NCCL_DEBUG_FILE=rccl_log)
+    rccl_log, rccl_why = None, None
+    if G > 1 and not peer_only:
+        if args.no_rccl_tuning_log:
+            rccl_why = "--no-rccl-tuning-log"
+        elif os.environ.get("NCCL_DEBUG_FILE"):
+            rccl_why = f"NCCL_DEBUG_FILE={os.environ['NCCL_DEBUG_FILE']} set by the caller"
+        else:
+            # RCCL reads these once, at its first call: every collective then
+            # logs its algorithm / protocol / channels (one line each) to the file.
+            rccl_log = os.path.join(tempfile.gettempdir(), f"cbx_rccl_tuning.r{rank}.{os.getpid()}.log")
+            os.environ.update(NCCL_DEBUG="INFO", NCCL_DEBUG_SUBSYS="TUNING", NCCL_DEBUG_FILE=rccl_log)
 
     import torch
 
@@ -585,6 +590,9 @@ def main():
             result["allreduce"]["rccl_tuning_source"] = (
                 "RCCL's own log (NCCL_DEBUG=INFO, NCCL_DEBUG_SUBSYS=TUNING), this process, every collective of the "
                 "run (calibration, tuning, timed)")
+        elif G > 1:
+            result["allreduce"]["rccl_tuning"] = None
+            result["allreduce"]["rccl_tuning_source"] = rccl_why or "no RCCL collective in this form"
 
     if G > 1 and not args.no_staged and peer_only:
         result["host_staged"] = {"skipped": "the host-staged step's collective is RCCL's, which refuses a repeated device"}

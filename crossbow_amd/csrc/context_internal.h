@@ -321,6 +321,7 @@ struct Device {
   // kernels B stay on `stream`; bucket_b[k] marks B(k) done, which A(k) of
   // the next step waits for instead of the whole previous step.
   hipStream_t a_stream = nullptr;
+  hipStream_t a_stream2 = nullptr;  // experiment: odd buckets' kernels A ($CBX_EXP_TWO_A)
   std::vector<hipEvent_t> bucket_b;
   hipEvent_t cross_entry = nullptr;
   float *decision = nullptr;           // 2 floats: the Phase-D decision, by step parity
@@ -484,6 +485,7 @@ struct cbx_context {
   // at context creation drops the comm stream's wait on kernel A, so the
   // collective races its input (results are then wrong; tests only).
   bool fault_skip_comm_wait = std::getenv("CBX_FAULT_SKIP_COMM_WAIT") != nullptr;
+  bool exp_two_a = std::getenv("CBX_EXP_TWO_A") != nullptr;
   // Bumped by every C-ABI call that may enqueue work on a sync stream other
   // than the barrier path itself: a cross-step pipelined step then joins the
   // whole sync stream instead of waiting bucket by bucket.
@@ -706,6 +708,7 @@ inline void close_device(Device &d) {
   for (hipEvent_t e : d.bucket_acc) (void)hipEventDestroy(e);
   for (hipEvent_t e : d.bucket_red) (void)hipEventDestroy(e);
   if (d.a_stream) (void)hipStreamSynchronize(d.a_stream);
+  if (d.a_stream2) (void)hipStreamSynchronize(d.a_stream2);
   for (hipEvent_t e : d.bucket_b) (void)hipEventDestroy(e);
   if (d.cross_entry) (void)hipEventDestroy(d.cross_entry);
   for (auto &pool : d.ord_pool)
@@ -714,6 +717,7 @@ inline void close_device(Device &d) {
   if (d.peer_r) (void)hipEventDestroy(d.peer_r);
   if (d.decision) (void)hipFree(d.decision);
   if (d.a_stream) (void)hipStreamDestroy(d.a_stream);
+  if (d.a_stream2) (void)hipStreamDestroy(d.a_stream2);
   for (hipStream_t st : {d.h2d_stream, d.d2h_stream})
     if (st) (void)hipStreamSynchronize(st);
   for (hipEvent_t e : d.stage_h2d) (void)hipEventDestroy(e);

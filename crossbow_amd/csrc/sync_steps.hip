@@ -227,7 +227,7 @@ struct SplitStep {
   std::vector<cbx::SmaArgs> &args;
   bool mom;
   int64_t b4 = 0, nb = 0, wait_stride = 1;
-  bool pipelined = false, cross = false, rsag = false, ocheck = false, spans = false;
+  bool pipelined = false, cross = false, rsag = false, ocheck = false, spans = false, two_a = false;
   unsigned long long foreign = 0;
   std::vector<char> join;
   // Kernel spans (Device::SpanSlot), per device: the step's slot, the
@@ -334,7 +334,8 @@ struct SplitStep {
     cross = pipelined && c->pipeline_mode == 1;
     rsag = c->allreduce_algo == CBX_ALLREDUCE_RSAG;
     ocheck = c->order_check && c->timing;
-    spans = c->timing && !ocheck && pipelined && nb <= Device::kSpanMaxBuckets;
+    two_a = cross && c->exp_two_a;
+    spans = c->timing && !ocheck && pipelined && nb <= Device::kSpanMaxBuckets && !two_a;
     for (Device &d : c->devs) spans = spans && !d.spans.empty();
     wait_stride = std::max(1, c->cross_wait_stride);
     foreign = c->foreign_ops.load(std::memory_order_acquire);
@@ -362,6 +363,7 @@ struct SplitStep {
         }
       }
       if (cross) {
+        if (two_a && !d.a_stream2) HIP_TRY(hipStreamCreateWithFlags(&d.a_stream2, hipStreamNonBlocking));
         if (!d.a_stream) {
           HIP_TRY(hipStreamCreateWithFlags(&d.a_stream, hipStreamNonBlocking));
           HIP_TRY(hipEventCreateWithFlags(&d.cross_entry, hipEventDisableTiming));
@@ -376,6 +378,7 @@ struct SplitStep {
         hipEvent_t e = spans ? tr[k].slot->entry : d.cross_entry;
         HIP_TRY(hipEventRecord(e, d.stream));
         HIP_TRY(hipStreamWaitEvent(d.a_stream, e, 0));
+        if (two_a) HIP_TRY(hipStreamWaitEvent(d.a_stream2, e, 0));
         note_wait(k, 1, e);
         if (spans) tr[k].last[0] = e;  // everything before it on the sync stream
       }
@@ -412,10 +415,13 @@ struct SplitStep {
       cbx::Timing t;
       if (b == 0) t.start = pipelined ? step_start_event(c, d, 2) : ring_event(c, d, EV_START);
       if (!pipelined) t.stop = ring_event(c, d, EV_A);
-      hipStream_t st = cross ? d.a_stream : d.stream;
+      hipStream_t st = cross ? (two_a && (b & 1) ? d.a_stream2 : d.a_stream) : d.stream;
       const int si = cross ? 1 : 0;
-      if (cross && !join[k] && b % wait_stride == 0) {  // B(b .. b+stride-1) of the last step
-        const int64_t w = std::min<int64_t>(b + wait_stride - 1, nb - 1);
+      // Two A streams: the per-stream position decides the wait; waiting on
+      // a later B implies every earlier one (the B's run in order).
+      const int64_t pos = two_a ? b / 2 : b;
+      if (cross && !join[k] && pos % wait_stride == 0) {  // B(b .. b+stride-1) of the last step
+        const int64_t w = std::min<int64_t>(two_a ? b + 2 * (wait_stride - 1) : b + wait_stride - 1, nb - 1);
         hipEvent_t e = ocheck ? d.ord[d.ord_cur ^ 1u].b1[w] : spans ? tr[k].prev->b_used[w] : d.bucket_b[w];
         HIP_TRY(hipStreamWaitEvent(st, e, 0));
         note_wait(k, si, e);

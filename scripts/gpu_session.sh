@@ -7,6 +7,7 @@
 #   enqueue    scripts/host_enqueue_multidev.py (single-process host cost)
 #   rocprof    rocprofv3 --kernel-trace --stats of bench.py $BENCH_ARGS
 #   markers    rocprofv3 --marker-trace --kernel-trace of the single-process rehearsal
+#   script:P   python P (a measurement script under scripts/)
 # Every GPU step has its own time limit; a fault / abort / timeout ends the
 # script (no later GPU step runs); a plain test failure does not.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
@@ -42,6 +43,7 @@ for s in "${STEPS[@]}"; do
     enqueue)
       run enqueue_peer 400 python scripts/host_enqueue_multidev.py --variant peer
       run enqueue_noop 600 python scripts/host_enqueue_multidev.py --variant fake-noop ;;
+    script:*) run "$(basename "${s#script:}" .py)" 600 python "${s#script:}" ;;
     rocprof) run rocprof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/rocprof -o run --output-format csv -- \
       python3 bench.py --no-cpu-baseline --no-staged --no-copy-ceiling --no-seam ${BENCH_ARGS:-} ;;
     markers) run markers 600 rocprofv3 --marker-trace --kernel-trace --stats -d gpurun_out/markers -o run \

@@ -1,0 +1,79 @@
+#!/usr/bin/env python3
+"""A/B on one MI355X: the G > 1 bucket pipeline (forced at G = 1, one-rank
+RCCL) in cross-step mode with kernels A on one stream vs alternating over two
+($CBX_EXP_TWO_A, read at context creation), so bucket k+1's waves can fill
+the CUs while bucket k's drain.  ResNet-50, R = 8, momentum 0.9; ms per step
+(wall clock over back-to-back steps), interleaved passes, best pass kept.
+JSON lines on stdout."""
+from __future__ import annotations
+
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def make(two):
+    from crossbow_amd import SYNC_BSP, UPDATE_SMA, TheGPU
+    from crossbow_amd.variables import MODELS, register
+    if two:
+        os.environ["CBX_EXP_TWO_A"] = "1"
+    else:
+        os.environ.pop("CBX_EXP_TWO_A", None)
+    g = TheGPU()
+    g.init([0])
+    n = register(g, MODELS["resnet50"]())
+    g.setUpdateModelType(UPDATE_SMA)
+    g.setEamsgdAlpha(0.1)
+    g.setMomentum(0.9, 0)
+    g.setModelManager(8, SYNC_BSP)
+    g.set_force_split(True)
+    g.fill_synthetic(1)
+    g.set_timing(True)
+    return g, n
+
+
+def timed(g, steps=30, warmup=5):
+    clock = [0]
+
+    def step():
+        clock[0] += 1
+        g.lockAny()
+        g.synchronise(0, clock[0], 0, False)
+        g.unlockAny()
+    for _ in range(warmup):
+        step()
+    g.wait()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    g.wait()
+    return (time.perf_counter() - t0) * 1e3 / steps
+
+
+def main():
+    ctx = {False: make(False), True: make(True)}
+    configs = [(1, 0, 1), (4, 1, 1), (8, 1, 1), (8, 1, 2), (8, 1, 4), (8, 0, 1)]
+    best = {}
+    for _ in range(3):
+        for nb, mode, stride in configs:
+            for two in (False, True):
+                g, n = ctx[two]
+                g.set_bucket_elements((1 << 62) if nb == 1 else -(-n // nb))
+                g.set_pipeline_mode(mode)
+                g.set_cross_wait_stride(stride)
+                ms = timed(g)
+                key = (nb, mode, stride, two)
+                best[key] = min(ms, best.get(key, ms))
+    for (nb, mode, stride, two), ms in sorted(best.items()):
+        print(json.dumps({"buckets": nb, "mode": mode, "stride": stride, "two_a_streams": two,
+                          "ms_per_step": round(ms, 4)}), flush=True)
+    for g, _ in ctx.values():
+        g.free()
+
+
+if __name__ == "__main__":
+    main()
