@@ -486,6 +486,7 @@ struct cbx_context {
   // collective races its input (results are then wrong; tests only).
   bool fault_skip_comm_wait = std::getenv("CBX_FAULT_SKIP_COMM_WAIT") != nullptr;
   bool exp_two_a = std::getenv("CBX_EXP_TWO_A") != nullptr;
+  bool exp_no_spans = std::getenv("CBX_EXP_NO_SPANS") != nullptr;
   // Bumped by every C-ABI call that may enqueue work on a sync stream other
   // than the barrier path itself: a cross-step pipelined step then joins the
   // whole sync stream instead of waiting bucket by bucket.

@@ -335,7 +335,7 @@ struct SplitStep {
     rsag = c->allreduce_algo == CBX_ALLREDUCE_RSAG;
     ocheck = c->order_check && c->timing;
     two_a = cross && c->exp_two_a;
-    spans = c->timing && !ocheck && pipelined && nb <= Device::kSpanMaxBuckets && !two_a;
+    spans = c->timing && !ocheck && pipelined && nb <= Device::kSpanMaxBuckets && !two_a && !c->exp_no_spans;
     for (Device &d : c->devs) spans = spans && !d.spans.empty();
     wait_stride = std::max(1, c->cross_wait_stride);
     foreign = c->foreign_ops.load(std::memory_order_acquire);

@@ -4,6 +4,8 @@ RCCL) in cross-step mode with kernels A on one stream vs alternating over two
 ($CBX_EXP_TWO_A, read at context creation), so bucket k+1's waves can fill
 the CUs while bucket k's drain.  ResNet-50, R = 8, momentum 0.9; ms per step
 (wall clock over back-to-back steps), interleaved passes, best pass kept.
+Variants: one / two A streams, with or without the per-dispatch span events
+($CBX_EXP_NO_SPANS), and one stream with timing off altogether.
 JSON lines on stdout."""
 from __future__ import annotations
 
@@ -16,13 +18,15 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
-def make(two):
+def make(variant):
     from crossbow_amd import SYNC_BSP, UPDATE_SMA, TheGPU
     from crossbow_amd.variables import MODELS, register
-    if two:
+    for k in ("CBX_EXP_TWO_A", "CBX_EXP_NO_SPANS"):
+        os.environ.pop(k, None)
+    if "two" in variant:
         os.environ["CBX_EXP_TWO_A"] = "1"
-    else:
-        os.environ.pop("CBX_EXP_TWO_A", None)
+    if "nospans" in variant:
+        os.environ["CBX_EXP_NO_SPANS"] = "1"
     g = TheGPU()
     g.init([0])
     n = register(g, MODELS["resnet50"]())
@@ -55,12 +59,14 @@ def timed(g, steps=30, warmup=5):
 
 
 def main():
-    ctx = {False: make(False), True: make(True)}
+    variants = ("one-spans", "one-nospans", "two-nospans", "one-notiming")
+    ctx = {v: make(v) for v in variants}
+    ctx["one-notiming"][0].set_timing(False)
     configs = [(1, 0, 1), (4, 1, 1), (8, 1, 1), (8, 1, 2), (8, 1, 4), (8, 0, 1)]
     best = {}
     for _ in range(3):
         for nb, mode, stride in configs:
-            for two in (False, True):
+            for two in variants:
                 g, n = ctx[two]
                 g.set_bucket_elements((1 << 62) if nb == 1 else -(-n // nb))
                 g.set_pipeline_mode(mode)
@@ -69,7 +75,7 @@ def main():
                 key = (nb, mode, stride, two)
                 best[key] = min(ms, best.get(key, ms))
     for (nb, mode, stride, two), ms in sorted(best.items()):
-        print(json.dumps({"buckets": nb, "mode": mode, "stride": stride, "two_a_streams": two,
+        print(json.dumps({"buckets": nb, "mode": mode, "stride": stride, "variant": two,
                           "ms_per_step": round(ms, 4)}), flush=True)
     for g, _ in ctx.values():
         g.free()
