@@ -43,7 +43,7 @@ for s in "${STEPS[@]}"; do
     enqueue)
       run enqueue_peer 400 python scripts/host_enqueue_multidev.py --variant peer
       run enqueue_noop 600 python scripts/host_enqueue_multidev.py --variant fake-noop ;;
-    script:*) run "$(basename "${s#script:}" .py)" 600 python "${s#script:}" ;;
+    script:*) run "$(basename "${s#script:}" .py)" 600 python ${s#script:} ${SCRIPT_ARGS:-} ;;
     rocprof) run rocprof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/rocprof -o run --output-format csv -- \
       python3 bench.py --no-cpu-baseline --no-staged --no-copy-ceiling --no-seam ${BENCH_ARGS:-} ;;
     markers) run markers 600 rocprofv3 --marker-trace --kernel-trace --stats -d gpurun_out/markers -o run \

@@ -59,12 +59,23 @@ def timed(g, steps=30, warmup=5):
 
 
 def main():
-    variants = ("one-spans", "one-nospans", "two-nospans", "one-notiming")
-    ctx = {v: make(v) for v in variants}
-    ctx["one-notiming"][0].set_timing(False)
-    configs = [(1, 0, 1), (4, 1, 1), (8, 1, 1), (8, 1, 2), (8, 1, 4), (8, 0, 1)]
+    import argparse
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--variants", default="one-spans,one-nospans,two-nospans,one-notiming")
+    ap.add_argument("--configs", default="1/0/1,4/1/1,8/1/1,8/1/2,8/1/4,8/0/1")
+    ap.add_argument("--passes", type=int, default=3)
+    a = ap.parse_args()
+    variants = a.variants.split(",")  # a repeated variant gets a context of its own (placement check)
+    ctx = {}
+    for i, v in enumerate(variants):
+        name = v if v not in ctx else f"{v}#{i}"
+        variants[i] = name
+        ctx[name] = make(v)
+        if "notiming" in v:
+            ctx[name][0].set_timing(False)
+    configs = [tuple(int(x) for x in c.split("/")) for c in a.configs.split(",")]
     best = {}
-    for _ in range(3):
+    for _ in range(a.passes):
         for nb, mode, stride in configs:
             for two in variants:
                 g, n = ctx[two]
