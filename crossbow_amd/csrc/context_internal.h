@@ -670,14 +670,37 @@ inline int probe_device(int hip_id, int *num_cus) {
   return CBX_OK;
 }
 
+// A non-blocking stream for the library's own work.  Experiment
+// ($CBX_EXP_QUEUES): "cumask" = a stream over every CU through
+// hipExtStreamCreateWithCUMask (a hardware queue of its own), "prio" = high
+// priority for even calls (hipStreamCreateWithPriority).
+inline int create_stream(hipStream_t *s, int num_cus, bool high = false) {
+  const char *q = std::getenv("CBX_EXP_QUEUES");
+  if (q && std::strcmp(q, "cumask") == 0) {
+    uint32_t mask[16];
+    for (int i = 0; i < 16; ++i) mask[i] = 0;
+    for (int i = 0; i < num_cus && i < 512; ++i) mask[i / 32] |= 1u << (i % 32);
+    HIP_TRY(hipExtStreamCreateWithCUMask(s, (uint32_t)((num_cus + 31) / 32), mask));
+    return CBX_OK;
+  }
+  if (q && std::strcmp(q, "prio") == 0 && high) {
+    int lo = 0, hi = 0;
+    HIP_TRY(hipDeviceGetStreamPriorityRange(&lo, &hi));
+    HIP_TRY(hipStreamCreateWithPriority(s, hipStreamNonBlocking, hi));
+    return CBX_OK;
+  }
+  HIP_TRY(hipStreamCreateWithFlags(s, hipStreamNonBlocking));
+  return CBX_OK;
+}
+
 inline int open_device(Device &d, int hip_id, int g) {
   TRY(probe_device(hip_id, &d.num_cus));
   d.hip_id = hip_id;
   d.g = g;
   d.file_id = g;
   // executioncontext.c:324: one non-blocking model-synchronisation stream.
-  HIP_TRY(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
-  HIP_TRY(hipStreamCreateWithFlags(&d.comm_stream, hipStreamNonBlocking));
+  TRY(create_stream(&d.stream, d.num_cus));
+  TRY(create_stream(&d.comm_stream, d.num_cus, true));
   HIP_TRY(hipEventCreateWithFlags(&d.synched, hipEventDisableTiming));
   for (int k = 0; k < EV_COUNT; ++k) HIP_TRY(hipEventCreate(&d.ev[k]));
   return CBX_OK;

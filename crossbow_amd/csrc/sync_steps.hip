@@ -363,9 +363,9 @@ struct SplitStep {
         }
       }
       if (cross) {
-        if (two_a && !d.a_stream2) HIP_TRY(hipStreamCreateWithFlags(&d.a_stream2, hipStreamNonBlocking));
+        if (two_a && !d.a_stream2) TRY(create_stream(&d.a_stream2, d.num_cus));
         if (!d.a_stream) {
-          HIP_TRY(hipStreamCreateWithFlags(&d.a_stream, hipStreamNonBlocking));
+          TRY(create_stream(&d.a_stream, d.num_cus, true));
           HIP_TRY(hipEventCreateWithFlags(&d.cross_entry, hipEventDisableTiming));
           HIP_TRY(hipMalloc(reinterpret_cast<void **>(&d.decision), 256));
           HIP_TRY(hipMemsetAsync(d.decision, 0, 256, d.stream));

@@ -21,8 +21,12 @@ sys.path.insert(0, ROOT)
 def make(variant):
     from crossbow_amd import SYNC_BSP, UPDATE_SMA, TheGPU
     from crossbow_amd.variables import MODELS, register
-    for k in ("CBX_EXP_TWO_A", "CBX_EXP_NO_SPANS"):
+    for k in ("CBX_EXP_TWO_A", "CBX_EXP_NO_SPANS", "CBX_EXP_QUEUES"):
         os.environ.pop(k, None)
+    if "cumask" in variant:
+        os.environ["CBX_EXP_QUEUES"] = "cumask"
+    if "prio" in variant:
+        os.environ["CBX_EXP_QUEUES"] = "prio"
     if "two" in variant:
         os.environ["CBX_EXP_TWO_A"] = "1"
     if "nospans" in variant:
