@@ -320,8 +320,12 @@ struct Device {
   // Cross-step pipeline (cbx_set_pipeline_mode 1): kernels A run on a_stream,
   // kernels B stay on `stream`; bucket_b[k] marks B(k) done, which A(k) of
   // the next step waits for instead of the whole previous step.
+  // Kernels A alternate over two streams, so the waves of bucket k+1 fill
+  // the CUs while bucket k's drain instead of after (8 buckets: 0.548 ms per
+  // step against 0.586-0.623 on one stream and 0.551 with one bucket,
+  // profiles/r03/pipeline_streams_ab.json).
   hipStream_t a_stream = nullptr;
-  hipStream_t a_stream2 = nullptr;  // experiment: odd buckets' kernels A ($CBX_EXP_TWO_A)
+  hipStream_t a_stream2 = nullptr;
   std::vector<hipEvent_t> bucket_b;
   hipEvent_t cross_entry = nullptr;
   float *decision = nullptr;           // 2 floats: the Phase-D decision, by step parity
@@ -485,8 +489,6 @@ struct cbx_context {
   // at context creation drops the comm stream's wait on kernel A, so the
   // collective races its input (results are then wrong; tests only).
   bool fault_skip_comm_wait = std::getenv("CBX_FAULT_SKIP_COMM_WAIT") != nullptr;
-  bool exp_two_a = std::getenv("CBX_EXP_TWO_A") != nullptr;
-  bool exp_no_spans = std::getenv("CBX_EXP_NO_SPANS") != nullptr;
   // Bumped by every C-ABI call that may enqueue work on a sync stream other
   // than the barrier path itself: a cross-step pipelined step then joins the
   // whole sync stream instead of waiting bucket by bucket.
@@ -670,26 +672,23 @@ inline int probe_device(int hip_id, int *num_cus) {
   return CBX_OK;
 }
 
-// A non-blocking stream for the library's own work.  Experiment
-// ($CBX_EXP_QUEUES): "cumask" = a stream over every CU through
-// hipExtStreamCreateWithCUMask (a hardware queue of its own), "prio" = high
-// priority for even calls (hipStreamCreateWithPriority).
-inline int create_stream(hipStream_t *s, int num_cus, bool high = false) {
-  const char *q = std::getenv("CBX_EXP_QUEUES");
-  if (q && std::strcmp(q, "cumask") == 0) {
-    uint32_t mask[16];
-    for (int i = 0; i < 16; ++i) mask[i] = 0;
-    for (int i = 0; i < num_cus && i < 512; ++i) mask[i / 32] |= 1u << (i % 32);
-    HIP_TRY(hipExtStreamCreateWithCUMask(s, (uint32_t)((num_cus + 31) / 32), mask));
-    return CBX_OK;
-  }
-  if (q && std::strcmp(q, "prio") == 0 && high) {
-    int lo = 0, hi = 0;
-    HIP_TRY(hipDeviceGetStreamPriorityRange(&lo, &hi));
-    HIP_TRY(hipStreamCreateWithPriority(s, hipStreamNonBlocking, hi));
-    return CBX_OK;
-  }
-  HIP_TRY(hipStreamCreateWithFlags(s, hipStreamNonBlocking));
+// A stream for the library's own work, on a hardware queue of its own.
+// ROCclr maps ordinary streams onto a pool of GPU_MAX_HW_QUEUES (4) queues
+// per device, shared by every stream of the process (torch's, RCCL's, ours);
+// two streams on one queue serialise at every stream wait, so the bucket
+// pipeline's waits on one stream stall the kernels of another.  Which
+// streams collide depends on creation order: 8-bucket cross-step steps
+// measured 0.59-0.62 ms on some contexts and 0.72-1.1 ms on others
+// (profiles/r03/pipeline_streams_ab.json).  A stream with a CU mask gets a
+// queue of its own (the mask is a queue property); the mask here is every
+// CU.  Such a stream synchronises with the null stream, as a default-flag
+// stream does (the reference's is non-blocking, executioncontext.c:324): the
+// only effect is extra ordering against null-stream work.
+inline int create_stream(hipStream_t *s, int num_cus) {
+  uint32_t mask[16] = {};
+  const int cus = std::min(num_cus, 512);
+  for (int i = 0; i < cus; ++i) mask[i / 32] |= 1u << (i % 32);
+  HIP_TRY(hipExtStreamCreateWithCUMask(s, (uint32_t)((cus + 31) / 32), mask));
   return CBX_OK;
 }
 
@@ -700,7 +699,7 @@ inline int open_device(Device &d, int hip_id, int g) {
   d.file_id = g;
   // executioncontext.c:324: one non-blocking model-synchronisation stream.
   TRY(create_stream(&d.stream, d.num_cus));
-  TRY(create_stream(&d.comm_stream, d.num_cus, true));
+  TRY(create_stream(&d.comm_stream, d.num_cus));
   HIP_TRY(hipEventCreateWithFlags(&d.synched, hipEventDisableTiming));
   for (int k = 0; k < EV_COUNT; ++k) HIP_TRY(hipEventCreate(&d.ev[k]));
   return CBX_OK;
@@ -852,32 +851,48 @@ inline int ring_span(Device &d, int slot, int a, int b, float *out) {
   return CBX_OK;
 }
 
-// Summed busy ms of the `kind` dispatches (Device::SpanKind) of the pipelined
-// step in ring slot `slot`: for each, stop - the latest event that bounded
-// its start, i.e. the minimum over those events of elapsed(event, stop).
+// Busy ms of the `kind` dispatches (Device::SpanKind) of the pipelined step
+// in ring slot `slot`: the length of the union of their intervals, each from
+// the latest event that bounded its start to its stop (kernels A on two
+// streams overlap; a plain sum would count the overlap twice).  Times are
+// taken relative to the first such dispatch's stop, so events before it read
+// negative (hipEventElapsedTime is signed; tests/test_gpu_parity.py pins it).
 // -1 when the step kept no span records (another form, or overwritten).
 inline int span_sum(Device &d, int slot, int kind, float *out) {
   *out = -1.0f;
   if (d.ring_span.empty() || d.ring_span[slot] < 0) return CBX_OK;
   Device::SpanSlot &sp = d.spans[d.ring_span[slot]];
   if (sp.ring_slot != slot || !sp.preds_valid) return CBX_OK;
-  float sum = 0.0f;
-  int n = 0;
+  hipEvent_t ref = nullptr;
+  std::vector<std::pair<float, float>> iv;
   for (const Device::SpanRec &r : sp.recs) {
     if (r.kind != kind) continue;
     if (r.npred <= 0) return CBX_OK;
     HIP_TRY(hipEventSynchronize(r.stop));
-    float best = 1e30f;
+    if (!ref) ref = r.stop;
+    float t1 = 0.0f, t0 = -1e30f;
+    HIP_TRY(hipEventElapsedTime(&t1, ref, r.stop));
     for (int i = 0; i < r.npred; ++i) {
-      float ms = 0.0f;
-      HIP_TRY(hipEventElapsedTime(&ms, r.pred[i], r.stop));
-      best = std::min(best, ms);
+      float tp = 0.0f;
+      HIP_TRY(hipEventElapsedTime(&tp, ref, r.pred[i]));
+      t0 = std::max(t0, tp);
     }
-    if (best < 0.0f) return CBX_OK;
-    sum += best;
-    ++n;
+    if (t1 < t0) return CBX_OK;
+    iv.emplace_back(t0, t1);
   }
-  if (n > 0) *out = sum;
+  if (iv.empty()) return CBX_OK;
+  std::sort(iv.begin(), iv.end());
+  float sum = 0.0f, lo = iv[0].first, hi = iv[0].second;
+  for (size_t i = 1; i < iv.size(); ++i) {
+    if (iv[i].first > hi) {
+      sum += hi - lo;
+      lo = iv[i].first;
+      hi = iv[i].second;
+    } else {
+      hi = std::max(hi, iv[i].second);
+    }
+  }
+  *out = sum + (hi - lo);
   return CBX_OK;
 }
 

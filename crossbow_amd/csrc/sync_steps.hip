@@ -227,17 +227,17 @@ struct SplitStep {
   std::vector<cbx::SmaArgs> &args;
   bool mom;
   int64_t b4 = 0, nb = 0, wait_stride = 1;
-  bool pipelined = false, cross = false, rsag = false, ocheck = false, spans = false, two_a = false;
+  bool pipelined = false, cross = false, rsag = false, ocheck = false, spans = false;
   unsigned long long foreign = 0;
   std::vector<char> join;
   // Kernel spans (Device::SpanSlot), per device: the step's slot, the
   // previous pipelined step's, the last stop event on each stream the step
-  // uses (0 sync stream, 1 a_stream, 2 comm_stream) and the events each of
-  // those streams waited on since.
+  // uses (0 sync stream, 1 a_stream, 2 comm_stream, 3 a_stream2) and the
+  // events each of those streams waited on since.
   struct Track {
     Device::SpanSlot *slot = nullptr, *prev = nullptr;
-    hipEvent_t last[3] = {};
-    std::vector<hipEvent_t> pending[3];
+    hipEvent_t last[4] = {};
+    std::vector<hipEvent_t> pending[4];
   };
   std::vector<Track> tr;
 
@@ -313,7 +313,9 @@ struct SplitStep {
       if (d.ring_count > 0) t.last[0] = ring_stop(d, prev_ring);
     } else if (!join[k]) {  // continues the previous cross step bucket by bucket (same nb, spans on)
       if (!t.prev) return fail(CBX_ERR_STATE, "span records of the previous step are missing");
-      t.last[1] = t.prev->a_used[nb - 1];
+      const int64_t last_odd = (nb - 1) & 1 ? nb - 1 : nb - 2, last_even = (nb - 1) & 1 ? nb - 2 : nb - 1;
+      t.last[1] = t.prev->a_used[last_even];
+      t.last[3] = t.prev->a_used[last_odd];
       t.last[0] = t.prev->b_used[nb - 1];
     }
     return CBX_OK;
@@ -334,8 +336,7 @@ struct SplitStep {
     cross = pipelined && c->pipeline_mode == 1;
     rsag = c->allreduce_algo == CBX_ALLREDUCE_RSAG;
     ocheck = c->order_check && c->timing;
-    two_a = cross && c->exp_two_a;
-    spans = c->timing && !ocheck && pipelined && nb <= Device::kSpanMaxBuckets && !two_a && !c->exp_no_spans;
+    spans = c->timing && !ocheck && pipelined && nb <= Device::kSpanMaxBuckets;
     for (Device &d : c->devs) spans = spans && !d.spans.empty();
     wait_stride = std::max(1, c->cross_wait_stride);
     foreign = c->foreign_ops.load(std::memory_order_acquire);
@@ -363,9 +364,9 @@ struct SplitStep {
         }
       }
       if (cross) {
-        if (two_a && !d.a_stream2) TRY(create_stream(&d.a_stream2, d.num_cus));
         if (!d.a_stream) {
-          TRY(create_stream(&d.a_stream, d.num_cus, true));
+          TRY(create_stream(&d.a_stream, d.num_cus));
+          TRY(create_stream(&d.a_stream2, d.num_cus));
           HIP_TRY(hipEventCreateWithFlags(&d.cross_entry, hipEventDisableTiming));
           HIP_TRY(hipMalloc(reinterpret_cast<void **>(&d.decision), 256));
           HIP_TRY(hipMemsetAsync(d.decision, 0, 256, d.stream));
@@ -378,8 +379,9 @@ struct SplitStep {
         hipEvent_t e = spans ? tr[k].slot->entry : d.cross_entry;
         HIP_TRY(hipEventRecord(e, d.stream));
         HIP_TRY(hipStreamWaitEvent(d.a_stream, e, 0));
-        if (two_a) HIP_TRY(hipStreamWaitEvent(d.a_stream2, e, 0));
+        HIP_TRY(hipStreamWaitEvent(d.a_stream2, e, 0));
         note_wait(k, 1, e);
+        note_wait(k, 3, e);
         if (spans) tr[k].last[0] = e;  // everything before it on the sync stream
       }
       if (ocheck) {
@@ -415,13 +417,14 @@ struct SplitStep {
       cbx::Timing t;
       if (b == 0) t.start = pipelined ? step_start_event(c, d, 2) : ring_event(c, d, EV_START);
       if (!pipelined) t.stop = ring_event(c, d, EV_A);
-      hipStream_t st = cross ? (two_a && (b & 1) ? d.a_stream2 : d.a_stream) : d.stream;
-      const int si = cross ? 1 : 0;
-      // Two A streams: the per-stream position decides the wait; waiting on
+      // Cross-step mode: even buckets on a_stream, odd ones on a_stream2.
+      hipStream_t st = cross ? ((b & 1) ? d.a_stream2 : d.a_stream) : d.stream;
+      const int si = cross ? ((b & 1) ? 3 : 1) : 0;
+      // The wait goes by the position on the kernel's own stream; waiting on
       // a later B implies every earlier one (the B's run in order).
-      const int64_t pos = two_a ? b / 2 : b;
-      if (cross && !join[k] && pos % wait_stride == 0) {  // B(b .. b+stride-1) of the last step
-        const int64_t w = std::min<int64_t>(two_a ? b + 2 * (wait_stride - 1) : b + wait_stride - 1, nb - 1);
+      const int64_t pos = cross ? b / 2 : b;
+      if (cross && !join[k] && pos % wait_stride == 0) {  // B(b), B(b+2) .. of the last step
+        const int64_t w = std::min<int64_t>(b + 2 * (wait_stride - 1), nb - 1);
         hipEvent_t e = ocheck ? d.ord[d.ord_cur ^ 1u].b1[w] : spans ? tr[k].prev->b_used[w] : d.bucket_b[w];
         HIP_TRY(hipStreamWaitEvent(st, e, 0));
         note_wait(k, si, e);

@@ -1,12 +1,16 @@
 #!/usr/bin/env python3
-"""A/B on one MI355X: the G > 1 bucket pipeline (forced at G = 1, one-rank
-RCCL) in cross-step mode with kernels A on one stream vs alternating over two
-($CBX_EXP_TWO_A, read at context creation), so bucket k+1's waves can fill
-the CUs while bucket k's drain.  ResNet-50, R = 8, momentum 0.9; ms per step
-(wall clock over back-to-back steps), interleaved passes, best pass kept.
-Variants: one / two A streams, with or without the per-dispatch span events
-($CBX_EXP_NO_SPANS), and one stream with timing off altogether.
-JSON lines on stdout."""
+"""The G > 1 bucket pipeline forced at G = 1 (one-rank RCCL) on one MI355X:
+ms per step by bucket count, pipeline mode and cross-step wait stride,
+ResNet-50, R = 8, momentum 0.9 (wall clock over back-to-back steps,
+interleaved passes, best pass kept), with timing on ("spans": the bench's
+setting, per-dispatch span events) and off ("notiming").  A repeated variant
+gets a context of its own (a placement check).  JSON lines on stdout.
+
+Round 3 ran it with experiment toggles (kernels A on one or two streams;
+library streams from the shared hardware-queue pool, on CU-mask queues of
+their own, or at high priority): profiles/r03/pipeline_streams_ab.json (as scripts/two_a_ab.py).  The
+winner, two A streams on CU-mask streams, is now the library's behaviour
+and the toggles are gone."""
 from __future__ import annotations
 
 import json
@@ -21,16 +25,6 @@ sys.path.insert(0, ROOT)
 def make(variant):
     from crossbow_amd import SYNC_BSP, UPDATE_SMA, TheGPU
     from crossbow_amd.variables import MODELS, register
-    for k in ("CBX_EXP_TWO_A", "CBX_EXP_NO_SPANS", "CBX_EXP_QUEUES"):
-        os.environ.pop(k, None)
-    if "cumask" in variant:
-        os.environ["CBX_EXP_QUEUES"] = "cumask"
-    if "prio" in variant:
-        os.environ["CBX_EXP_QUEUES"] = "prio"
-    if "two" in variant:
-        os.environ["CBX_EXP_TWO_A"] = "1"
-    if "nospans" in variant:
-        os.environ["CBX_EXP_NO_SPANS"] = "1"
     g = TheGPU()
     g.init([0])
     n = register(g, MODELS["resnet50"]())
@@ -65,7 +59,7 @@ def timed(g, steps=30, warmup=5):
 def main():
     import argparse
     ap = argparse.ArgumentParser()
-    ap.add_argument("--variants", default="one-spans,one-nospans,two-nospans,one-notiming")
+    ap.add_argument("--variants", default="spans,notiming")
     ap.add_argument("--configs", default="1/0/1,4/1/1,8/1/1,8/1/2,8/1/4,8/0/1")
     ap.add_argument("--passes", type=int, default=3)
     a = ap.parse_args()

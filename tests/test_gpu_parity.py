@@ -268,6 +268,21 @@ def test_pipelined_timing_spans(mode):
         g.free()
 
 
+def test_hip_event_elapsed_time_is_signed():
+    """The kernel-span union (context_internal.h span_sum) takes every event's
+    time relative to one reference, so events before it must read negative."""
+    import torch
+    s = torch.cuda.Stream()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(s)
+    with torch.cuda.stream(s):
+        torch.cuda._sleep(2_000_000)
+    e1.record(s)
+    e1.synchronize()
+    assert e0.elapsed_time(e1) > 0 and e1.elapsed_time(e0) < 0
+    assert abs(e0.elapsed_time(e1) + e1.elapsed_time(e0)) < 1e-3
+
+
 def test_timing_history_after_the_ring_wraps():
     """More back-to-back fused steps than the timing ring holds (1024): a step
     queued behind a busy GPU borrows the previous slot's stop as its start, and
