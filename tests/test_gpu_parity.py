@@ -229,11 +229,11 @@ def test_pipelined_timing_spans(mode):
     bounded its start), so N > 1 benches report the kernels as they ran in
     the timed region; beyond 64 buckets the step keeps no spans (-1)."""
     from crossbow_amd import _lib
-    n, R = 200_000, 2
+    n, R = 300_000, 2
     g = make_gpu(n, R, 0.1, 0.9)
     try:
         g.set_force_split(True)
-        g.set_bucket_elements(16_384)  # 13 buckets
+        g.set_bucket_elements(16_384)  # 19 buckets
         g.set_pipeline_mode(mode)
         g.fill_synthetic(7)
         g.set_timing(True)
@@ -250,7 +250,7 @@ def test_pipelined_timing_spans(mode):
         assert len(hk) == 6 and all(x > 0 for x in hk) and all(x > 0 for x in hb) and all(x > 0 for x in hs)
         if mode == 0:  # one stream: A and B never overlap, so their busy time fits in the step
             assert all(k + b <= s * 1.001 + 0.002 for k, b, s in zip(hk, hb, hs)), (hk, hb, hs)
-        g.set_bucket_elements(1024)  # 196 buckets: more than the span records keep
+        g.set_bucket_elements(4096)  # 74 buckets (4,096 floats, the smallest): more than the span records keep
         for c in range(6, 8):
             g.lockAny()
             g.synchronise(0, c, 0, False)
