@@ -672,23 +672,21 @@ inline int probe_device(int hip_id, int *num_cus) {
   return CBX_OK;
 }
 
-// A stream for the library's own work, on a hardware queue of its own.
-// ROCclr maps ordinary streams onto a pool of GPU_MAX_HW_QUEUES (4) queues
-// per device, shared by every stream of the process (torch's, RCCL's, ours);
-// two streams on one queue serialise at every stream wait, so the bucket
-// pipeline's waits on one stream stall the kernels of another.  Which
-// streams collide depends on creation order: 8-bucket cross-step steps
-// measured 0.59-0.62 ms on some contexts and 0.72-1.1 ms on others
-// (profiles/r03/pipeline_streams_ab.json).  A stream with a CU mask gets a
-// queue of its own (the mask is a queue property); the mask here is every
-// CU.  Such a stream synchronises with the null stream, as a default-flag
-// stream does (the reference's is non-blocking, executioncontext.c:324): the
-// only effect is extra ordering against null-stream work.
-inline int create_stream(hipStream_t *s, int num_cus) {
-  uint32_t mask[16] = {};
-  const int cus = std::min(num_cus, 512);
-  for (int i = 0; i < cus; ++i) mask[i / 32] |= 1u << (i % 32);
-  HIP_TRY(hipExtStreamCreateWithCUMask(s, (uint32_t)((cus + 31) / 32), mask));
+// A non-blocking stream for the library's own work (executioncontext.c:324).
+// ROCclr maps streams onto a pool of GPU_MAX_HW_QUEUES (4) hardware queues
+// per device, shared by every stream of the process: a new stream takes a
+// new queue until the pool is full, then the least-used one.  Two streams on
+// one queue serialise at every stream wait, so the bucket pipeline's waits
+// on one stream would stall another's kernels: 8-bucket cross-step steps
+// measured 0.59-0.62 ms on some contexts and 0.72-1.1 ms on others, by
+// creation order (profiles/r03/pipeline_streams_ab.json).  So a device's four
+// streams (sync, comm, and the two of kernels A) are created together in
+// open_device, before RCCL creates its own, and take the pool's first
+// queues.  (CU-mask streams get queues of their own but synchronise with the
+// null stream, and that deadlocked two real-RCCL ranks: a synchronous copy
+// on one waited for a collective the other could not enqueue.)
+inline int create_stream(hipStream_t *s) {
+  HIP_TRY(hipStreamCreateWithFlags(s, hipStreamNonBlocking));
   return CBX_OK;
 }
 
@@ -698,8 +696,10 @@ inline int open_device(Device &d, int hip_id, int g) {
   d.g = g;
   d.file_id = g;
   // executioncontext.c:324: one non-blocking model-synchronisation stream.
-  TRY(create_stream(&d.stream, d.num_cus));
-  TRY(create_stream(&d.comm_stream, d.num_cus));
+  TRY(create_stream(&d.stream));
+  TRY(create_stream(&d.comm_stream));
+  TRY(create_stream(&d.a_stream));
+  TRY(create_stream(&d.a_stream2));
   HIP_TRY(hipEventCreateWithFlags(&d.synched, hipEventDisableTiming));
   for (int k = 0; k < EV_COUNT; ++k) HIP_TRY(hipEventCreate(&d.ev[k]));
   return CBX_OK;

@@ -364,9 +364,7 @@ struct SplitStep {
         }
       }
       if (cross) {
-        if (!d.a_stream) {
-          TRY(create_stream(&d.a_stream, d.num_cus));
-          TRY(create_stream(&d.a_stream2, d.num_cus));
+        if (!d.cross_entry) {
           HIP_TRY(hipEventCreateWithFlags(&d.cross_entry, hipEventDisableTiming));
           HIP_TRY(hipMalloc(reinterpret_cast<void **>(&d.decision), 256));
           HIP_TRY(hipMemsetAsync(d.decision, 0, 256, d.stream));
