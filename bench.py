@@ -37,6 +37,9 @@ import sys
 import tempfile
 import time
 
+# before the HIP runtime starts (crossbow_amd/_lib.py explains the value)
+os.environ.setdefault("GPU_MAX_HW_QUEUES", "16")
+
 ROOT = os.path.dirname(os.path.abspath(__file__))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)

@@ -1,6 +1,9 @@
 import os
 import sys
 
+# before any HIP runtime starts in this process or its children (crossbow_amd/_lib.py)
+os.environ.setdefault("GPU_MAX_HW_QUEUES", "16")
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
