@@ -187,7 +187,11 @@ def _rank_main(rank, world, jobs, d, q):
         cases = {c.name: c for c in CASES}
         goldens = {gc["name"]: gc for gc in C.golden_cases(world)}
         out = []
+        progress = os.environ.get("CBX_TEST_PROGRESS_DIR")  # a diagnosis aid: one line per job start / end
         for j, (kind, name) in enumerate(jobs):
+            if progress:
+                with open(os.path.join(progress, f"realrccl_w{world}_r{rank}.log"), "a") as f:
+                    f.write(f"start {j} {kind} {name}\n")
             g = C.init_rank(L, A, rank, world, share_uid(L, rank, os.path.join(d, f"uid_{j}")))
             try:
                 if kind == "case":
@@ -208,6 +212,9 @@ def _rank_main(rank, world, jobs, d, q):
             finally:
                 g.free()
             out.append((name, res))
+            if progress:
+                with open(os.path.join(progress, f"realrccl_w{world}_r{rank}.log"), "a") as f:
+                    f.write(f"end {j} {kind} {name} bad={bool(res['bad'])}\n")
         q.put((rank, out, None))
     except Exception:  # pragma: no cover - reported to the parent
         import traceback
