@@ -442,18 +442,22 @@ struct SplitStep {
 
   // The collective of bucket b (common.c:14-54: grouped, fp32 sum; bucket 0
   // also carries the control block right in front of the data).  `wait_acc`:
-  // the comm stream first waits for kernel A of that bucket (-1: no wait; an
-  // earlier collective of the same group already waited on a later bucket,
-  // which implies this one: A runs in order).
-  int collective(int64_t b, bool on_comm, int64_t wait_acc, size_t k0, size_t k1) {
+  // the comm stream first waits for kernels A up to that bucket, from bucket
+  // `wait_from` on (-1: no wait; an earlier collective of the same group
+  // already waited).  Kernels A run in order on their stream, so the last
+  // one implies the earlier ones; in cross-step mode they alternate over two
+  // streams, and the last one on each stream is waited for.
+  int collective(int64_t b, bool on_comm, int64_t wait_from, int64_t wait_acc, size_t k0, size_t k1) {
     const int64_t start = start_of(b), len = len_of(b);
     if (on_comm && wait_acc >= 0 && !c->fault_skip_comm_wait) {
       for (size_t k = k0; k < k1; ++k) {
         Device &d = c->devs[k];
         HIP_TRY(hipSetDevice(d.hip_id));
-        hipEvent_t e = ev_a(k, wait_acc);
-        HIP_TRY(hipStreamWaitEvent(d.comm_stream, e, 0));
-        note_wait(k, 2, e);
+        for (int64_t a = wait_acc; a >= wait_from && a > wait_acc - (cross ? 2 : 1); --a) {
+          hipEvent_t e = ev_a(k, a);
+          HIP_TRY(hipStreamWaitEvent(d.comm_stream, e, 0));
+          note_wait(k, 2, e);
+        }
       }
     }
     for (size_t k = k0; ocheck && k < k1; ++k) {
@@ -578,7 +582,7 @@ struct SplitStep {
     for (size_t k = k0; k < k1; ++k) TRY(prepare_device(k));
     if (!pipelined) {
       TRY(accumulate(0, k0, k1));
-      TRY(collective(0, false, -1, k0, k1));
+      TRY(collective(0, false, -1, -1, k0, k1));
       for (size_t k = k0; k < k1; ++k) {
         Device &d = c->devs[k];
         HIP_TRY(hipSetDevice(d.hip_id));
@@ -599,7 +603,7 @@ struct SplitStep {
         TRY(accumulate(b, k0, k1));
         if ((b + 1) % ar_group != 0 && b != nb - 1) continue;
         const int64_t g0 = b - b % ar_group;
-        for (int64_t j = g0; j <= b; ++j) TRY(collective(j, true, j == g0 ? b : -1, k0, k1));
+        for (int64_t j = g0; j <= b; ++j) TRY(collective(j, true, g0, j == g0 ? b : -1, k0, k1));
         const int64_t upto = cross ? b + 1 : g0;
         for (; applied < upto; ++applied) TRY(apply(applied, k0, k1));
       }
