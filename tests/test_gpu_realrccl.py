@@ -167,7 +167,11 @@ def run_order(g, world, algo):
     g("cbx_fill_synthetic", 5)
     g("cbx_set_order_check", 1)
     bad = []
+    progress = os.environ.get("CBX_TEST_PROGRESS_DIR")
     for step in range(6):
+        if progress:
+            with open(os.path.join(progress, f"order_w{world}_pid{os.getpid()}.log"), "a") as f:
+                f.write(f"algo {algo} step {step}\n")
         g("cbx_lock_any")
         g("cbx_synchronise", 0, step + 1, 0, 0)
         g("cbx_unlock_any")
@@ -188,6 +192,10 @@ def _rank_main(rank, world, jobs, d, q):
         goldens = {gc["name"]: gc for gc in C.golden_cases(world)}
         out = []
         progress = os.environ.get("CBX_TEST_PROGRESS_DIR")  # a diagnosis aid: one line per job start / end
+        if progress:  # and every rank's Python stacks after 100 s (where a hang sits on the host)
+            import faulthandler
+            tb = open(os.path.join(progress, f"realrccl_w{world}_r{rank}.stacks"), "w")
+            faulthandler.dump_traceback_later(100, repeat=False, file=tb)
         for j, (kind, name) in enumerate(jobs):
             if progress:
                 with open(os.path.join(progress, f"realrccl_w{world}_r{rank}.log"), "a") as f:
