@@ -121,14 +121,14 @@ def _spawn(world, target, args_of_rank, timeout):
         for _ in range(world):
             rank, res, err = q.get(timeout=timeout)
             got[rank] = (res, err)
+            # A rank that failed leaves the others waiting in a collective it
+            # will never join: report it now instead of hanging to the timeout.
+            assert err is None, f"rank {rank}:\n{err}"
     finally:
         for p in procs:
-            p.join(timeout=30)
+            p.join(timeout=30 if len(got) == world else 1)
             if p.is_alive():
                 p.kill()
-    for rank in range(world):
-        res, err = got[rank]
-        assert err is None, f"rank {rank}:\n{err}"
     return {r: got[r][0] for r in range(world)}
 
 
