@@ -36,8 +36,8 @@ for s in "${STEPS[@]}"; do
         run "single_n$g" 300 python bench.py --gpus $g --single-process --rehearse-one-gpu --steps 20 --warmup 3 \
           --no-staged --no-cpu-baseline
       done
-      for g in 2 4; do
-        run "perrank_n$g" 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node $g --master-addr 127.0.0.1 \
+      for g in 2 4 8; do
+        run "perrank_n$g" 500 python -m torch.distributed.run --nnodes=1 --nproc-per-node $g --master-addr 127.0.0.1 \
           --master-port $((29600 + g)) bench.py --gpus $g --rehearse-one-gpu --steps 20 --warmup 3 --no-staged
       done ;;
     enqueue)
