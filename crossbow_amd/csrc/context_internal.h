@@ -134,7 +134,10 @@ class EnqueuePool {
       std::unique_lock<std::mutex> l(m_);
       cv_done_.wait(l, [this] { return pending_.load(std::memory_order_acquire) == 0; });
     }
-    job_ = nullptr;
+    {
+      std::lock_guard<std::mutex> l(m_);  // a worker outside this run may be reading it
+      job_ = nullptr;
+    }
     for (int k = 0; k < n; ++k)
       if (rc_[k] < 0) {
         g_last_error = err_[k];
