@@ -23,6 +23,7 @@
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
+#include <exception>
 #include <functional>
 #include <map>
 #include <memory>
@@ -111,7 +112,11 @@ class EnqueuePool {
   int run(int n, const std::function<int(int)> &fn) {
     while ((int)threads_.size() < n - 1) {
       const int k = (int)threads_.size() + 1;
-      threads_.emplace_back([this, k] { worker(k); });
+      try {
+        threads_.emplace_back([this, k] { worker(k); });
+      } catch (const std::exception &e) {  // no exception crosses the C-ABI
+        return fail(CBX_ERR_STATE, "cannot start enqueue thread %d: %s", k, e.what());
+      }
     }
     rc_.assign(n, 0);
     err_.assign(n, std::string());
