@@ -590,6 +590,10 @@ def main():
         if rccl_log:
             gpu.wait()
             result["allreduce"]["rccl_tuning"] = rccl_tuning(rccl_log)
+            try:
+                os.remove(rccl_log)
+            except OSError:
+                pass
             result["allreduce"]["rccl_tuning_source"] = (
                 "RCCL's own log (NCCL_DEBUG=INFO, NCCL_DEBUG_SUBSYS=TUNING), this process, every collective of the "
                 "run (calibration, tuning, timed)")
