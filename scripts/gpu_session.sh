@@ -3,6 +3,7 @@
 #   tests      the whole -m gpu suite
 #   tests:K    only the tests matching -k K
 #   bench      python bench.py $BENCH_ARGS
+#   smoke      __graft_entry__.smoke()
 #   rehearse   bench.py at N = 2 / 4 / 8 in both process forms on one GPU
 #   enqueue    scripts/host_enqueue_multidev.py (single-process host cost)
 #   rocprof    rocprofv3 --kernel-trace --stats of bench.py $BENCH_ARGS
@@ -31,6 +32,7 @@ for s in "${STEPS[@]}"; do
     tests) run pytest_gpu 900 $PYTEST tests ;;
     tests:*) run "pytest_${s#tests:}" 600 $PYTEST tests -k "${s#tests:}" ;;
     bench) run bench 600 python bench.py ${BENCH_ARGS:-} ;;
+    smoke) run smoke 300 python -c "import __graft_entry__ as e; e.smoke()" ;;
     rehearse)
       for g in 2 4 8; do
         run "single_n$g" 300 python bench.py --gpus $g --single-process --rehearse-one-gpu --steps 20 --warmup 3 \
