@@ -7,6 +7,10 @@
 //   2 writeval : producer hipStreamWriteValue32(flag, k+1); consumer hipStreamWaitValue32(flag >= k+1)
 //   3 kernel   : the producer kernel's last workgroup publishes k+1 itself (release atomic);
 //                consumer hipStreamWaitValue32(flag >= k+1); no packet on the producer stream
+//   4 kernel-signal : as 3, the flag in hipMallocSignalMemory memory (what
+//                hipStreamWaitValue32 documents) and a system-scope release
+//   5 kernel-nowait : the producer publishes as in 3, nobody waits (the
+//                publish's own cost); 6 kernel-signal-nowait likewise for 4
 // Prints producer-stream time per kernel and total time (JSON lines).
 // Build: hipcc --offload-arch=gfx950 -O3 -o syncbench syncbench.hip
 #include <hip/hip_runtime.h>
@@ -28,7 +32,7 @@ typedef float v4f __attribute__((ext_vector_type(4)));
 
 // 8 read streams + 4 write streams per element, one float4 per lane.
 __global__ __launch_bounds__(256) void produce(const v4f *__restrict__ in, v4f *__restrict__ out, uint32_t n4,
-                                               uint32_t *flag, uint32_t value, uint32_t *ticket) {
+                                               uint32_t *flag, uint32_t value, uint32_t *ticket, int system_scope) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n4) {
     v4f t = 0.0f;
@@ -46,7 +50,12 @@ __global__ __launch_bounds__(256) void produce(const v4f *__restrict__ in, v4f *
       if (done == gridDim.x) {
         *ticket = 0;
         __threadfence();
-        __hip_atomic_store(flag, value, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        if (system_scope) {
+          __threadfence_system();
+          __hip_atomic_store(flag, value, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        } else {
+          __hip_atomic_store(flag, value, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        }
       }
     }
   }
@@ -67,6 +76,9 @@ int main(int argc, char **argv) {
   CK(hipMalloc(&out, (size_t)4 * n4 * 16));
   CK(hipMalloc(&small, 4096));
   CK(hipMalloc(&flag, 256));
+  uint32_t *sflag = nullptr;
+  CK(hipExtMallocWithFlags(reinterpret_cast<void **>(&sflag), 256, hipMallocSignalMemory));
+  CK(hipMemset(sflag, 0, 256));
   CK(hipMalloc(&ticket, 256));
   CK(hipMemset(in, 0, (size_t)8 * n4 * 16));
   CK(hipMemset(flag, 0, 256));
@@ -92,7 +104,7 @@ int main(int argc, char **argv) {
     CK(hipEventRecord(fork, p));
     CK(hipStreamWaitEvent(c, fork, 0));
     for (int k = 0; k < nk; ++k) {
-      hipLaunchKernelGGL(produce, dim3(grid), dim3(256), 0, p, in, out, n4, nullptr, 0u, ticket);
+      hipLaunchKernelGGL(produce, dim3(grid), dim3(256), 0, p, in, out, n4, nullptr, 0u, ticket, 0);
       CK(hipEventRecord(ev[k], p));
       CK(hipStreamWaitEvent(c, ev[k], 0));
       hipLaunchKernelGGL(consume, dim3(1), dim3(64), 0, c, small, (uint32_t)k);
@@ -119,7 +131,7 @@ int main(int argc, char **argv) {
                 tot * 1e3 / reps / nk);
   }
   for (int round = 0; round < 3; ++round)
-    for (int mode = 0; mode < 4; ++mode) {
+    for (int mode = 0; mode < 7; ++mode) {
       float prod_ms = 0, tot_ms = 0;
       for (int r = 0; r < reps + 2; ++r) {
         CK(hipDeviceSynchronize());
@@ -127,18 +139,19 @@ int main(int argc, char **argv) {
         CK(hipStreamWaitEvent(c, t0, 0));
         for (int k = 0; k < nk; ++k) {
           const uint32_t v = ++counter;
-          hipLaunchKernelGGL(produce, dim3(grid), dim3(256), 0, p, in, out, n4, mode == 3 ? flag : nullptr, v,
-                             ticket);
+          uint32_t *f = (mode == 3 || mode == 5) ? flag : (mode == 4 || mode == 6) ? sflag : nullptr;
+          hipLaunchKernelGGL(produce, dim3(grid), dim3(256), 0, p, in, out, n4, f, v, ticket,
+                             (mode == 4 || mode == 6) ? 1 : 0);
           if (mode == 1) {
             CK(hipEventRecord(ev[k], p));
             CK(hipStreamWaitEvent(c, ev[k], 0));
           } else if (mode == 2) {
             CK(hipStreamWriteValue32(p, flag, v, 0));
             CK(hipStreamWaitValue32(c, flag, v, hipStreamWaitValueGte, 0xffffffffu));
-          } else if (mode == 3) {
-            CK(hipStreamWaitValue32(c, flag, v, hipStreamWaitValueGte, 0xffffffffu));
+          } else if (mode == 3 || mode == 4) {
+            CK(hipStreamWaitValue32(c, mode == 3 ? flag : sflag, v, hipStreamWaitValueGte, 0xffffffffu));
           }
-          if (mode != 0) hipLaunchKernelGGL(consume, dim3(1), dim3(64), 0, c, small, (uint32_t)k);
+          if (mode >= 1 && mode <= 4) hipLaunchKernelGGL(consume, dim3(1), dim3(64), 0, c, small, (uint32_t)k);
         }
         CK(hipEventRecord(t1, p));
         CK(hipEventRecord(t2, c));
@@ -149,10 +162,11 @@ int main(int argc, char **argv) {
         CK(hipEventElapsedTime(&b, t0, t2));
         if (r >= 2) {
           prod_ms += a;
-          tot_ms += (mode == 0 ? a : (b > a ? b : a));
+          tot_ms += (mode == 0 || mode >= 5 ? a : (b > a ? b : a));
         }
       }
-      const char *names[] = {"none", "event", "writeval", "kernel-flag"};
+      const char *names[] = {"none", "event", "writeval", "kernel-flag", "kernel-flag-signal", "kernel-flag-nowait",
+                             "kernel-flag-signal-nowait"};
       std::printf("{\"round\":%d,\"mode\":\"%s\",\"kernels\":%d,\"producer_us_per_kernel\":%.2f,\"total_us_per_kernel\":%.2f}\n",
                   round, names[mode], nk, prod_ms * 1e3 / reps / nk, tot_ms * 1e3 / reps / nk);
       std::fflush(stdout);
