@@ -77,8 +77,8 @@ int main(int argc, char **argv) {
   CK(hipMalloc(&small, 4096));
   CK(hipMalloc(&flag, 256));
   uint32_t *sflag = nullptr;
-  CK(hipExtMallocWithFlags(reinterpret_cast<void **>(&sflag), 256, hipMallocSignalMemory));
-  CK(hipMemset(sflag, 0, 256));
+  CK(hipExtMallocWithFlags(reinterpret_cast<void **>(&sflag), 8, hipMallocSignalMemory));  // a signal: 8 bytes
+  CK(hipMemset(sflag, 0, 8));
   CK(hipMalloc(&ticket, 256));
   CK(hipMemset(in, 0, (size_t)8 * n4 * 16));
   CK(hipMemset(flag, 0, 256));
