@@ -6,7 +6,8 @@
  * batch-norm statistics),
  * autotune add / del (also while task threads reserve, lock and release
  * replicas: the ids they hold may be deleted under them), BN averaging,
- * timing queries and teardown.
+ * timing queries, one process over four (repeated) devices with the
+ * per-device enqueue threads on and off, and teardown.
  *
  * Built with host-side AddressSanitizer + UndefinedBehaviorSanitizer
  * (scripts/build_sanitized.sh: -Xarch_host -fsanitize=..., GPU code is not
@@ -42,10 +43,10 @@
 		}                                                                            \
 	} while (0)
 
-static cbx_context *setup (int n1, int n2, int R, int sync, int type, float momentum) {
+static cbx_context *setup_on (int ndev, int n1, int n2, int R, int sync, int type, float momentum) {
 	cbx_context *c = NULL;
-	int dev = 0;
-	CHECK (cbx_init (&c, &dev, 1));
+	int devs[4] = { 0, 0, 0, 0 };  /* one card repeated: the one-process form rehearsed */
+	CHECK (cbx_init (&c, devs, ndev));
 	int bytes = 4 * (n1 + n2);
 	CHECK (cbx_set_model (c, 2, bytes));
 	int s1[2] = { n1 / 4, 4 }, s2[1] = { n2 };
@@ -62,9 +63,13 @@ static cbx_context *setup (int n1, int n2, int R, int sync, int type, float mome
 	CHECK (cbx_set_weight_decay (c, 1e-4f));
 	CHECK (cbx_set_eamsgd_alpha (c, 0.1f));
 	CHECK (cbx_set_model_manager (c, R, sync));
-	EXPECT (cbx_num_replicas (c) == R);
+	EXPECT (cbx_num_replicas (c) == ndev * R);  /* R per device */
 	EXPECT (cbx_model_elements (c) == n1 + n2);
 	return c;
+}
+
+static cbx_context *setup (int n1, int n2, int R, int sync, int type, float momentum) {
+	return setup_on (1, n1, n2, R, sync, type, momentum);
 }
 
 static void barrier (cbx_context *c, int clock, int autotune) {
@@ -245,6 +250,9 @@ int main (void) {
 	EXPECT (cbx_set_cross_wait_stride (c, 0) == CBX_ERR_INVALID);
 	EXPECT (cbx_check_order (c) == CBX_ERR_STATE);  /* not enabled */
 	EXPECT (cbx_set_allreduce_algorithm (c, 3) == CBX_ERR_INVALID);
+	EXPECT (cbx_set_enqueue_threads (c, 2) == CBX_ERR_INVALID);
+	EXPECT (cbx_set_enqueue_threads (c, -2) == CBX_ERR_INVALID);
+	CHECK (cbx_set_enqueue_threads (c, 1));  /* one device: a pool of one thread */
 	for (int clock = 3; clock < 13; ++clock) {
 		if (clock == 5) CHECK (cbx_replica_set_copy (c, 1, 1));
 		if (clock == 6) CHECK (cbx_set_pipeline_mode (c, 0));  /* back to within-step buckets */
@@ -327,6 +335,26 @@ int main (void) {
 		CHECK (cbx_average_batchnorm_stats (c, 2, elements, mean, var, updated));
 	}
 	CHECK (cbx_free (c));
+
+	/* One process over several devices (the card repeated, so peer reads):
+	 * each device's step enqueued by its own pool thread, then by this one,
+	 * within-step and cross-step buckets, the pool torn down by cbx_free. */
+	for (int threads = 1; threads >= 0; --threads) {
+		c = setup_on (4, n1, n2, 1, CBX_SYNC_BSP, CBX_UPDATE_SMA, 0.9f);
+		CHECK (cbx_set_allreduce_algorithm (c, CBX_ALLREDUCE_PEER));
+		CHECK (cbx_set_enqueue_threads (c, threads));
+		CHECK (cbx_set_bucket_elements (c, 4096));
+		for (int clock = 1; clock < 7; ++clock) {
+			if (clock == 4) CHECK (cbx_set_pipeline_mode (c, 1));
+			CHECK (cbx_lock_any (c));
+			CHECK (cbx_synchronise (c, 0, clock, 0, 0));
+			CHECK (cbx_unlock_any (c));
+		}
+		CHECK (cbx_wait (c));
+		CHECK (cbx_replica_read (c, 3, CBX_BUF_DATA, host, (size_t) 4 * n));
+		EXPECT (all_finite (host, (size_t) n));
+		CHECK (cbx_free (c));
+	}
 	free (host);
 	printf ("abi_driver: ok\n");
 	fflush (stdout);
