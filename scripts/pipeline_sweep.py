@@ -9,8 +9,10 @@ gets a context of its own (a placement check).  JSON lines on stdout.
 Round 3 ran it with experiment toggles (kernels A on one or two streams;
 library streams from the shared hardware-queue pool, on CU-mask queues of
 their own, or at high priority): profiles/r03/pipeline_streams_ab.json (as scripts/two_a_ab.py).  The
-winner, two A streams on CU-mask streams, is now the library's behaviour
-and the toggles are gone."""
+library now runs kernels A on two streams; its four streams are plain
+non-blocking streams created together, each on a hardware queue of its own
+(GPU_MAX_HW_QUEUES 16; CU-mask streams synchronise with the null stream, so
+they were not kept), and the toggles are gone."""
 from __future__ import annotations
 
 import json
