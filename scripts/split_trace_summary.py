@@ -10,7 +10,6 @@ rows.sort(key=lambda r: int(r["Start_Timestamp"]))
 ev = [(("A" if "accumulate" in r["Kernel_Name"] else "B"), int(r["Start_Timestamp"]), int(r["End_Timestamp"]),
        int(r["Grid_Size_X"]), r["Queue_Id"]) for r in rows]
 full = max(e[3] for e in ev if e[0] == "A")
-one = [e for e in ev if e[3] == full or (e[0] == "B" and e[3] >= max(x[3] for x in ev if x[0] == "B"))]
 def union(iv):
     iv = sorted(iv); tot = 0; lo, hi = iv[0]
     for a, b in iv[1:]:
