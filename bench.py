@@ -29,15 +29,23 @@ Run:  python bench.py [--gpus N --steps K --warmup W]
 from __future__ import annotations
 
 import argparse
+import faulthandler
 import json
 import os
 import re
+import signal
+import socket
 import statistics
+import subprocess
 import sys
 import tempfile
+import threading
 import time
 
-# before the HIP runtime starts (crossbow_amd/_lib.py explains the value)
+# Before the HIP runtime starts (it reads this once): the bucket pipeline
+# needs a hardware queue per library stream (crossbow_amd/_lib.py, DESIGN.md
+# section 5); an explicit setting by the caller wins and is reported.
+HW_QUEUES_SET_BY = "caller" if "GPU_MAX_HW_QUEUES" in os.environ else "bench.py default"
 os.environ.setdefault("GPU_MAX_HW_QUEUES", "16")
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -94,12 +102,94 @@ def parse():
                         "the default when --gpus N > 1 runs without a torch.distributed.run environment. With "
                         "--rehearse-one-gpu every device is device 0 and the all-reduce is the peer-read form "
                         "(RCCL refuses a repeated device)")
-    p.add_argument("--no-rccl-tuning-log", action="store_true",
-                   help="N > 1 with RCCL: do not log RCCL's per-collective tuning choices (NCCL_DEBUG=INFO, "
-                        "NCCL_DEBUG_SUBSYS=TUNING into a file) for the allreduce.rccl_tuning field")
+    p.add_argument("--rccl-tuning-log", action="store_true",
+                   help="N > 1 with RCCL: log RCCL's per-collective tuning choices (NCCL_DEBUG=INFO, "
+                        "NCCL_DEBUG_SUBSYS=TUNING into a file) in THIS run for the allreduce.rccl_tuning field "
+                        "(one log line per collective on the host's enqueue path, so off by default)")
+    p.add_argument("--no-rccl-tuning-run", action="store_true",
+                   help="N > 1 with RCCL: skip the separate short run (same configuration, RCCL's tuning log on) "
+                        "that fills allreduce.rccl_tuning after the timed region")
+    p.add_argument("--bucket-elements", type=int, default=0,
+                   help="G>1 pipeline bucket in fp32 elements (overrides --bucket-mb; skips the tuner)")
+    p.add_argument("--pipeline-mode", type=int, default=None, help="with an explicit bucket size: 0 or 1")
+    p.add_argument("--wait-stride", type=int, default=None, help="with an explicit bucket size: cross-step wait stride")
+    p.add_argument("--allreduce-group", type=int, default=None, help="with an explicit bucket size: all-reduce group")
+    p.add_argument("--allreduce-algorithm", type=int, default=None,
+                   help="with an explicit bucket size: 0 all-reduce, 1 peer-read, 2 reduce-scatter + all-gather")
+    p.add_argument("--enqueue-threads", type=int, default=None,
+                   help="one process over N devices, explicit bucket size: 0 one thread (the reference's), 1 per device")
+    p.add_argument("--watchdog-scale", type=float, default=1.0,
+                   help="multiplies every phase deadline of the watchdog (0 = off); on a missed deadline the run "
+                        "writes every thread's stack to stderr and exits with code 3")
+    p.add_argument("--watchdog-selftest", type=float, default=0.0, help=argparse.SUPPRESS)
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
                    help="PMC-derived HBM bytes per launch (written by scripts/pmc_traffic.py)")
     return p.parse_args()
+
+
+class Watchdog:
+    """Deadlines per phase of the run, so a run that stalls (a collective
+    that never completes, a tuner candidate that hangs, a lost device) ends
+    with a diagnosis instead of silently: a daemon thread checks the current
+    phase's deadline and, once it passes, writes which phase and which tuner
+    candidate were in flight, the last completed phase and every thread's
+    Python stack (faulthandler) to stderr, then leaves with os._exit(3) (no
+    restart, no exec).  Every phase is one stderr line on rank 0."""
+
+    def __init__(self, scale: float, rank: int):
+        self.scale, self.rank = scale, rank
+        self.phase, self.deadline, self.seconds, self.last_done = None, None, 0.0, None
+        self.lock = threading.Lock()
+        if scale > 0:
+            threading.Thread(target=self._watch, name="bench-watchdog", daemon=True).start()
+
+    def enter(self, name: str, seconds: float) -> None:
+        with self.lock:
+            if self.phase is not None:
+                self.last_done = self.phase
+            self.phase, self.seconds = name, seconds * self.scale
+            self.deadline = time.monotonic() + self.seconds if self.scale > 0 else None
+        if self.rank == 0:
+            log(f"[bench] phase {name}" + (f" (deadline {self.seconds:.0f} s)" if self.scale > 0 else ""))
+
+    def stop(self) -> None:
+        with self.lock:
+            self.deadline = None
+
+    def _watch(self) -> None:
+        while True:
+            time.sleep(0.2)
+            with self.lock:
+                late = self.deadline is not None and time.monotonic() > self.deadline
+                phase, secs, done = self.phase, self.seconds, self.last_done
+            if late:
+                sys.stderr.write(f"[bench] WATCHDOG rank {self.rank}: phase '{phase}' missed its {secs:.0f} s "
+                                 f"deadline; last completed phase: '{done}'; stacks of every thread follow\n")
+                sys.stderr.flush()
+                faulthandler.dump_traceback(file=sys.stderr, all_threads=True)
+                sys.stderr.flush()
+                os._exit(3)
+
+
+def free_port() -> int:
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
+
+
+def lib_buckets(n: int, bucket_elems: int, G: int) -> int:
+    """The bucket count the library cuts n elements into (SplitStep::prepare_common)."""
+    pad = 1024
+    n4 = -(-(-(-n // 4)) // pad) * pad
+    if bucket_elems <= 0:
+        if G <= 1:
+            return 1
+        b4 = -(-(n4 // 8) // pad) * pad
+    else:
+        b4 = -(-(bucket_elems // 4) // pad) * pad
+    if b4 <= 0 or b4 > n4:
+        b4 = n4
+    return -(-n4 // b4)
 
 
 def alg_bytes(n, R, momentum, G):
@@ -315,8 +405,60 @@ def span_stats(gpu, _lib, locals_, steps):
     return tuple(out)
 
 
+def rccl_tuning_run(args, G, single, cfg, wd):
+    """RCCL's own algorithm / protocol / channel choices for the collectives
+    of the chosen configuration, from a separate short run (3 steps) with
+    RCCL's TUNING log on: the log writes a line per collective on the host's
+    enqueue path, so the measured run keeps it off.  The same process form
+    and device selection as this run; returns (entries or None, source)."""
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(G), "--steps", "3", "--warmup", "1",
+           "--calib-steps", "1", "--no-cpu-baseline", "--no-staged", "--no-copy-ceiling", "--no-optimiser",
+           "--no-seam", "--rccl-tuning-log", "--no-rccl-tuning-run", "--watchdog-scale", str(args.watchdog_scale),
+           "--model", args.model, "--replicas", str(args.replicas), "--alpha", str(args.alpha),
+           "--momentum", str(args.momentum), "--bucket-elements", str(cfg["bucket_elements"]),
+           "--pipeline-mode", str(cfg["mode"]), "--wait-stride", str(cfg["stride"]),
+           "--allreduce-group", str(cfg["group"]), "--allreduce-algorithm", str(cfg["algorithm"])]
+    if args.rehearse_one_gpu:
+        cmd.append("--rehearse-one-gpu")
+    env = {k: v for k, v in os.environ.items() if not k.startswith(("NCCL_DEBUG", "NCCL_HOSTID"))}
+    if single:
+        cmd += ["--single-process"]
+        if cfg.get("enqueue_threads") is not None:
+            cmd += ["--enqueue-threads", str(cfg["enqueue_threads"])]
+    else:
+        for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "GROUP_RANK", "GROUP_WORLD_SIZE",
+                  "ROLE_RANK", "ROLE_WORLD_SIZE", "ROLE_NAME", "MASTER_ADDR", "MASTER_PORT"):
+            env.pop(k, None)
+        env = {k: v for k, v in env.items() if not k.startswith("TORCHELASTIC")}
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(G),
+               "--master-addr", "127.0.0.1", "--master-port", str(free_port())] + cmd[1:]
+    wd.enter("rccl tuning run", 420)
+    p = subprocess.Popen(cmd, cwd=ROOT, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True,
+                         start_new_session=True)
+    try:
+        out, err = p.communicate(timeout=360)
+    except subprocess.TimeoutExpired:
+        os.killpg(p.pid, signal.SIGKILL)
+        p.communicate()
+        return None, "the separate tuning-log run timed out (360 s)"
+    if p.returncode != 0:
+        return None, f"the separate tuning-log run failed (rc {p.returncode}): {err.strip()[-300:]}"
+    try:
+        line = [ln for ln in out.splitlines() if ln.strip()][-1]
+        t = json.loads(line)["allreduce"]["rccl_tuning"]
+    except (IndexError, KeyError, ValueError) as e:
+        return None, f"the separate tuning-log run printed no tuning table ({e})"
+    return t, ("RCCL's own log (NCCL_DEBUG=INFO, NCCL_DEBUG_SUBSYS=TUNING) of a separate 3-step run of the same "
+               "configuration and process form: the timed steps above ran without the log")
+
+
 def main():
     args = parse()
+    if args.watchdog_selftest > 0:  # CPU test of the watchdog: a phase that stalls past its deadline
+        wd = Watchdog(1.0, 0)
+        wd.enter("selftest stall", args.watchdog_selftest)
+        time.sleep(args.watchdog_selftest * 20 + 10)
+        raise SystemExit("watchdog did not fire")
     # stdout carries the ONE JSON line and nothing else: native libraries
     # print banners there (RCCL's "RCCL version : ..." at communicator init),
     # so fd 1 is pointed at stderr for the run and the result goes to a
@@ -324,6 +466,10 @@ def main():
     sys.stdout.flush()
     result_out = os.fdopen(os.dup(1), "w")
     os.dup2(2, 1)
+    rank0 = int(os.environ.get("RANK", "0"))
+    wd = Watchdog(args.watchdog_scale, rank0)
+    # the first `import torch` on a fresh box can take minutes (image paging)
+    wd.enter("init (torch, HIP, communicators)", 900)
     from crossbow_amd import dist as D
     rank, world, local_rank = D.env_rank()
     G = args.gpus
@@ -342,21 +488,16 @@ def main():
                              "(one process per GPU) or without it (one process over N GPUs)")
     nlocal = G if single else 1
     peer_only = single and args.rehearse_one_gpu  # RCCL refuses a repeated device: the peer-read form only
-    rccl_log, rccl_why = None, None
-    if G > 1 and not peer_only:
-        if args.no_rccl_tuning_log:
-            rccl_why = "--no-rccl-tuning-log"
-        elif os.environ.get("NCCL_DEBUG_FILE"):
-            rccl_why = f"NCCL_DEBUG_FILE={os.environ['NCCL_DEBUG_FILE']} set by the caller"
-        else:
-            # RCCL reads these once, at its first call: every collective then
-            # logs its algorithm / protocol / channels (one line each) to the file.
-            rccl_log = os.path.join(tempfile.gettempdir(), f"cbx_rccl_tuning.r{rank}.{os.getpid()}.log")
-            os.environ.update(NCCL_DEBUG="INFO", NCCL_DEBUG_SUBSYS="TUNING", NCCL_DEBUG_FILE=rccl_log)
+    rccl_log = None
+    if G > 1 and not peer_only and args.rccl_tuning_log:
+        # RCCL reads these once, at its first call: every collective then logs
+        # its algorithm / protocol / channels (one line each) to the file.
+        rccl_log = os.path.join(tempfile.gettempdir(), f"cbx_rccl_tuning.r{rank}.{os.getpid()}.log")
+        os.environ.update(NCCL_DEBUG="INFO", NCCL_DEBUG_SUBSYS="TUNING", NCCL_DEBUG_FILE=rccl_log)
 
     import torch
 
-    from crossbow_amd import SYNC_BSP, UPDATE_SMA, TheGPU, _lib
+    from crossbow_amd import SYNC_BSP, UPDATE_SMA, CbxError, TheGPU, _lib
     ALLREDUCE_PEER = _lib.ALLREDUCE_PEER
     from crossbow_amd.variables import MODELS, register
 
@@ -369,6 +510,7 @@ def main():
         uid = D.share_unique_id(rank, world, TheGPU.unique_id)
         gpu.init_rank(local_rank, world, rank, uid)
 
+    wd.enter("setup (model, synthetic replicas)", 300)
     shapes = MODELS[args.model]()
     n = register(gpu, shapes)
     gpu.setUpdateModelType(UPDATE_SMA)
@@ -382,7 +524,11 @@ def main():
     gpu.set_kernel_config(args.block, args.blocks_per_cu, args.policy, args.unroll)
     gpu.set_kernel_occupancy(args.waves_per_cu)
     one_bucket = 1 << 62
-    bucket_elems = int(args.bucket_mb * (1 << 20) / 4) if args.bucket_mb > 0 else (one_bucket if args.bucket_mb < 0 else 0)
+    if args.bucket_elements > 0:
+        bucket_elems = args.bucket_elements
+    else:
+        bucket_elems = int(args.bucket_mb * (1 << 20) / 4) if args.bucket_mb > 0 else (one_bucket if args.bucket_mb < 0 else 0)
+    explicit = bucket_elems != 0
     if args.force_split:
         gpu.set_force_split(True)
     if peer_only:
@@ -397,8 +543,10 @@ def main():
         nonlocal clock
         clock += 1
         gpu.lockAny()
-        gpu.synchronise(0, clock, 0, False)
-        gpu.unlockAny()
+        try:
+            gpu.synchronise(0, clock, 0, False)
+        finally:
+            gpu.unlockAny()
 
     split = G > 1 or args.force_split
     calib = None
@@ -409,6 +557,7 @@ def main():
     if split:
         # Calibration: one bucket, everything in order on the sync stream, so
         # HIP events separate kernel A, the collective and kernel B.
+        wd.enter("calibration (one bucket, in order)", 180)
         gpu.set_bucket_elements(one_bucket)
         for _ in range(args.calib_steps):
             step()
@@ -420,23 +569,37 @@ def main():
                  "step": list(gpu.timing_history(_lib.T_STEP)[-k:])}
     gpu.set_bucket_elements(bucket_elems)
     tuning = None
-    pipeline_mode = 0
-    wait_stride = 1
-    ar_group = 1
-    ar_algo = ALLREDUCE_PEER if peer_only else 0
-    if split and args.bucket_mb == 0 and not peer_only:
-        # warm-up autotune of the bucket count on the live communicator (same choice on every rank)
-        bucket_elems, pipeline_mode, wait_stride, ar_group, ar_algo, tuning = D.tune_buckets(
-            gpu, n, world, step, progress=(lambda m: log(f"[bench] {m}")) if rank == 0 else None,
-            ndev=G, peer=single)
+    chosen = {"bucket_elements": bucket_elems, "buckets": lib_buckets(n, bucket_elems, G), "mode": 0, "stride": 1,
+              "group": 1, "algorithm": ALLREDUCE_PEER if peer_only else 0,
+              "enqueue_threads": 0 if single else None}
+    if split and not explicit:
+        # warm-up autotune of the pipeline on the live communicator (same choice on every rank)
+        tuning = D.tune_buckets(gpu, n, world, step, progress=(lambda m: log(f"[bench] {m}")) if rank == 0 else None,
+                                ndev=G, peer=single, peer_only=peer_only, threads=single,
+                                phase=lambda name: wd.enter(name, 90))
+        chosen.update(bucket_elements=tuning.bucket_elements, buckets=tuning.buckets, mode=tuning.mode,
+                      stride=tuning.stride, group=tuning.group, algorithm=tuning.algorithm,
+                      enqueue_threads=tuning.enqueue_threads)
+    elif split:
+        for key, flag, setter in (("mode", args.pipeline_mode, gpu.set_pipeline_mode),
+                                  ("stride", args.wait_stride, gpu.set_cross_wait_stride),
+                                  ("group", args.allreduce_group, gpu.set_allreduce_group),
+                                  ("algorithm", args.allreduce_algorithm, gpu.set_allreduce_algorithm)):
+            if flag is not None:
+                setter(flag)
+                chosen[key] = flag
+        if single and args.enqueue_threads is not None:
+            gpu.set_enqueue_threads(args.enqueue_threads)
+            chosen["enqueue_threads"] = args.enqueue_threads
+    ar_algo = chosen["algorithm"]
 
+    wd.enter("warm-up", 180)
     for _ in range(args.warmup):
         step()
     gpu.wait()
     torch.cuda.synchronize()
     D.barrier(world)
-    if rank == 0:
-        log("[bench] timed region")
+    wd.enter("timed region", 120 + 0.2 * args.steps)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         h0 = time.perf_counter()
@@ -447,6 +610,7 @@ def main():
     el = time.perf_counter() - t0
     D.barrier(world)
     el = D.max_over_ranks(el, world)
+    wd.enter("timing read-back", 120)
     spans = span_stats(gpu, _lib, nlocal, args.steps) if split else None
 
     step_bytes, kernel_bytes = alg_bytes(n, args.replicas, args.momentum, 2 if split else 1)
@@ -482,15 +646,17 @@ def main():
             "parallelism": f"sma-dp{G}",
             "process_form": None if G == 1 else ("single" if single else "per-rank"),
             "pipeline": "fused" if not split else "accumulate+collective+apply, bucketed on two streams",
-            "buckets": (None if not split else 1 if ar_algo == ALLREDUCE_PEER else
-                        int(min(tuning, key=lambda k: tuning[k]).split("/")[0])
-                        if tuning and not min(tuning, key=lambda k: tuning[k]).startswith("peer")
-                        else -(-n // min(bucket_elems, n)) if bucket_elems else "library default (8)"),
-            "pipeline_mode": None if not split else pipeline_mode,
-            "cross_wait_stride": None if not split else wait_stride,
-            "allreduce_group": None if not split else ar_group,
-            "allreduce_algorithm": None if not split else form,
-            "bucket_tuning_ms_per_step": tuning,
+            "buckets": chosen["buckets"] if split else None,
+            "pipeline_mode": chosen["mode"] if split else None,
+            "cross_wait_stride": chosen["stride"] if split else None,
+            "allreduce_group": chosen["group"] if split else None,
+            "allreduce_algorithm": form if split else None,
+            "enqueue_threads": chosen["enqueue_threads"] if single else None,
+            "bucket_tuning_ms_per_step": tuning.table if tuning else None,
+            "tuning_errors": tuning.errors if tuning else None,
+            # ROCclr's hardware queues per device (read once at HIP start): the
+            # pipeline's streams each need one
+            "hw_queues": {"GPU_MAX_HW_QUEUES": int(os.environ["GPU_MAX_HW_QUEUES"]), "set_by": HW_QUEUES_SET_BY},
             "kernel_config": dict(block=args.block, blocks_per_cu=args.blocks_per_cu, policy=args.policy,
                                   unroll=args.unroll, waves_per_cu=args.waves_per_cu, bucket_mb=args.bucket_mb),
         },
@@ -525,6 +691,7 @@ def main():
                 "launch_ms_mean": round(kern_ms, 4), "launch_ms_median": round(statistics.median(kern), 4),
                 "launches": len(kern), "timed_in": timed_in}
 
+    coll_busy = None
     if not split:
         result["roofline"] = roofline(list(gpu.timing_history(_lib.T_KERNEL)[-args.steps:]), "timed region")
     else:
@@ -533,20 +700,24 @@ def main():
         # the calibration's one-bucket, in-order figure is kept apart.
         b_bytes = (12 + 8 * (1 if args.momentum > 0 else 0)) * n
         unpiped = roofline(calib["kernel"], "calibration steps (one bucket, in order)")
+        # the slowest rank's mean times set the roofline and the link rate (max
+        # over ranks; every rank takes part in both reductions)
+        a_max = D.max_over_ranks(statistics.mean(spans[0]) if spans else -1.0, world)
+        coll_max = D.max_over_ranks(statistics.mean(spans[1]) if spans else -1.0, world)
         if spans is not None:
             a_ms, coll_ms, b_ms = spans
-            # the slowest rank's mean kernel time sets the roofline (max over ranks)
             result["roofline"] = roofline(
                 a_ms, "timed region: per step, the summed busy spans of kernel A's dispatches (each its stop minus "
                       "the latest event bounding its start: an upper bound incl. dispatch latency), beside the "
                       f"collectives; {'mean over the local devices, ' if nlocal > 1 else ''}slowest rank",
-                mean_ms=D.max_over_ranks(statistics.mean(a_ms), world))
+                mean_ms=a_max)
             result["roofline"]["apply_kernel"] = roofline(b_ms, "timed region (summed busy spans of kernel B)",
                                                           b_bytes, "sma_apply_kernel")
             ab = [x + y for x, y in zip(a_ms, b_ms)]
             result["roofline"]["a_plus_b"] = roofline(ab, "timed region (kernels A + B)", kernel_bytes + b_bytes,
                                                       "sma_accumulate_kernel+sma_apply_kernel")
-            result["roofline"]["collective_busy_ms_mean"] = round(statistics.mean(coll_ms), 4)
+            coll_busy = coll_max
+            result["roofline"]["collective_busy_ms_mean"] = round(coll_busy, 4)
         else:
             result["roofline"] = dict(unpiped, timed_in=unpiped["timed_in"] + " (the timed steps kept no spans)")
         result["roofline_unpipelined"] = unpiped
@@ -557,6 +728,7 @@ def main():
         # Host side of the step (lockAny + synchronise + unlockAny, every local
         # device's enqueue) against the device's step: the single-process form
         # enqueues all G devices' kernels and collectives from one thread.
+        wd.enter("host enqueue (idle GPU)", 120)
         idle = []
         for _ in range(5):
             gpu.wait()
@@ -576,17 +748,29 @@ def main():
                                "refuses a repeated device): the single-process form's host side and code path, "
                                "not an N-GPU measurement")
     if split:
+        # The link: the collective's bytes per GPU over its busy time.  An
+        # all-reduce (either form) moves 2(G-1)/G x 4n bytes per GPU (busbw);
+        # the peer-read reduction reads (G-1)/G x 4n of its shard from the
+        # peers (kernel B's remote reads of D sit inside kernel B's span).
+        def link(ms, timed_in):
+            if not ms or ms <= 0 or G <= 1:
+                return {"ms": round(ms, 4) if ms else ms, "timed_in": timed_in}
+            algbw = 4 * n / (ms * 1e-3) / 1e9
+            busbw = algbw * ((G - 1) / G if ar_algo == ALLREDUCE_PEER else 2 * (G - 1) / G)
+            return {"ms": round(ms, 4), "algbw_GBs": round(algbw, 1), "busbw_GBs": round(busbw, 1),
+                    "xgmi_frac": round(busbw / ((G - 1) * XGMI_LINK_GBS), 4), "timed_in": timed_in}
         ar_ms = statistics.median(calib["allreduce"])
-        algbw = 4 * n / (ar_ms * 1e-3) / 1e9
-        busbw = algbw * 2 * (G - 1) / G if G > 1 else 0.0
-        result["allreduce"] = {"form": form, "ms_median": round(ar_ms, 4), "algbw_GBs": round(algbw, 1),
-                               "busbw_GBs": round(busbw, 1),
-                               # a G-GPU all-reduce can use the G-1 links from each GPU to its peers
-                               "xgmi_links": G - 1, "xgmi_peak_GBs": (G - 1) * XGMI_LINK_GBS,
-                               "xgmi_frac": round(busbw / ((G - 1) * XGMI_LINK_GBS), 4) if G > 1 else None,
-                               "apply_ms_median": round(statistics.median(calib["apply"]), 4),
-                               "unpipelined_step_ms_median": round(statistics.median(calib["step"]), 4),
-                               "timed_in": "calibration steps (one bucket, in order)"}
+        unp = link(ar_ms, "calibration steps (one bucket, in order: the collective alone)")
+        unp.update(apply_ms_median=round(statistics.median(calib["apply"]), 4),
+                   step_ms_median=round(statistics.median(calib["step"]), 4))
+        timed = (link(coll_busy, "timed region: per step, the union of the collectives' busy spans (each from the "
+                                 "latest event bounding its start to its end), beside kernels A and B; slowest rank")
+                 if coll_busy else None)
+        result["allreduce"] = {"form": form, "xgmi_links": G - 1, "xgmi_peak_GBs": (G - 1) * XGMI_LINK_GBS,
+                               "bytes_per_step": 4 * n,
+                               "busbw_note": ("peer-read: (G-1)/G x 4n remote bytes per GPU in the reduction" if
+                                              ar_algo == ALLREDUCE_PEER else "2(G-1)/G x 4n bytes per GPU"),
+                               "timed": timed, "unpipelined": unp}
         if rccl_log:
             gpu.wait()
             result["allreduce"]["rccl_tuning"] = rccl_tuning(rccl_log)
@@ -595,11 +779,8 @@ def main():
             except OSError:
                 pass
             result["allreduce"]["rccl_tuning_source"] = (
-                "RCCL's own log (NCCL_DEBUG=INFO, NCCL_DEBUG_SUBSYS=TUNING), this process, every collective of the "
-                "run (calibration, tuning, timed)")
-        elif G > 1:
-            result["allreduce"]["rccl_tuning"] = None
-            result["allreduce"]["rccl_tuning_source"] = rccl_why or "no RCCL collective in this form"
+                "RCCL's own log (NCCL_DEBUG=INFO, NCCL_DEBUG_SUBSYS=TUNING) of THIS run (--rccl-tuning-log): every "
+                "collective of calibration, tuning and the timed region")
 
     if G > 1 and not args.no_staged and peer_only:
         result["host_staged"] = {"skipped": "the host-staged step's collective is RCCL's, which refuses a repeated device"}
@@ -610,7 +791,7 @@ def main():
         # all-reduce / kernel B per bucket.  Max over ranks of the median of 3.
         # The pinned mirror is allocated first (no collective); every rank
         # must have one before any rank enters the staged step's collectives.
-        from crossbow_amd import CbxError
+        wd.enter("host-staged step", 300)
         why = None
         try:
             gpu.stage_in()
@@ -637,16 +818,20 @@ def main():
                 "timed": "HIP events per device (staged step: host in, host and device out), max over devices"}}
 
     if rank == 0 and G == 1 and not args.no_optimiser:
+        wd.enter("replica optimiser step", 120)
         result["replica_optimiser"] = bench_optimiser(gpu, torch, n, args)
     if rank == 0 and G == 1 and not args.no_seam:
+        wd.enter("sma.c seam", 180)
         result["seam"] = bench_seam(torch, n, args)
 
     if rank == 0 and G == 1:
         if not args.no_copy_ceiling:
+            wd.enter("copy ceiling", 120)
             result["copy_ceiling_GBs"] = round(gpu.bench_copy(1 << 30, 20), 1)
         if not args.no_staged:
             # Host-staged rate (north_star): pinned H2D of z, last, s_i, w_i,
             # the step, pinned D2H of z, last, w_i.  Reported, never `value`.
+            wd.enter("host-staged step", 300)
             samples = []
             for _ in range(3):
                 gpu.stage_in()
@@ -696,6 +881,7 @@ def main():
                 "timed": "HIP events on the fused staged kernel's own dispatch (one launch: host in, host + device out)"}
         if not args.no_cpu_baseline:
             # multithreaded first: OpenBLAS's pool must not start out bound to core 0
+            wd.enter("CPU baseline", 4 * args.cpu_seconds + 240)
             threads = max(1, min(16, len(os.sched_getaffinity(0))))
             mt = cpu_baseline_threads(args, n, threads)
             result["cpu_baseline"] = cpu_baseline(args, n)
@@ -705,7 +891,26 @@ def main():
         else:
             result["cpu_baseline"] = None
 
+    wd.enter("free", 120)
     gpu.free()
+    if split and G > 1 and not rccl_log:
+        # RCCL's algorithm / protocol / channel choices, from a separate short
+        # run of the chosen configuration with RCCL's tuning log on (rank 0
+        # launches it once this run's buffers are freed; the others wait).
+        if peer_only or ar_algo == ALLREDUCE_PEER:
+            entries, source = None, "no RCCL collective in the chosen form"
+        elif args.no_rccl_tuning_run:
+            entries, source = None, "--no-rccl-tuning-run"
+        elif rank == 0:
+            entries, source = rccl_tuning_run(args, G, single, chosen, wd)
+        else:
+            wd.enter("rccl tuning run (rank 0's)", 420)
+            entries, source = None, None
+        if world > 1:
+            D.barrier(world)
+        result["allreduce"]["rccl_tuning"] = entries
+        result["allreduce"]["rccl_tuning_source"] = source
+    wd.stop()
     if rank == 0:
         print(json.dumps(result), file=result_out, flush=True)
     D.finalize(world)

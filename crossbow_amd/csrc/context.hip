@@ -1371,6 +1371,9 @@ int cbx_set_timing(cbx_context *c, int enable) {
     d.ring_count = 0;
     d.span_pos = 0;
     d.span_last = -1;
+    // The span records a continuing cross-step step would start from are
+    // gone with the ring: the next cross-pipelined step joins.
+    d.cross_valid = false;
     if (c->timing && d.ring.empty()) {
       HIP_TRY(hipSetDevice(d.hip_id));
       d.ring.resize((size_t)Device::kRing * 4, nullptr);

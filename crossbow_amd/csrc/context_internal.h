@@ -412,7 +412,9 @@ struct Device {
   // that includes the dispatch latency (SplitStep, cbx_timing_history).
   static constexpr int kSpanRing = 64;
   static constexpr int64_t kSpanMaxBuckets = 64;
-  static constexpr int kSpanPreds = 4;
+  // a peer-read reduction waits for the last kernel A on both A streams of
+  // every device, plus its stream's previous dispatch
+  static constexpr int kSpanPreds = 2 * cbx::kMaxDevices + 2;
   enum SpanKind { SPAN_A = 0, SPAN_B = 1, SPAN_COLL = 2 };
   struct SpanRec {
     hipEvent_t stop = nullptr;
@@ -497,13 +499,24 @@ struct cbx_context {
   // at context creation drops the comm stream's wait on kernel A, so the
   // collective races its input (results are then wrong; tests only).
   bool fault_skip_comm_wait = std::getenv("CBX_FAULT_SKIP_COMM_WAIT") != nullptr;
+  // $CBX_FAULT_ONE_STREAM_COMM_WAIT restores the wait the pipeline had before
+  // round 3's fix: with kernels A on two streams (mode 1) and all-reduce
+  // groups, the group's comm wait covers only its last kernel A, not the last
+  // one on the other A stream; a one-wave delay ahead of every kernel A that
+  // wait skips makes the race certain (tests only: results are then wrong).
+  bool fault_one_stream_comm_wait = std::getenv("CBX_FAULT_ONE_STREAM_COMM_WAIT") != nullptr;
+  // $CBX_FAULT_FAIL_STEP_BUCKETS=N: a split SMA step over exactly N buckets
+  // fails before it enqueues anything (the bench tuner's error path, tests only).
+  int64_t fault_fail_buckets = std::getenv("CBX_FAULT_FAIL_STEP_BUCKETS")
+                                   ? std::atoll(std::getenv("CBX_FAULT_FAIL_STEP_BUCKETS")) : 0;
   // Bumped by every C-ABI call that may enqueue work on a sync stream other
   // than the barrier path itself: a cross-step pipelined step then joins the
   // whole sync stream instead of waiting bucket by bucket.
   std::atomic<unsigned long long> foreign_ops{0};
-  // One process over several local devices: each device's share of a barrier
-  // step is enqueued by a thread of its own (cbx_set_enqueue_threads; -1 auto
-  // = on with two or more local devices, 0 = the reference's one thread).
+  // One process over several local devices: 1 = each device's share of a
+  // barrier step is enqueued by a thread of its own (cbx_set_enqueue_threads);
+  // 0 and -1 (auto, the default) = the reference's one thread, until the
+  // threaded form is measured on distinct devices (bench.py's tuner times both).
   int enqueue_threads = -1;
   std::unique_ptr<cbx::host::EnqueuePool> pool;
 };
@@ -511,7 +524,7 @@ struct cbx_context {
 namespace cbx::host {
 
 // Whether a barrier step enqueues each local device's work on its own thread.
-inline bool threaded(const cbx_context *c) { return c->devs.size() > 1 && c->enqueue_threads != 0; }
+inline bool threaded(const cbx_context *c) { return c->devs.size() > 1 && c->enqueue_threads == 1; }
 
 // Runs fn(k) for every local device k, on one thread per device when the
 // context enqueues threaded, else in device order on this thread.

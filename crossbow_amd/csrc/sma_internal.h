@@ -192,6 +192,9 @@ hipError_t launch_sma_shard_momentum(const SmaArgs &a, const LaunchConfig &cfg, 
 // An empty dispatch whose own timestamps mark a point on `stream` (the
 // stream-order check, cbx_set_order_check).
 hipError_t launch_order_probe(hipStream_t stream, Timing t);
+// One wave idling `ticks` of the wall clock (hipDeviceAttributeWallClockRate,
+// kHz), touching no memory: fault injection for the order check's own tests.
+hipError_t launch_delay(hipStream_t stream, uint64_t ticks);
 // Host-staged step through zero-copy (cbx_synchronise_staged, staging mode
 // CBX_STAGING_ZEROCOPY): the kernels read their inputs straight from the
 // pinned host mirror over PCIe and write their outputs to the host mirror AND

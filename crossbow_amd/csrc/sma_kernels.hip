@@ -569,7 +569,10 @@ __global__ __launch_bounds__(256) void sma_peer_reduce_kernel(const PeerArgs p) 
 // pointer is fetched with a scalar load).
 template <bool MOM, int P, int U>
 __global__ __launch_bounds__(256) void sma_peer_apply_kernel(const SmaArgs a, const PeerArgs p) {
-  const bool copy = a.ctrl_in[0] > 0.0f;
+  // the Phase-D decision as in sma_apply_kernel (decision_mode: cross-step buckets)
+  const float requests = a.decision_mode == 2 ? *a.decision : a.ctrl_in[0];
+  if (a.decision_mode == 1 && blockIdx.x == 0 && threadIdx.x == 0) *a.decision = requests;
+  const bool copy = requests > 0.0f;
   const uint32_t trip = gridDim.x * blockDim.x * U;
   const uint32_t n4 = (uint32_t)a.n4;
   const uint32_t shard4 = (uint32_t)p.shard4;
@@ -1193,6 +1196,20 @@ __global__ void order_probe_kernel() {}
 
 hipError_t launch_order_probe(hipStream_t stream, Timing t) {
   hipExtLaunchKernelGGL(order_probe_kernel, dim3(1), dim3(64), 0, stream, t.start, t.stop, 0);
+  return hipGetLastError();
+}
+
+// One wave that idles for `ticks` of the constant-rate wall clock (fault
+// injection only: it holds back the kernel queued behind it on its stream, so
+// a race the injected fault opens is certain rather than timing-dependent).
+// No memory is touched; the loop is bounded whatever the clock does.
+__global__ void delay_kernel(uint64_t ticks) {
+  const uint64_t t0 = wall_clock64();
+  for (int i = 0; i < (1 << 20) && wall_clock64() - t0 < ticks; ++i) __builtin_amdgcn_s_sleep(8);
+}
+
+hipError_t launch_delay(hipStream_t stream, uint64_t ticks) {
+  hipLaunchKernelGGL(delay_kernel, dim3(1), dim3(64), 0, stream, ticks);
   return hipGetLastError();
 }
 

@@ -106,13 +106,20 @@ int ensure_comms(cbx_context *c) {
 
 // ---------------------------------------------------------------------------
 // Peer-read all-reduce, single process over G devices (sma_internal.h,
-// PeerArgs).  Per device, all on its sync stream:
-//   A(g)  [wait A(h) of every other device]  R(g)  [wait R(h) ...]  B(g)
-// R(g) sums shard g of every device's acc into this device's D (device
-// order from +0), B(g) reads each shard of D from its owner.  The next
-// step's A(h) follows B(h) on h's stream, and B(h) waited for every R, so
-// no device overwrites an acc another device is still reading; R of the
-// next step waits for every A of it, which follow every B of this one.
+// PeerArgs): the collective of SplitStep below becomes R, a kernel on every
+// device g that sums shard g of the bucket from every device's acc into g's
+// own D (device order from +0), and kernel B reads each shard of D from its
+// owner.  Per bucket k, on device g:
+//   A_g(k)  ->  R_g(k) waits A_h(k) of EVERY device h  ->  B_g(k) waits R_h(k) of every h
+// One bucket: all three in order on the sync stream.  Buckets: A on the
+// A streams, R on the comm stream, B on the sync stream, exactly as the
+// RCCL all-reduce's pipeline (modes 0 and 1, wait strides, groups), so R(k)
+// and B(k) overlap A(k+1).  Cross-step safety, the RCCL form's plus the
+// peers': A_h(k) of the next step overwrites acc_h(k), which R_g(k) of this
+// step reads, and follows B_h(k) (stream order, or its cross-step wait),
+// which waited for every R_g(k); R_g(k) of the next step overwrites D_g(k),
+// which B_h(k) of this step reads, and waits for every A_h(k) of the next
+// step, which follow B_h(k).
 // ---------------------------------------------------------------------------
 int ensure_peer_access(cbx_context *c) {
   if (c->peer_ready) return CBX_OK;
@@ -136,64 +143,11 @@ int ensure_peer_access(cbx_context *c) {
   return CBX_OK;
 }
 
-int sma_step_peer(cbx_context *c, std::vector<cbx::SmaArgs> &args, bool mom) {
-  TRY(ensure_peer_access(c));
-  const int G = (int)c->devs.size();
+// Float4s per device shard of a peer-read bucket of `len4` float4s: whole
+// kPadFloat4 units, so a wave's float4s never straddle two owners.
+inline int64_t peer_shard4(int64_t len4, int G) {
   const int64_t pad = cbx::kPadFloat4;
-  const int64_t s4 = ((c->n4 + G - 1) / G + pad - 1) / pad * pad;  // float4s per shard
-  cbx::PeerArgs p;
-  std::memset(&p, 0, sizeof(p));
-  p.G = G;
-  p.shard4 = s4;
-  for (int h = 0; h < G; ++h) {
-    p.ctrl_in[h] = base_ctrl(c->devs[h], CBX_BUF_GRADIENT);
-    p.D[h] = reinterpret_cast<const cbx::v4f *>(base_dev(c, c->devs[h], CBX_BUF_DIFF));
-  }
-  // Three phases, each on every device before the next (a device waits on
-  // the others' events, which must be recorded first); with enqueue threads
-  // each phase runs one thread per device.
-  TRY(for_devices(c, [&](int k) -> int {
-    Device &d = c->devs[k];
-    HIP_TRY(hipSetDevice(d.hip_id));
-    cbx::LaunchConfig cfg = c->cfg;
-    cfg.num_cus = d.num_cus;
-    HIP_TRY(cbx::launch_sma_accumulate(args[k], true, cfg, d.stream, {ring_event(c, d, EV_START), ring_event(c, d, EV_A)}));
-    HIP_TRY(hipEventRecord(d.peer_a, d.stream));
-    return CBX_OK;
-  }));
-  TRY(for_devices(c, [&](int k) -> int {
-    Device &d = c->devs[k];
-    HIP_TRY(hipSetDevice(d.hip_id));
-    for (int h = 0; h < G; ++h)
-      if (h != k) HIP_TRY(hipStreamWaitEvent(d.stream, c->devs[h].peer_a, 0));
-    const int64_t start = std::min<int64_t>((int64_t)k * s4, c->n4);
-    cbx::PeerArgs r = p;
-    for (int h = 0; h < G; ++h)
-      r.acc[h] = reinterpret_cast<const cbx::v4f *>(base_dev(c, c->devs[h], CBX_BUF_GRADIENT)) + start;
-    r.out = reinterpret_cast<cbx::v4f *>(base_dev(c, d, CBX_BUF_DIFF)) + start;
-    r.ctrl_out = base_ctrl(d, CBX_BUF_DIFF);
-    r.n4 = std::min(s4, c->n4 - start);  // 0 for a trailing empty shard: block 0 still sums the control block
-    cbx::LaunchConfig cfg = c->apply_cfg;
-    cfg.num_cus = d.num_cus;
-    HIP_TRY(cbx::launch_sma_peer_reduce(r, cfg, d.stream, {nullptr, ring_event(c, d, EV_AR)}));
-    HIP_TRY(hipEventRecord(d.peer_r, d.stream));
-    return CBX_OK;
-  }));
-  TRY(for_devices(c, [&](int k) -> int {
-    Device &d = c->devs[k];
-    HIP_TRY(hipSetDevice(d.hip_id));
-    for (int h = 0; h < G; ++h)
-      if (h != k) HIP_TRY(hipStreamWaitEvent(d.stream, c->devs[h].peer_r, 0));
-    cbx::LaunchConfig cfg = c->apply_cfg;
-    cfg.num_cus = d.num_cus;
-    HIP_TRY(cbx::launch_sma_peer_apply(args[k], p, mom, cfg, d.stream, {nullptr, step_stop_event(c, d, EV_B)}));
-    d.span_last = -1;
-    ring_advance(c, d, 1);
-    d.cross_valid = false;
-    return CBX_OK;
-  }));
-  c->last_step_split = true;
-  return CBX_OK;
+  return ((len4 + G - 1) / G + pad - 1) / pad * pad;
 }
 
 // ---------------------------------------------------------------------------
@@ -227,9 +181,16 @@ struct SplitStep {
   std::vector<cbx::SmaArgs> &args;
   bool mom;
   int64_t b4 = 0, nb = 0, wait_stride = 1;
-  bool pipelined = false, cross = false, rsag = false, ocheck = false, spans = false;
+  bool pipelined = false, cross = false, rsag = false, peer = false, ocheck = false, spans = false;
   unsigned long long foreign = 0;
   std::vector<char> join;
+  // Peer-read steps enqueued by one thread per device: device k's count of
+  // this step's kernels A (a_seq) and reductions R (r_seq) enqueued with
+  // their events recorded.  A device enqueues a wait on another device's
+  // event only once that device's count covers it (a wait on an event not
+  // yet recorded would wait on its previous step's record instead).
+  std::unique_ptr<std::atomic<int64_t>[]> a_seq, r_seq;
+  std::atomic<bool> failed{false};
   // Kernel spans (Device::SpanSlot), per device: the step's slot, the
   // previous pipelined step's, the last stop event on each stream the step
   // uses (0 sync stream, 1 a_stream, 2 comm_stream, 3 a_stream2) and the
@@ -249,10 +210,30 @@ struct SplitStep {
   // The event kernel A(b) of this step stops (the collective of b waits on it).
   hipEvent_t ev_a(size_t k, int64_t b) {
     Device &d = c->devs[k];
+    if (peer && !pipelined) return d.peer_a;  // one bucket: recorded after A on the sync stream
     return ocheck ? d.ord[d.ord_cur].a1[b] : spans ? tr[k].slot->a[b] : d.bucket_acc[b];
   }
   // The event recorded on the comm stream after the collective of bucket b.
-  hipEvent_t ev_red(size_t k, int64_t b) { return spans ? tr[k].slot->red[b] : c->devs[k].bucket_red[b]; }
+  hipEvent_t ev_red(size_t k, int64_t b) {
+    if (peer && !pipelined) return c->devs[k].peer_r;
+    return spans ? tr[k].slot->red[b] : c->devs[k].bucket_red[b];
+  }
+
+  // Peer-read, threaded: publish that device k's event of bucket b is
+  // recorded / wait until every device's is.
+  void publish(std::unique_ptr<std::atomic<int64_t>[]> &seq, size_t k, int64_t b) {
+    if (seq) seq[k].store(b + 1, std::memory_order_release);
+  }
+  int await_all(std::unique_ptr<std::atomic<int64_t>[]> &seq, int64_t b) {
+    if (!seq) return CBX_OK;
+    for (size_t h = 0; h < c->devs.size(); ++h)
+      while (seq[h].load(std::memory_order_acquire) <= b) {
+        if (failed.load(std::memory_order_acquire))
+          return fail(CBX_ERR_STATE, "peer-read step: the enqueue of another device failed");
+        sched_yield();
+      }
+    return CBX_OK;
+  }
 
   void note_wait(size_t k, int s, hipEvent_t e) {
     if (spans) tr[k].pending[s].push_back(e);
@@ -311,8 +292,9 @@ struct SplitStep {
     if (t.prev) t.last[2] = t.prev->red[t.prev->nb - 1];
     if (!cross) {
       if (d.ring_count > 0) t.last[0] = ring_stop(d, prev_ring);
+    } else if (!join[k] && !t.prev) {
+      join[k] = 1;  // the previous step's span records are gone (timing reset): join the whole sync stream
     } else if (!join[k]) {  // continues the previous cross step bucket by bucket (same nb, spans on)
-      if (!t.prev) return fail(CBX_ERR_STATE, "span records of the previous step are missing");
       const int64_t last_odd = (nb - 1) & 1 ? nb - 1 : nb - 2, last_even = (nb - 1) & 1 ? nb - 2 : nb - 1;
       t.last[1] = t.prev->a_used[last_even];
       t.last[3] = t.prev->a_used[last_odd];
@@ -332,9 +314,21 @@ struct SplitStep {
     }
     if (b4 <= 0 || b4 > c->n4) b4 = c->n4;
     nb = (c->n4 + b4 - 1) / b4;
+    if (c->fault_fail_buckets > 0 && nb == c->fault_fail_buckets)
+      return fail(CBX_ERR_STATE, "fault injection: a split step over %lld buckets fails ($CBX_FAULT_FAIL_STEP_BUCKETS)",
+                  (long long)nb);
     pipelined = nb > 1;
     cross = pipelined && c->pipeline_mode == 1;
     rsag = c->allreduce_algo == CBX_ALLREDUCE_RSAG;
+    peer = c->allreduce_algo == CBX_ALLREDUCE_PEER && c->G > 1;
+    if (peer && threaded(c)) {
+      a_seq.reset(new std::atomic<int64_t>[c->devs.size()]);
+      r_seq.reset(new std::atomic<int64_t>[c->devs.size()]);
+      for (size_t k = 0; k < c->devs.size(); ++k) {
+        a_seq[k].store(0, std::memory_order_relaxed);
+        r_seq[k].store(0, std::memory_order_relaxed);
+      }
+    }
     ocheck = c->order_check && c->timing;
     spans = c->timing && !ocheck && pipelined && nb <= Device::kSpanMaxBuckets;
     for (Device &d : c->devs) spans = spans && !d.spans.empty();
@@ -428,14 +422,26 @@ struct SplitStep {
         note_wait(k, si, e);
       }
       if (pipelined) t.stop = ev_a(k, b);
+      if (cross && c->fault_one_stream_comm_wait) {
+        // Fault injection: a kernel A the faulted comm wait skips (not the
+        // last of its all-reduce group) starts 0.5 ms late.
+        const int64_t ar_group = std::max(1, c->allreduce_group);
+        if ((b + 1) % ar_group != 0 && b != nb - 1) {
+          int khz = 0;
+          HIP_TRY(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, d.hip_id));
+          HIP_TRY(cbx::launch_delay(st, (uint64_t)khz / 2));
+        }
+      }
       if (ocheck) {
         Device::OrderStep &o = d.ord[d.ord_cur];
         HIP_TRY(cbx::launch_order_probe(st, {nullptr, o.pa[b]}));
         o.a1[b] = t.stop;  // with timing on, A always carries a stop event (the pool's or the ring's)
       }
       HIP_TRY(cbx::launch_sma_accumulate(offset_args(args[k], start_of(b), len_of(b)), b == 0, cfg, st, t));
+      if (peer && !pipelined) HIP_TRY(hipEventRecord(d.peer_a, st));  // the other devices' R waits on it
       if (spans) tr[k].slot->a_used[b] = t.stop;
       note_dispatch(k, si, Device::SPAN_A, t.stop, b == 0 ? t.start : nullptr);
+      publish(a_seq, k, b);
     }
     return CBX_OK;
   }
@@ -450,14 +456,30 @@ struct SplitStep {
   int collective(int64_t b, bool on_comm, int64_t wait_from, int64_t wait_acc, size_t k0, size_t k1) {
     const int64_t start = start_of(b), len = len_of(b);
     if (on_comm && wait_acc >= 0 && !c->fault_skip_comm_wait) {
+      // the last kernel A on each A stream (two in cross-step mode); the
+      // peer-read reduction reads every device's acc, so it waits for every
+      // device's kernels A
+      const int64_t streams = cross && !c->fault_one_stream_comm_wait ? 2 : 1;
+      TRY(await_all(a_seq, wait_acc));
       for (size_t k = k0; k < k1; ++k) {
         Device &d = c->devs[k];
         HIP_TRY(hipSetDevice(d.hip_id));
-        for (int64_t a = wait_acc; a >= wait_from && a > wait_acc - (cross ? 2 : 1); --a) {
-          hipEvent_t e = ev_a(k, a);
-          HIP_TRY(hipStreamWaitEvent(d.comm_stream, e, 0));
-          note_wait(k, 2, e);
-        }
+        for (int64_t a = wait_acc; a >= wait_from && a > wait_acc - streams; --a)
+          for (size_t h = peer ? 0 : k; h < (peer ? c->devs.size() : k + 1); ++h) {
+            hipEvent_t e = ev_a(h, a);
+            HIP_TRY(hipStreamWaitEvent(d.comm_stream, e, 0));
+            note_wait(k, 2, e);
+          }
+      }
+    } else if (peer && !on_comm) {
+      // one bucket, in order on the sync stream: its own kernel A by stream
+      // order, the other devices' by their events
+      TRY(await_all(a_seq, b));
+      for (size_t k = k0; k < k1; ++k) {
+        Device &d = c->devs[k];
+        HIP_TRY(hipSetDevice(d.hip_id));
+        for (size_t h = 0; h < c->devs.size(); ++h)
+          if (h != k) HIP_TRY(hipStreamWaitEvent(d.stream, ev_a(h, b), 0));
       }
     }
     for (size_t k = k0; ocheck && k < k1; ++k) {
@@ -465,7 +487,32 @@ struct SplitStep {
       HIP_TRY(hipSetDevice(d.hip_id));
       HIP_TRY(cbx::launch_order_probe(on_comm ? d.comm_stream : d.stream, {nullptr, d.ord[d.ord_cur].c0[b]}));
     }
-    if (rsag) {
+    if (peer) {
+      // Peer-read reduction R: device k sums shard k of the bucket from every
+      // device's acc into its own D (device order from +0: the oracle's);
+      // bucket 0 also sums the control blocks.
+      const int G = (int)c->devs.size();
+      const int64_t sh4 = peer_shard4(len, G);
+      for (size_t k = k0; k < k1; ++k) {
+        Device &d = c->devs[k];
+        HIP_TRY(hipSetDevice(d.hip_id));
+        const int64_t s0 = std::min<int64_t>((int64_t)k * sh4, len);
+        cbx::PeerArgs r;
+        std::memset(&r, 0, sizeof(r));
+        r.G = G;
+        r.shard4 = sh4;
+        for (int h = 0; h < G; ++h) {
+          r.acc[h] = reinterpret_cast<const cbx::v4f *>(base_dev(c, c->devs[h], CBX_BUF_GRADIENT)) + start + s0;
+          r.ctrl_in[h] = base_ctrl(c->devs[h], CBX_BUF_GRADIENT);
+        }
+        r.out = reinterpret_cast<cbx::v4f *>(base_dev(c, d, CBX_BUF_DIFF)) + start + s0;
+        r.ctrl_out = b == 0 ? base_ctrl(d, CBX_BUF_DIFF) : nullptr;
+        r.n4 = std::min(sh4, len - s0);  // 0 for a trailing empty shard (one block runs, and sums the control block)
+        cbx::LaunchConfig cfg = c->apply_cfg;
+        cfg.num_cus = d.num_cus;
+        HIP_TRY(cbx::launch_sma_peer_reduce(r, cfg, on_comm ? d.comm_stream : d.stream));
+      }
+    } else if (rsag) {
       // Reduce-scatter form: shard g of the bucket (len / G float4s) is
       // reduced on rank g, which applies the base momentum to its shard of
       // last; the all-gather of last (or of D without momentum) then hands
@@ -532,18 +579,29 @@ struct SplitStep {
         HIP_TRY(hipEventRecord(ev_red(k, b), d.comm_stream));
         note_dispatch(k, 2, Device::SPAN_COLL, ev_red(k, b), nullptr);
       }
+    } else if (peer) {
+      for (size_t k = k0; k < k1; ++k) {  // the other devices' kernels B wait on it
+        Device &d = c->devs[k];
+        HIP_TRY(hipSetDevice(d.hip_id));
+        HIP_TRY(hipEventRecord(ev_red(k, b), d.stream));
+      }
     }
+    for (size_t k = k0; k < k1; ++k) publish(r_seq, k, b);
     return CBX_OK;
   }
 
   // Kernel B (Phase C, + D on copy) of bucket b on devices [k0, k1).
   int apply(int64_t b, size_t k0, size_t k1) {
+    if (peer) TRY(await_all(r_seq, b));
     for (size_t k = k0; k < k1; ++k) {
       Device &d = c->devs[k];
       HIP_TRY(hipSetDevice(d.hip_id));
-      if (pipelined) {
-        HIP_TRY(hipStreamWaitEvent(d.stream, ev_red(k, b), 0));
-        note_wait(k, 0, ev_red(k, b));
+      // its bucket's collective; the peer-read kernel B reads D from every
+      // shard's owner, so it waits for every device's reduction
+      for (size_t h = peer ? 0 : k; h < (peer ? c->devs.size() : k + 1); ++h) {
+        if (!pipelined && h == k) continue;  // in order on this stream
+        HIP_TRY(hipStreamWaitEvent(d.stream, ev_red(h, b), 0));
+        note_wait(k, 0, ev_red(h, b));
       }
       cbx::LaunchConfig cfg = c->apply_cfg;
       cfg.num_cus = d.num_cus;
@@ -567,7 +625,17 @@ struct SplitStep {
         if (!t.stop) t.stop = o.b1[b];
         o.b1[b] = t.stop;
       }
-      HIP_TRY(cbx::launch_sma_apply(a, mom && !rsag, cfg, d.stream, t));
+      if (peer) {
+        cbx::PeerArgs p;
+        std::memset(&p, 0, sizeof(p));
+        p.G = (int)c->devs.size();
+        p.shard4 = peer_shard4(len_of(b), p.G);
+        for (int h = 0; h < p.G; ++h)
+          p.D[h] = reinterpret_cast<const cbx::v4f *>(base_dev(c, c->devs[h], CBX_BUF_DIFF)) + start_of(b);
+        HIP_TRY(cbx::launch_sma_peer_apply(a, p, mom, cfg, d.stream, t));
+      } else {
+        HIP_TRY(cbx::launch_sma_apply(a, mom && !rsag, cfg, d.stream, t));
+      }
       if (cross && !in_dispatch && !spans) HIP_TRY(hipEventRecord(d.bucket_b[b], d.stream));
       if (spans) tr[k].slot->b_used[b] = t.stop;  // the last B's is the ring's stop event
       note_dispatch(k, 0, Device::SPAN_B, t.stop, nullptr);
@@ -634,8 +702,15 @@ struct SplitStep {
 
   int run() {
     TRY(prepare_common());
-    if (threaded(c)) TRY(for_devices(c, [this](int k) { return run_devices((size_t)k, (size_t)k + 1); }));
-    else TRY(run_devices(0, c->devs.size()));
+    if (threaded(c)) {
+      TRY(for_devices(c, [this](int k) {
+        const int rc = run_devices((size_t)k, (size_t)k + 1);
+        if (rc < 0) failed.store(true, std::memory_order_release);  // releases the others' peer waits
+        return rc;
+      }));
+    } else {
+      TRY(run_devices(0, c->devs.size()));
+    }
     c->last_step_split = true;
     return CBX_OK;
   }
@@ -652,9 +727,8 @@ int sma_step(cbx_context *c, int first) {
   }
 
   if (c->G > 1 ? c->allreduce_algo != CBX_ALLREDUCE_PEER : c->force_split) TRY(ensure_comms(c));
-  if (c->allreduce_algo == CBX_ALLREDUCE_PEER && c->G > 1) {
-    TRY(sma_step_peer(c, args, mom));
-  } else if (c->G == 1 && !c->force_split) {
+  if (c->allreduce_algo == CBX_ALLREDUCE_PEER && c->G > 1) TRY(ensure_peer_access(c));
+  if (c->G == 1 && !c->force_split) {
     // Single GPU: Phase B is the identity, so A + C (+ D) fuse into one pass.
     // (sma.c:63 waits on base->updated; every producer of z is this stream,
     // so stream order already gives that dependency.)
@@ -671,7 +745,16 @@ int sma_step(cbx_context *c, int first) {
     c->last_step_split = false;
   } else {
     SplitStep split(c, args, mom);
-    TRY(split.run());
+    const int rc = split.run();
+    if (rc < 0) {
+      // A step that failed part-way left its per-bucket and span events
+      // half-recorded: the next step must not continue from it.
+      for (Device &d : c->devs) {
+        d.cross_valid = false;
+        d.span_last = -1;
+      }
+      return rc;
+    }
   }
 
   TRY(finish_step(c));

@@ -12,9 +12,10 @@ i % G (the reference's round-robin placement, clib-multigpu/modelmanager.c:51-64
 from __future__ import annotations
 
 import os
-from typing import Callable, Optional, Tuple
+from dataclasses import dataclass, field
+from typing import Callable, Dict, Optional, Tuple
 
-from ._abi import ALLREDUCE_PEER, ALLREDUCE_RCCL, ALLREDUCE_RSAG
+from ._abi import ALLREDUCE_PEER, ALLREDUCE_RCCL, ALLREDUCE_RSAG, CbxError
 
 
 def env_rank() -> Tuple[int, int, int]:
@@ -69,10 +70,26 @@ def max_over_ranks(value: float, world: int) -> float:
     return float(t.item())
 
 
+@dataclass
+class Tuning:
+    """What ``tune_buckets`` chose (already set on the context) and why."""
+    bucket_elements: int
+    buckets: int
+    mode: int
+    stride: int
+    group: int
+    algorithm: int
+    enqueue_threads: Optional[int]          # None: not timed (one local device)
+    table: Dict[str, float] = field(default_factory=dict)   # key -> ms per step (max over ranks)
+    errors: Dict[str, str] = field(default_factory=dict)    # key -> why the candidate was dropped
+
+
 def tune_buckets(gpu, n: int, world: int, step: Callable[[], None], candidates=(1, 2, 4, 8),
                  steps: int = 10, warmup: int = 2, modes=(0, 1), strides=(1, 2, 4), passes: int = 2,
                  group_candidates=(2, 4), progress: Optional[Callable[[str], None]] = None,
-                 ndev: Optional[int] = None, peer: bool = False):
+                 ndev: Optional[int] = None, peer: bool = False, peer_only: bool = False,
+                 peer_candidates=(1, 4, 8), threads: bool = False,
+                 phase: Optional[Callable[[str], None]] = None) -> Tuning:
     """Pick the configuration of the G > 1 pipeline (kernel A / collective /
     kernel B per bucket) by timing each candidate on the live communicator,
     the way a runtime tunes itself in its warm-up.
@@ -95,23 +112,30 @@ def tune_buckets(gpu, n: int, world: int, step: Callable[[], None], candidates=(
     collective's form (``gpu.set_allreduce_algorithm``): one all-reduce, or,
     where G divides 1024, reduce-scatter + base momentum on the rank's shard
     + all-gather, which moves the same link bytes in two collectives per
-    bucket and saves kernel B's momentum pass on (G-1)/G of the model.  Then
-    the all-reduce grouping of the winner (``gpu.set_allreduce_group``, 4-9 %
-    in mode 0, profiles/r01/allreduce_group_ab.json).  The group and the
-    form are reset first, so an earlier setting never skews the sweep.
-    Candidates are timed in ``passes`` interleaved passes and each keeps its
-    best pass, so one noisy sample (a few percent on one GPU) does not decide.
+    bucket and saves kernel B's momentum pass on (G-1)/G of the model; with
+    one process over every device (``peer``) also the peer-read form at
+    ``peer_candidates`` buckets (``peer_only``: that form alone, e.g. when
+    RCCL refuses the device selection).  Then the all-reduce grouping of the
+    winner (``gpu.set_allreduce_group``, 4-9 % in mode 0,
+    profiles/r01/allreduce_group_ab.json) and, with ``threads`` (one process
+    over several devices), the winner with one enqueue thread per device
+    against the reference's one thread (``gpu.set_enqueue_threads``).  The
+    group, the form and the threads are reset first, so an earlier setting
+    never skews the sweep.  Candidates are timed in ``passes`` interleaved
+    passes and each keeps its best pass, so one noisy sample (a few percent
+    on one GPU) does not decide.
 
-    ``progress`` (if given) receives one line per timed candidate.
-    ``ndev`` is the number of GPUs (default ``world``: one process per GPU);
-    with one process over every GPU (``peer``), the peer-read form
-    (``ALLREDUCE_PEER``: no RCCL pass, no buckets) is timed as one more
-    candidate, key "peer".
+    A candidate whose step fails (``CbxError``: e.g. a collective form the
+    communicator refuses) is dropped on every rank (the failure is
+    max-reduced, so all ranks keep the same candidates) and recorded in
+    ``Tuning.errors``; the sweep goes on.  ``phase(name)`` (if given) is
+    called before each candidate, ``progress`` receives one line per timed
+    candidate.  ``ndev`` is the number of GPUs (default ``world``: one
+    process per GPU).
 
-    Returns (bucket_elements, mode, stride, group, algorithm, {key: ms_per_step})
-    with keys "<buckets>/<mode>" for stride 1, "<buckets>/<mode>/s<stride>",
-    the same with "/rsag" for the reduce-scatter form, and "<key of the
-    winner>/g<group>".
+    Keys: "<buckets>/<mode>" for stride 1, "<buckets>/<mode>/s<stride>", the
+    same + "/rsag" or "/peer" for the other forms, "<key of the winner>/g<group>"
+    and "<key of the final choice>/t1" (threaded enqueue).
     """
     import time
 
@@ -120,46 +144,82 @@ def tune_buckets(gpu, n: int, world: int, step: Callable[[], None], candidates=(
             return [(0, 1)]
         return [(m, s) for m in modes for s in ((1,) if m == 0 else strides) if s == 1 or s < nb]
 
-    def timed_steps():
-        for _ in range(warmup):
-            step()
-        gpu.wait()
+    errors: Dict[str, str] = {}
+
+    def failed_anywhere(key: str, why: Optional[str]) -> bool:
+        """Agree over ranks whether this candidate failed (every rank then
+        drops it, and every rank reaches the same collectives next)."""
+        if max_over_ranks(0.0 if why is None else 1.0, world) == 0.0:
+            return False
+        errors[key] = why or "failed on another rank"
+        if progress:
+            progress(f"tune {key}: dropped ({errors[key]})")
+        return True
+
+    def run_steps(k: int) -> Optional[str]:
+        try:
+            for _ in range(k):
+                step()
+            gpu.wait()
+            return None
+        except CbxError as e:
+            try:
+                gpu.wait()
+            except CbxError:
+                pass
+            return str(e)
+
+    def attempt(key: str) -> Optional[float]:
+        """ms per step of the current setting (max over ranks), or None: the
+        candidate failed on some rank and is dropped on every rank."""
+        if phase:
+            phase(f"tune {key}")
+        if failed_anywhere(key, run_steps(warmup)):
+            return None
         barrier(world)
         t0 = time.perf_counter()
-        for _ in range(steps):
-            step()
-        gpu.wait()
-        return max_over_ranks((time.perf_counter() - t0) * 1e3 / steps, world)
+        why = run_steps(steps)
+        el = (time.perf_counter() - t0) * 1e3 / steps
+        if failed_anywhere(key, why):
+            return None
+        ms = max_over_ranks(el, world)
+        if progress:
+            progress(f"tune {key}: {ms:.4f} ms/step")
+        return ms
 
     def elems_of(nb):
         return (1 << 62) if nb <= 1 else max(1, -(-n // nb))
 
     G = world if ndev is None else ndev
-    algos = [ALLREDUCE_RCCL]
-    if 1 < G <= 16 and 1024 % G == 0:
-        algos.append(ALLREDUCE_RSAG)
+    algos = []
+    if not peer_only:
+        algos.append(ALLREDUCE_RCCL)
+        if 1 < G <= 16 and 1024 % G == 0:
+            algos.append(ALLREDUCE_RSAG)
+    if (peer or peer_only) and 1 < G <= 16:
+        algos.append(ALLREDUCE_PEER)
     gpu.set_allreduce_group(1)
+    if threads:
+        gpu.set_enqueue_threads(0)
     results = {}
     for _ in range(max(1, passes)):
-        if peer and 1 < G <= 16:
-            gpu.set_allreduce_algorithm(ALLREDUCE_PEER)
-            ms = timed_steps()
-            key = (1, 0, 1, ALLREDUCE_PEER)
-            results[key] = min(ms, results.get(key, ms))
-            if progress:
-                progress(f"tune {tuning_key(*key)}: {ms:.4f} ms/step")
         for algo in algos:
             gpu.set_allreduce_algorithm(algo)
-            for nb in candidates:
+            for nb in (peer_candidates if algo == ALLREDUCE_PEER else candidates):
                 for mode, stride in combos(nb):
+                    key = (nb, mode, stride, algo)
+                    if tuning_key(*key) in errors:
+                        continue
                     gpu.set_bucket_elements(elems_of(nb))
                     gpu.set_pipeline_mode(mode)
                     gpu.set_cross_wait_stride(stride)
-                    ms = timed_steps()
-                    key = (nb, mode, stride, algo)
+                    ms = attempt(tuning_key(*key))
+                    if ms is None:
+                        results.pop(key, None)
+                        continue
                     results[key] = min(ms, results.get(key, ms))
-                    if progress:
-                        progress(f"tune {tuning_key(*key)}: {ms:.4f} ms/step")
+    if not results:
+        raise CbxError(-1, f"every tuning candidate failed: {errors}")
     best = min(results, key=lambda k: (results[k], k))
     nb, mode, stride, algorithm = best
     gpu.set_allreduce_algorithm(algorithm)
@@ -171,28 +231,52 @@ def tune_buckets(gpu, n: int, world: int, step: Callable[[], None], candidates=(
     # later collective starts.  Over xGMI the later start may cost more than
     # the waits save, so it is timed, not assumed.
     group = 1
-    groups = [grp for grp in group_candidates if 1 < grp < nb and algorithm != ALLREDUCE_PEER]
+    groups = [grp for grp in group_candidates if 1 < grp < nb]
+    best_ms = results[best]
     if groups:
-        timed = {1: results[best]}
+        timed = {1: best_ms}
         for _ in range(max(1, passes)):
             for grp in groups:
+                key = tuning_key(*best) + f"/g{grp}"
+                if key in errors:
+                    continue
                 gpu.set_allreduce_group(grp)
-                ms = timed_steps()
+                ms = attempt(key)
+                if ms is None:
+                    timed.pop(grp, None)
+                    continue
                 timed[grp] = min(ms, timed.get(grp, ms))
-                if progress:
-                    progress(f"tune {tuning_key(*best)}/g{grp}: {ms:.4f} ms/step")
         for grp in groups:
-            out[tuning_key(*best) + f"/g{grp}"] = timed[grp]
+            if grp in timed:
+                out[tuning_key(*best) + f"/g{grp}"] = timed[grp]
         group = min(timed, key=lambda g: (timed[g], g))
+        best_ms = timed[group]
     gpu.set_allreduce_group(group)
-    return elems_of(nb), mode, stride, group, algorithm, out
+    # Then who enqueues: the reference's one thread over every local device,
+    # or one thread per device (host-bound at 8 devices on one thread,
+    # DESIGN.md section 6; on 8 distinct devices unmeasured until now).
+    enqueue_threads = None
+    if threads:
+        final = tuning_key(*best) + (f"/g{group}" if group > 1 else "")
+        t_ms = None
+        for _ in range(max(1, passes)):
+            if final + "/t1" in errors:
+                break
+            gpu.set_enqueue_threads(1)
+            ms = attempt(final + "/t1")
+            if ms is not None:
+                t_ms = ms if t_ms is None else min(t_ms, ms)
+        if t_ms is not None:
+            out[final + "/t1"] = t_ms
+        enqueue_threads = 1 if t_ms is not None and t_ms < best_ms else 0
+        gpu.set_enqueue_threads(enqueue_threads)
+    return Tuning(bucket_elements=elems_of(nb), buckets=nb, mode=mode, stride=stride, group=group,
+                  algorithm=algorithm, enqueue_threads=enqueue_threads, table=out, errors=errors)
 
 
 def tuning_key(nb: int, mode: int, stride: int = 1, algo: int = ALLREDUCE_RCCL) -> str:
-    if algo == ALLREDUCE_PEER:
-        return "peer"
     key = f"{nb}/{mode}" if stride == 1 else f"{nb}/{mode}/s{stride}"
-    return key + ("/rsag" if algo == ALLREDUCE_RSAG else "")
+    return key + {ALLREDUCE_RSAG: "/rsag", ALLREDUCE_PEER: "/peer"}.get(algo, "")
 
 
 def local_replicas(size: int, world: int, rank: int):

@@ -417,13 +417,13 @@ class TheGPU:
         return check(self._L.cbx_check_order(self._ctx))
 
     def set_enqueue_threads(self, mode: int) -> None:
-        """One process over several devices: 0 = one thread enqueues every device's step (the
-        reference's), 1 = one thread per device, -1 (default) = 1 with two or more devices."""
+        """One process over several devices: 0 and -1 (the default) = one thread enqueues every
+        device's step (the reference's), 1 = one thread per device."""
         check(self._L.cbx_set_enqueue_threads(self._ctx, mode))
 
     def set_allreduce_algorithm(self, algorithm: int) -> None:
-        """ALLREDUCE_RCCL (default), ALLREDUCE_PEER (one process over every device: peer reads over xGMI)
-        or ALLREDUCE_RSAG (reduce-scatter, momentum on the shard, all-gather)."""
+        """ALLREDUCE_RCCL (default), ALLREDUCE_PEER (one process over every device: peer reads over xGMI,
+        bucketed like the all-reduce) or ALLREDUCE_RSAG (reduce-scatter, momentum on the shard, all-gather)."""
         check(self._L.cbx_set_allreduce_algorithm(self._ctx, algorithm))
 
     def set_staging_mode(self, mode: int) -> None:

@@ -389,7 +389,11 @@ int cbx_set_allreduce_group (cbx_context *ctx, int group);
  *     device g sums shard g of every device's acc by direct peer reads, then
  *     kernel B on each device reads every shard of D from its owner
  *     (two-shot over all xGMI links at once; the reference's non-NCCL path
- *     copies peer buffers, common.c:64-95).  Sums in device order: bit-exact
+ *     copies peer buffers, common.c:64-95).  Bucketed and pipelined like
+ *     the all-reduce (bucket size, modes, strides, groups above): the
+ *     reduction of bucket k runs on the all-reduce stream beside kernel A of
+ *     bucket k+1 and waits for kernel A(k) of EVERY device; kernel B(k) waits
+ *     for every device's reduction of k.  Sums in device order: bit-exact
  *     against the rank-order oracle and identical on every device.  The
  *     host-staged step and S-SGD keep RCCL.
  *   CBX_ALLREDUCE_RSAG (2): every process form.  Per bucket, RCCL
@@ -427,10 +431,13 @@ int cbx_set_staging_mode (cbx_context *ctx, int mode);
  *       and collectives (NCCL's thread-per-device use of ncclCommInitAll's
  *       communicators); the call returns once every device's work is
  *       enqueued, as before;
- *  -1   (default) 1 with two or more local devices.
+ *  -1   (default) 0: the reference's form, until measured otherwise on
+ *       distinct devices (bench.py's warm-up tuner times 0 against 1).
  * Same work on the same streams in the same per-device order: results are
- * identical.  At 8 devices and 8 buckets one thread spends longer enqueuing
- * a step than the GPUs spend running it.          */
+ * identical (a threaded peer-read step orders its cross-device waits behind
+ * the other devices' event records).  At 8 devices and 8 buckets one thread
+ * may spend longer enqueuing a step than the GPUs spend running it
+ * (DESIGN.md section 6).                                                   */
 int cbx_set_enqueue_threads (cbx_context *ctx, int mode);
 /* Force the multi-GPU pipeline (kernel A + RCCL all-reduce + kernel B) even
  * at G = 1 (a one-rank communicator), so a single-GPU host exercises it.  */

@@ -202,9 +202,14 @@ class _FakeGpu:
     """Stands in for TheGPU in tune_buckets: a step 'costs' a rank-dependent
     time per bucket count (sleep), so the ranks disagree locally."""
 
-    def __init__(self, rank, n):
+    def __init__(self, rank, n, fail_on=None):
         self.rank, self.n, self.elems, self.mode, self.stride, self.group = rank, n, 0, 0, 1, 1
         self.algo = 0
+        self.threads = -1
+        self.fail_on = fail_on  # (buckets, mode) whose steps raise CbxError on this rank
+
+    def set_enqueue_threads(self, t):
+        self.threads = t
 
     def set_allreduce_algorithm(self, a):
         self.algo = a
@@ -227,6 +232,9 @@ class _FakeGpu:
     def step(self):
         import time
         nb = 1 if self.elems >= self.n else -(-self.n // self.elems)
+        if self.fail_on == (nb, self.mode):
+            from crossbow_amd._abi import CbxError
+            raise CbxError(-5, f"injected failure at {nb} buckets, mode {self.mode}")
         # rank 0 is fastest at 8 buckets, rank 1 at 2; the max over ranks is lowest at 4
         cost = {0: {1: 9, 2: 7, 4: 4, 8: 1}, 1: {1: 9, 2: 1, 4: 4, 8: 7}}[self.rank][nb]
         cost += 2 if (self.mode >= 1 and self.rank == 1) else 0  # cross-step modes slower on rank 1
@@ -247,9 +255,9 @@ def _tune_main(rank, world, port, q):
         g = _FakeGpu(rank, 1000)
         g.group = 3  # a group left over from an earlier setting must not skew the sweep
         g.algo = 2   # nor an algorithm left over: the sweep runs on the all-reduce
-        elems, mode, stride, group, algo, res = D.tune_buckets(g, 1000, world, g.step, steps=2, warmup=1)
-        q.put((rank, (elems, g.elems, mode, g.mode, stride, g.stride, group, g.group, algo, g.algo, sorted(res)),
-               None))
+        t = D.tune_buckets(g, 1000, world, g.step, steps=2, warmup=1)
+        q.put((rank, (t.bucket_elements, g.elems, t.mode, g.mode, t.stride, g.stride, t.group, g.group, t.algorithm,
+                      g.algo, sorted(t.table)), None))
         D.finalize(world)
     except Exception:  # pragma: no cover
         import traceback
@@ -291,3 +299,57 @@ def test_bucket_tuning_agrees_across_ranks():
     want += ["4/0/rsag/g2"]  # groups 1 < g < buckets, timed for the winner only
     assert cands == sorted(want)
     assert a0 == a1 == seta0 == seta1 == 2  # faster on both ranks: chosen
+
+
+def _tune_fail_main(rank, world, port, q):
+    import sys
+    sys.path.insert(0, ROOT)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    try:
+        from crossbow_amd import dist as D
+        D.init(world, rank, backend="gloo")
+        # 4 buckets (the max-over-ranks winner of test_bucket_tuning_agrees_across_ranks)
+        # fail in mode 0 on rank 1 only; one process over 2 "devices" also times the
+        # peer-read form and the threaded enqueue
+        g = _FakeGpu(rank, 1000, fail_on=(4, 0) if rank == 1 else None)
+        t = D.tune_buckets(g, 1000, world, g.step, steps=2, warmup=1, threads=True)
+        q.put((rank, (t.buckets, t.mode, t.algorithm, t.enqueue_threads, g.threads, sorted(t.table), t.errors), None))
+        D.finalize(world)
+    except Exception:  # pragma: no cover
+        import traceback
+        q.put((rank, None, traceback.format_exc()))
+
+
+def test_bucket_tuning_drops_a_failing_candidate_on_every_rank():
+    # A candidate whose step raises CbxError on ONE rank is dropped on every
+    # rank (else the ranks would disagree on the winner and their RCCL call
+    # sequences diverge), recorded in Tuning.errors, and the sweep goes on.
+    import torch.multiprocessing as mp
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_tune_fail_main, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = {}
+    try:
+        for _ in range(world):
+            rank, res, err = q.get(timeout=240)
+            out[rank] = (res, err)
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
+    for rank in range(world):
+        assert out[rank][1] is None, out[rank][1]
+    r0, r1 = out[0][0], out[1][0]
+    assert r0[:6] == r1[:6], (r0, r1)
+    nb, mode, algo, threads, set_threads, table, errors = r0
+    assert "4/0" not in table and "4/0/rsag" not in table, table
+    assert "4/1" in table  # the same bucket count in mode 1 still runs
+    assert sorted(errors) == ["4/0", "4/0/rsag"], errors
+    assert "injected failure" in r1[6]["4/0"] and r0[6]["4/0"] == "failed on another rank"
+    assert threads in (0, 1) and set_threads == threads
+    assert (nb, mode) != (4, 0)

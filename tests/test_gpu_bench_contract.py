@@ -62,11 +62,20 @@ def test_bench_two_ranks_through_the_launcher_prints_one_json_line():
     assert 0 < r["apply_kernel"]["frac"] < 1 and 0 < r["a_plus_b"]["frac"] < 1
     assert r["collective_busy_ms_mean"] > 0
     assert d["roofline_unpipelined"]["timed_in"].startswith("calibration")
-    # RCCL's own tuning choices, parsed from its TUNING log
-    t = d["allreduce"]["rccl_tuning"]
-    assert isinstance(t, list) and t, d["allreduce"]
+    # the link rate of the collectives as they ran in the timed region, the
+    # calibration's (the collective alone) apart
+    ar = d["allreduce"]
+    assert ar["timed"]["busbw_GBs"] > 0 and ar["timed"]["xgmi_frac"] > 0, ar
+    assert ar["timed"]["timed_in"].startswith("timed region")
+    assert ar["unpipelined"]["busbw_GBs"] > 0 and ar["unpipelined"]["timed_in"].startswith("calibration")
+    # RCCL's own tuning choices, parsed from its TUNING log of a separate short
+    # run (the measured run keeps RCCL's per-collective log off)
+    t = ar["rccl_tuning"]
+    assert isinstance(t, list) and t, ar
     assert all(e["collective"] and e["algo"] and e["proto"] and e["bytes"] > 0 and e["calls"] > 0 for e in t)
+    assert "separate" in ar["rccl_tuning_source"]
     assert d["host"]["enqueue_ms_per_step_timed"] > 0 and d["host"]["devices_per_process"] == 1
+    assert d["config"]["hw_queues"]["GPU_MAX_HW_QUEUES"] >= 1
 
 
 @pytest.mark.timeout(300)
@@ -79,10 +88,37 @@ def test_bench_single_process_two_devices_one_gpu():
     assert p.returncode == 0, p.stderr[-2000:]
     d = _one_line(p.stdout)
     _check(d, 2)
-    assert d["config"]["process_form"] == "single" and d["config"]["allreduce_algorithm"] == "peer-read two-shot"
+    c = d["config"]
+    assert c["process_form"] == "single" and c["allreduce_algorithm"] == "peer-read two-shot"
     assert d["host"]["devices_per_process"] == 2 and d["host"]["enqueue_ms_per_step_idle_gpu"] > 0
     assert d["roofline"]["timed_in"].startswith("timed region") and "roofline_unpipelined" in d
     assert "rehearsal" in d
+    # the tuner timed the peer-read form at 1 / 4 / 8 buckets and, for the
+    # winner, one enqueue thread per device against the reference's one
+    table = c["bucket_tuning_ms_per_step"]
+    assert {"1/0/peer", "4/0/peer", "4/1/peer", "8/1/peer"} <= set(table), table
+    assert any(k.endswith("/t1") for k in table), table
+    assert c["enqueue_threads"] in (0, 1) and c["buckets"] in (1, 4, 8)
+    assert not c["tuning_errors"], c["tuning_errors"]
+    assert d["allreduce"]["rccl_tuning"] is None and d["allreduce"]["timed"]["busbw_GBs"] > 0
+
+
+@pytest.mark.timeout(300)
+def test_bench_tuner_drops_a_failing_candidate():
+    """A tuner candidate whose steps fail ($CBX_FAULT_FAIL_STEP_BUCKETS: every
+    split step over exactly 4 buckets returns an error before it enqueues
+    anything) is dropped and recorded; the run goes on and picks another."""
+    env = dict(os.environ, CBX_FAULT_FAIL_STEP_BUCKETS="4")
+    cmd = [sys.executable, "bench.py", "--force-split"] + QUICK
+    p = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=280, env=env)
+    assert p.returncode == 0, p.stderr[-2000:]
+    d = _one_line(p.stdout)
+    _check(d, 1)
+    c = d["config"]
+    assert sorted(c["tuning_errors"]) == ["4/0", "4/1", "4/1/s2"], c["tuning_errors"]
+    assert all("fault injection" in v for v in c["tuning_errors"].values())
+    assert not any(k.startswith("4/") for k in c["bucket_tuning_ms_per_step"])
+    assert c["buckets"] != 4 and "1/0" in c["bucket_tuning_ms_per_step"]
 
 
 @pytest.mark.timeout(300)

@@ -17,7 +17,9 @@ same G and against the committed golden fixtures; ring-order loopback: the
 G > 1 tolerance plus z / last bitwise identical on every device.
 
 The peer-read all-reduce (cbx_set_allreduce_algorithm PEER: two-shot over
-direct peer reads, no RCCL pass) runs only in this form; its cases, and the
+direct peer reads, no RCCL pass, bucketed and pipelined like the all-reduce)
+runs only in this form; its cases (1 to 25 buckets, both pipeline modes,
+groups, wait strides), and the
 golden fixtures run through it, are bit for bit against the oracle (device
 order from +0 is the oracle's order).  On one GPU every "peer" is device 0
 itself, so this pins the algorithm, not its xGMI speed.
@@ -61,6 +63,14 @@ CASES = [
     Case("sma-peer-no-momentum", 20_011, 1, 0.0, 2, utype=3, algo=1),
     Case("sma-peer-empty-shards", 1031, 2, 0.9, 3, copy={2: 0}, algo=1),  # n4 = one pad: trailing shards empty
     Case("sma-peer-big", 300_007, 3, 0.9, 2, algo=1),
+    # the peer-read form bucketed and pipelined like the all-reduce (the cases
+    # above run the library default, 8 buckets): one bucket in order, groups,
+    # the cross-step pipeline with a wait stride, many small buckets
+    Case("sma-peer-one-bucket", 300_007, 2, 0.9, 3, bucket=1 << 40, copy={1: 0}, held={2: 1}, algo=1),
+    Case("sma-peer-buckets-group", 300_007, 3, 0.9, 3, bucket=65_536, group=3, copy={1: 2}, algo=1),
+    Case("sma-peer-buckets-cross", 300_007, 2, 0.9, 5, bucket=65_536, copy={2: 1}, held={3: 0}, mode=1, stride=2,
+         group=2, algo=1),
+    Case("sma-peer-many-buckets", 100_003, 2, 0.0, 3, bucket=4096, utype=3, mode=1, copy={1: 1}, algo=1),
     # switching between the algorithms, and from the cross-step pipeline, between steps
     Case("sma-peer-switch", 300_007, 2, 0.9, 5, bucket=65_536, mode=1, copy={3: 1}, algo_at={1: 1, 2: 0, 4: 1}),
     # the reduce-scatter form (RSAG: reduce-scatter, momentum on the shard, all-gather)
@@ -75,12 +85,14 @@ CASES = [
 
 def _jobs(G):
     if G == 3:  # a non-power-of-two clique: the plain step in both orders, and the peer path (RSAG is refused)
-        names = ("sma", "sma-ring", "sma-peer", "sma-peer-empty-shards")
+        names = ("sma", "sma-ring", "sma-peer", "sma-peer-empty-shards", "sma-peer-buckets-cross")
     elif G == 16:  # the most devices one process takes (kMaxDevices): plain, ring order, peer, reduce-scatter
-        names = ("sma-copy-ssp", "sma-ring", "sma-peer", "sma-peer-empty-shards", "sma-rsag", "sma-rsag-ring")
+        names = ("sma-copy-ssp", "sma-ring", "sma-peer", "sma-peer-empty-shards", "sma-peer-buckets-cross", "sma-rsag",
+                 "sma-rsag-ring")
     elif G == 8:
         names = ("sma-copy-ssp", "sma-buckets-cross", "ssgd-buckets", "sma-ring", "sma-ring-buckets-cross",
-                 "sma-peer", "sma-peer-empty-shards", "sma-peer-switch", "sma-rsag", "sma-rsag-buckets-cross",
+                 "sma-peer", "sma-peer-empty-shards", "sma-peer-switch", "sma-peer-one-bucket", "sma-peer-buckets-cross",
+                 "sma-peer-many-buckets", "sma-rsag", "sma-rsag-buckets-cross",
                  "sma-rsag-ring", "sma-rsag-switch")
     else:
         names = [c.name for c in CASES]
@@ -124,12 +136,13 @@ def _worker(G, jobs, ckdir, q, threads=-1):
 
 
 @pytest.mark.skipif(not os.path.exists(C.VARIANT), reason="run scripts/build_fake_rccl.sh first")
-@pytest.mark.parametrize("G,threads", [(2, -1), (3, -1), (4, -1), (8, -1), (16, -1), (2, 0), (8, 0)])
+@pytest.mark.parametrize("G,threads", [(2, 1), (3, 1), (4, 1), (8, 1), (16, 1), (2, 0), (4, -1), (8, 0)])
 def test_one_process_many_devices_vs_oracle(G, threads):
-    """threads -1 (the default): one enqueue thread per device, each issuing
-    its own communicator's collectives (the loopback meets them at a
-    rendezvous); 0: the reference's single thread, collectives grouped
-    across the devices."""
+    """threads 1: one enqueue thread per device, each issuing its own
+    communicator's collectives (the loopback meets them at a rendezvous) and,
+    in the peer-read form, waiting on the other devices' events only once
+    their threads recorded them; 0 and -1 (the default): the reference's
+    single thread, collectives grouped across the devices."""
     import multiprocessing as mp
     jobs = _jobs(G)
     ctx = mp.get_context("spawn")

@@ -819,6 +819,45 @@ def test_cross_step_pipeline(momentum, bucket, stride, group, algo):
     # Phase D requests, SSP holds, a host write between two steps (which
     # must make the next step join the whole sync stream) and a switch to the
     # in-step mode and back; bit-exact with the oracle throughout.
+    _cross_step_run(momentum, bucket, stride, group, algo)
+
+
+def _cross_step_child(hw_queues, q):
+    # a fresh process: ROCclr reads GPU_MAX_HW_QUEUES once, at HIP's start
+    os.environ["GPU_MAX_HW_QUEUES"] = hw_queues
+    try:
+        _cross_step_run(0.9, 65_536, 2, 2, 0)
+        _cross_step_run(0.9, 16_384, 1, 1, 2)
+        q.put(None)
+    except BaseException:  # pragma: no cover - reported to the parent
+        import traceback
+        q.put(traceback.format_exc())
+
+
+@pytest.mark.timeout(240)
+def test_cross_step_pipeline_live_at_hip_default_hw_queues():
+    # The library's four streams per device share ROCclr's hardware queues
+    # when GPU_MAX_HW_QUEUES is HIP's default 4 (with RCCL's and torch's
+    # streams beside them), so a stream wait can hold back another stream's
+    # work queued behind it: slower, but it must stay
+    # live and bit-exact.  The cross-step pipeline with two A streams, wait
+    # stride 2 and all-reduce groups of 2, and 19 buckets in the reduce-scatter
+    # form, in a process started with GPU_MAX_HW_QUEUES=4.
+    import multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_cross_step_child, args=("4", q))
+    p.start()
+    try:
+        err = q.get(timeout=200)
+    finally:
+        p.join(timeout=30)
+        if p.is_alive():
+            p.kill()
+    assert err is None, err
+
+
+def _cross_step_run(momentum, bucket, stride, group, algo):
     from crossbow_amd import BUF_DATA
     n, R = 300_001, 3
     st = O.make_state(n, 1, R, 0.1, momentum)
@@ -832,10 +871,15 @@ def test_cross_step_pipeline(momentum, bucket, stride, group, algo):
         g.set_allreduce_algorithm(algo)
         upload(g, st)
         want = st.clone()
+        # "timing": cbx_set_timing calls before the step (timing on restarts
+        # the span records a continuing step starts from: the step joins)
         plan = [{}, {"copy": 1}, {"hold": 2}, {}, {"write": 0}, {"mode": 0}, {"mode": 1, "copy": 2, "hold": 0},
-                {"mode": 0}, {"mode": 1}]
+                {"mode": 0}, {"mode": 1}, {"timing": [True]}, {}, {"timing": [True]}, {"timing": [False, True]},
+                {"copy": 0}, {"timing": [False]}, {}]
         for step, p in enumerate(plan):
             want.locked[:] = 1
+            for on in p.get("timing", []):
+                g.set_timing(on)
             if "mode" in p:
                 g.set_pipeline_mode(p["mode"])
             if "write" in p:
@@ -976,6 +1020,50 @@ def test_stream_order_check_detects_a_race(monkeypatch):
         with pytest.raises(CbxError, match="the collective started before kernel A ended"):
             g.check_order()
         g.wait()
+    finally:
+        g.free()
+
+
+@pytest.mark.parametrize("fault", [True, False])
+def test_two_a_stream_group_wait_race_is_caught(monkeypatch, fault):
+    # Pins round 3's fix (the comm stream waits for the last kernel A on EACH
+    # of the two A streams of a cross-step all-reduce group).
+    # $CBX_FAULT_ONE_STREAM_COMM_WAIT restores the earlier wait (the group's
+    # last kernel A only) and holds back, by 0.5 ms, every kernel A that wait
+    # skips: with groups of 2 the even buckets' A on the first A stream, so
+    # the group's collective certainly reads acc before it is written.  The
+    # order check must name the race; without the switch the same pipeline
+    # passes the check and stays bit-exact.
+    from crossbow_amd import CbxError
+    n, R = 300_001, 3
+    st = O.make_state(n, 1, R, 0.1, 0.9)
+    if fault:
+        monkeypatch.setenv("CBX_FAULT_ONE_STREAM_COMM_WAIT", "1")
+    g = make_gpu(n, R, 0.1, 0.9)
+    monkeypatch.delenv("CBX_FAULT_ONE_STREAM_COMM_WAIT", raising=False)
+    try:
+        g.set_force_split(True)
+        g.set_bucket_elements(65_536)  # 5 buckets
+        g.set_pipeline_mode(1)
+        g.set_cross_wait_stride(1)
+        g.set_allreduce_group(2)
+        g.set_order_check(True)
+        upload(g, st)
+        want = st.clone()
+        for step in range(2):
+            want.locked[:] = 1
+            g.lockAny()
+            g.synchronise(0, step + 1, 0, False)
+            g.unlockAny()
+            O.sma_step(want)
+        if fault:
+            with pytest.raises(CbxError, match="the collective started before kernel A ended"):
+                g.check_order()
+            g.wait()
+        else:
+            assert g.check_order() == 2
+            g.wait()
+            compare_states(download(g, st), want)
     finally:
         g.free()
 

@@ -229,6 +229,12 @@ def _rank_main(rank, world, jobs, d, q):
         q.put((rank, None, traceback.format_exc()))
 
 
+def _rank_main_hw_queues(rank, world, jobs, d, hw_queues, q):
+    # a fresh process: ROCclr reads GPU_MAX_HW_QUEUES once, at HIP's start
+    os.environ["GPU_MAX_HW_QUEUES"] = hw_queues
+    _rank_main(rank, world, jobs, d, q)
+
+
 def _spawn(world, target, args_of_rank, timeout):
     from tests.test_gpu_multirank import _spawn as spawn
     return spawn(world, target, args_of_rank, timeout)
@@ -255,6 +261,25 @@ def test_real_rccl_ranks_on_one_gpu_vs_oracle(world):
     if world >= 3:
         # the tolerance path was really taken: RCCL summed outside the oracle's order
         assert differs > 0, "RCCL's sums never left the oracle's order"
+
+
+@pytest.mark.timeout(300)
+def test_real_rccl_random_run_live_at_hip_default_hw_queues():
+    # The 4-rank randomised run (bucket sizes, pipeline modes, wait strides,
+    # all-reduce groups and collective forms switched between steps, Phase D,
+    # SSP holds, host writes, the stream order checked every two steps) with
+    # GPU_MAX_HW_QUEUES=4, HIP's default: the library's four streams per
+    # device then share hardware queues with RCCL's and each other, so a
+    # stream wait can hold back work queued behind it.  Slower, but it must
+    # stay live and correct.
+    world, jobs = 4, [("random", "random-long-run")]
+    with tempfile.TemporaryDirectory(dir=C.loopback_dir()) as d:
+        res = _spawn(world, _rank_main_hw_queues, lambda r: (r, world, jobs, d, "4"), timeout=280)
+    for rank in range(world):
+        (name, r), = res[rank]
+        assert name == "random-long-run" and not r["bad"], f"rank {rank}: {r['bad']}"
+    assert len({res[r][0][1]["digest"][r] for r in range(world)}) == 1, "z / last differ across ranks"
+    assert sum(res[r][0][1]["differs"] for r in range(world)) > 0, "RCCL's sums never left the oracle's order"
 
 
 def _full_size_main(rank, world, R, steps, mode, algo, d, q):
