@@ -39,6 +39,8 @@ def main():
                 print(json.dumps({"round": r, "hw_queues": int(q), "error": p.stderr[-1500:]}), flush=True)
                 raise SystemExit(p.returncode)
             for line in p.stdout.splitlines():
+                if not line.startswith("{"):  # native libraries' banners (RCCL's version line)
+                    continue
                 d = json.loads(line)
                 d.update(round=r, hw_queues=int(q))
                 print(json.dumps(d), flush=True)
