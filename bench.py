@@ -42,9 +42,11 @@ import tempfile
 import threading
 import time
 
-# Before the HIP runtime starts (it reads this once): the bucket pipeline
-# needs a hardware queue per library stream (crossbow_amd/_lib.py, DESIGN.md
-# section 5); an explicit setting by the caller wins and is reported.
+# Before the HIP runtime starts (it reads this once): ROCclr's hardware
+# queues per device.  16 gives each of the pipeline's streams a queue of its
+# own, the recommended deployment setting (HIP's default 4
+# measured within 3 % on one GPU); an explicit setting by the caller wins.
+# Reported in config.hw_queues either way.
 HW_QUEUES_SET_BY = "caller" if "GPU_MAX_HW_QUEUES" in os.environ else "bench.py default"
 os.environ.setdefault("GPU_MAX_HW_QUEUES", "16")
 
@@ -901,6 +903,9 @@ def main():
             entries, source = None, "no RCCL collective in the chosen form"
         elif args.no_rccl_tuning_run:
             entries, source = None, "--no-rccl-tuning-run"
+        elif args.rehearse_one_gpu and not single and 2 * G + 2 > 16:
+            # the separate run's ranks would join this run's on the one GPU
+            entries, source = None, f"not run: a {G}-rank rehearsal plus {G} more ranks exceeds 16 processes on one GPU"
         elif rank == 0:
             entries, source = rccl_tuning_run(args, G, single, chosen, wd)
         else:

@@ -13,13 +13,6 @@ from __future__ import annotations
 import ctypes
 import os
 
-# Before the HIP runtime starts (it reads this once): every stream of the
-# process shares GPU_MAX_HW_QUEUES hardware queues per device (default 4); a
-# device's four library streams plus RCCL's and torch's need more, or a
-# stream wait on a shared queue holds back other streams' work behind it
-# (csrc/context.hip, cbx_default_hw_queues).  An explicit setting wins.
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "16")
-
 import torch  # noqa: F401,E402  (see module docstring: one HIP runtime per process)
 
 from ._abi import *  # noqa: F401,F403  (status codes, constants, CbxError)

@@ -81,17 +81,14 @@ int load_buffer(float *dev, size_t bytes, const std::string &path, std::vector<c
 
 
 // Hardware queues.  ROCclr maps a process's streams onto GPU_MAX_HW_QUEUES
-// hardware queues per device (default 4), shared once that many exist.  A
-// device here has four streams of its own (sync, comm, two for kernels A)
-// and RCCL and the host application add theirs; a stream wait queued on a
-// shared queue holds back everything behind it on that queue, whichever
-// stream it belongs to: the bucket pipeline then ran 20-80 % slower on
-// some contexts, by creation order (profiles/r03/pipeline_streams_ab.json),
-// and RCCL's internal work could wait behind one of our waits.  So when the
-// library is loaded before the HIP runtime starts (a JVM loading the JNI
-// shim), 16 queues become the default; an explicit setting wins.  The
-// Python package sets the same default at import (crossbow_amd/_lib.py).
-__attribute__((constructor)) static void cbx_default_hw_queues() { setenv("GPU_MAX_HW_QUEUES", "16", 0); }
+// hardware queues per device (default 4), shared once that many exist; a
+// stream wait queued on a shared queue holds back everything behind it.  A
+// device here has four streams of its own (sync, comm, two for kernels A),
+// created together in open_device so they take the first queues.  At HIP's
+// default 4 the bucket pipeline measured within 3 % of 16 queues on one GPU
+// (profiles/r04/hw_queues_ab.jsonl), so the library leaves the
+// setting to the deployment (16 recommended) and never
+// changes the process environment itself.
 
 // ===========================================================================
 // C-ABI

@@ -703,10 +703,11 @@ inline int probe_device(int hip_id, int *num_cus) {
 // creation order (profiles/r03/pipeline_streams_ab.json).  So a device's four
 // streams (sync, comm, and the two of kernels A) are created together in
 // open_device, before RCCL creates its own, and take the pool's first
-// queues, and GPU_MAX_HW_QUEUES defaults to 16 (context.hip), so each keeps
-// a queue of its own.  (CU-mask streams get queues of their own too, but
-// they synchronise with the null stream; the reference's sync stream is
-// non-blocking.)
+// queues: at HIP's default 4 queues the pipeline then measured within 3 % of
+// 16 (profiles/r04/hw_queues_ab.jsonl); 16 is the recommended deployment
+// setting, which the library does not impose.  (CU-mask
+// streams get queues of their own too, but they synchronise with the null
+// stream; the reference's sync stream is non-blocking.)
 inline int create_stream(hipStream_t *s) {
   HIP_TRY(hipStreamCreateWithFlags(s, hipStreamNonBlocking));
   return CBX_OK;
