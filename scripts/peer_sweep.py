@@ -34,20 +34,35 @@ def main():
     ap.add_argument("--warmup", type=int, default=4)
     ap.add_argument("--timing", type=int, default=1)
     ap.add_argument("--gap-ms", type=float, default=0.0, help="host sleep between configurations (trace splitting)")
+    ap.add_argument("--variants", default="default",
+                    help="comma-separated contexts: 'default', or an experiment toggle set at the context's creation "
+                         "('norelay': CBX_EXP_PEER_NO_RELAY)")
     a = ap.parse_args()
     from crossbow_amd import SYNC_BSP, UPDATE_SMA, TheGPU, _lib
     from crossbow_amd.variables import MODELS, register
-    g = TheGPU()
-    g.init(list(range(a.G)) if a.distinct else [0] * a.G)
-    n = register(g, MODELS["resnet50"]())
-    g.setUpdateModelType(UPDATE_SMA)
-    g.setEamsgdAlpha(0.1)
-    g.setMomentum(0.9, 0)
-    g.setModelManager(8, SYNC_BSP)
-    g.set_allreduce_algorithm(_lib.ALLREDUCE_PEER)
-    g.fill_synthetic(1)
-    g.set_timing(bool(a.timing))
+    toggles = {"default": None, "norelay": "CBX_EXP_PEER_NO_RELAY"}
+
+    def make(variant):
+        env = toggles[variant]
+        if env:
+            os.environ[env] = "1"
+        g = TheGPU()
+        g.init(list(range(a.G)) if a.distinct else [0] * a.G)
+        if env:
+            del os.environ[env]
+        n = register(g, MODELS["resnet50"]())
+        g.setUpdateModelType(UPDATE_SMA)
+        g.setEamsgdAlpha(0.1)
+        g.setMomentum(0.9, 0)
+        g.setModelManager(8, SYNC_BSP)
+        g.set_allreduce_algorithm(_lib.ALLREDUCE_PEER)
+        g.fill_synthetic(1)
+        g.set_timing(bool(a.timing))
+        return g, n
+
+    ctxs = {v: make(v) for v in a.variants.split(",")}
     clock = [0]
+    g = None
 
     def step():
         clock[0] += 1
@@ -61,7 +76,8 @@ def main():
     order = []
     for _ in range(a.passes):
         for nb, mode, stride, group in configs:
-            for t in threads:
+            for t, variant in [(t, v) for t in threads for v in ctxs]:
+                g, n = ctxs[variant]
                 g.set_enqueue_threads(t)
                 g.set_bucket_elements((1 << 62) if nb == 1 else -(-n // nb))
                 g.set_pipeline_mode(mode)
@@ -75,17 +91,18 @@ def main():
                     step()
                 g.wait()
                 ms = (time.perf_counter() - t0) * 1e3 / a.steps
-                key = (nb, mode, stride, group, t)
+                key = (nb, mode, stride, group, t, variant)
                 best[key] = min(ms, best.get(key, ms))
                 order.append(key)
                 if a.gap_ms > 0:
                     time.sleep(a.gap_ms / 1e3)
-    for (nb, mode, stride, group, t), ms in sorted(best.items()):
+    for (nb, mode, stride, group, t, variant), ms in sorted(best.items()):
         print(json.dumps({"G": a.G, "distinct": a.distinct, "buckets": nb, "mode": mode, "stride": stride,
-                          "group": group, "enqueue_threads": t, "timing": a.timing, "steps": a.steps,
+                          "group": group, "enqueue_threads": t, "variant": variant, "timing": a.timing, "steps": a.steps,
                           "warmup": a.warmup, "ms_per_step": round(ms, 4)}), flush=True)
     print(json.dumps({"order": [list(k) for k in order], "steps": a.steps, "warmup": a.warmup}), flush=True)
-    g.free()
+    for g, _ in ctxs.values():
+        g.free()
 
 
 if __name__ == "__main__":

@@ -58,7 +58,7 @@ def main():
             d = [e[1] - e[0] for e in timed if e[2] == k]
             kinds[k] = {"sum_us_per_step": round(sum(d) / 1e3 / steps, 1), "launches_per_step": len(d) // steps,
                         "median_us": round(statistics.median(d) / 1e3, 1) if d else None}
-        print(json.dumps({"config": dict(zip(("buckets", "mode", "stride", "group", "threads"), key)),
+        print(json.dumps({"config": dict(zip(("buckets", "mode", "stride", "group", "threads", "variant"), key)),
                           "wall_us_per_step": round(wall, 1), "busy_us_per_step": round(busy, 1),
                           "idle_us_per_step": round(wall - busy, 1), "kernels": kinds}), flush=True)
 
