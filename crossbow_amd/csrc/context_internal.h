@@ -325,10 +325,6 @@ struct Device {
   std::vector<hipEvent_t> stage_k;        // per bucket: outputs computed
   std::vector<hipEvent_t> bucket_acc;  // per bucket: kernel A done (stream -> comm_stream)
   std::vector<hipEvent_t> bucket_red;  // per bucket: all-reduce done (comm_stream -> stream)
-  // Peer-read form: per bucket, every device's reduction of it done (the comm
-  // stream waits for the other devices' and records this; kernel B waits on
-  // this one event instead of one per device).
-  std::vector<hipEvent_t> bucket_all;
   // Cross-step pipeline (cbx_set_pipeline_mode 1): kernels A run on a_stream,
   // kernels B stay on `stream`; bucket_b[k] marks B(k) done, which A(k) of
   // the next step waits for instead of the whole previous step.
@@ -509,10 +505,6 @@ struct cbx_context {
   // one on the other A stream; a one-wave delay ahead of every kernel A that
   // wait skips makes the race certain (tests only: results are then wrong).
   bool fault_one_stream_comm_wait = std::getenv("CBX_FAULT_ONE_STREAM_COMM_WAIT") != nullptr;
-  // Experiment toggle (scripts/peer_sweep.py --variants): $CBX_EXP_PEER_NO_RELAY
-  // at context creation makes kernel B of the bucketed peer-read form wait on
-  // every device's reduction itself instead of the comm stream's relay event.
-  bool exp_peer_no_relay = std::getenv("CBX_EXP_PEER_NO_RELAY") != nullptr;
   // $CBX_FAULT_FAIL_STEP_BUCKETS=N: a split SMA step over exactly N buckets
   // fails before it enqueues anything (the bench tuner's error path, tests only).
   int64_t fault_fail_buckets = std::getenv("CBX_FAULT_FAIL_STEP_BUCKETS")
@@ -761,7 +753,6 @@ inline void close_device(Device &d) {
   }
   for (hipEvent_t e : d.bucket_acc) (void)hipEventDestroy(e);
   for (hipEvent_t e : d.bucket_red) (void)hipEventDestroy(e);
-  for (hipEvent_t e : d.bucket_all) (void)hipEventDestroy(e);
   if (d.a_stream) (void)hipStreamSynchronize(d.a_stream);
   if (d.a_stream2) (void)hipStreamSynchronize(d.a_stream2);
   for (hipEvent_t e : d.bucket_b) (void)hipEventDestroy(e);

@@ -219,10 +219,6 @@ struct SplitStep {
     return spans ? tr[k].slot->red[b] : c->devs[k].bucket_red[b];
   }
 
-  // Peer-read, pipelined in mode 0: kernel B waits on its comm stream's relay
-  // of every device's reduction (collective), not on each device's.
-  bool relay() const { return peer && pipelined && !cross && !c->exp_peer_no_relay; }
-
   // Peer-read, threaded: publish that device k's event of bucket b is
   // recorded / wait until every device's is.
   void publish(std::unique_ptr<std::atomic<int64_t>[]> &seq, size_t k, int64_t b) {
@@ -359,11 +355,6 @@ struct SplitStep {
           d.bucket_acc.push_back(ea);
           d.bucket_red.push_back(er);
           d.bucket_b.push_back(eb);
-        }
-        while (peer && (int64_t)d.bucket_all.size() < nb) {
-          hipEvent_t e;
-          HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-          d.bucket_all.push_back(e);
         }
       }
       if (cross) {
@@ -596,49 +587,23 @@ struct SplitStep {
       }
     }
     for (size_t k = k0; k < k1; ++k) publish(r_seq, k, b);
-    if (relay()) {
-      // Relay (mode 0): the comm stream, which has little else to do, waits
-      // for the other devices' reductions of the bucket and marks "every
-      // shard of D(b) is reduced", so the sync stream, which also carries the
-      // next kernels A, pays one wait per bucket, not one per device (a
-      // satisfied cross-queue wait costs its queue ~4.5 us:
-      // profiles/r04/waitbench.jsonl).  In mode 1 kernels A have streams of
-      // their own, kernel B's waits hold nothing else back, and the relay
-      // would only lengthen the comm stream's chain before the next bucket's
-      // reduction (profiles/r04/peer_ab_*.jsonl).
-      TRY(await_all(r_seq, b));
-      for (size_t k = k0; k < k1; ++k) {
-        Device &d = c->devs[k];
-        HIP_TRY(hipSetDevice(d.hip_id));
-        for (size_t h = 0; h < c->devs.size(); ++h) {
-          if (h == k) continue;  // its own reduction: stream order
-          HIP_TRY(hipStreamWaitEvent(d.comm_stream, ev_red(h, b), 0));
-          note_wait(k, 2, ev_red(h, b));
-        }
-        HIP_TRY(hipEventRecord(d.bucket_all[b], d.comm_stream));
-      }
-    }
     return CBX_OK;
   }
 
   // Kernel B (Phase C, + D on copy) of bucket b on devices [k0, k1).
   int apply(int64_t b, size_t k0, size_t k1) {
-    if (peer && !relay()) TRY(await_all(r_seq, b));  // else the comm stream relayed them
+    if (peer) TRY(await_all(r_seq, b));
     for (size_t k = k0; k < k1; ++k) {
       Device &d = c->devs[k];
       HIP_TRY(hipSetDevice(d.hip_id));
       // its bucket's collective; the peer-read kernel B reads D from every
-      // shard's owner, so it waits for every device's reduction (pipelined:
-      // the one event its comm stream relays, see collective)
-      if (relay()) {
-        HIP_TRY(hipStreamWaitEvent(d.stream, d.bucket_all[b], 0));
-        note_wait(k, 0, d.bucket_all[b]);
-      } else {
-        for (size_t h = peer ? 0 : k; h < (peer ? c->devs.size() : k + 1); ++h) {
-          if (!pipelined && h == k) continue;  // in order on this stream
-          HIP_TRY(hipStreamWaitEvent(d.stream, ev_red(h, b), 0));
-          note_wait(k, 0, ev_red(h, b));
-        }
+      // shard's owner, so it waits for every device's reduction.  (Relaying
+      // them through the comm stream, one wait here instead of G, measured
+      // slower in both modes: profiles/r04/peer_ab.jsonl.)
+      for (size_t h = peer ? 0 : k; h < (peer ? c->devs.size() : k + 1); ++h) {
+        if (!pipelined && h == k) continue;  // in order on this stream
+        HIP_TRY(hipStreamWaitEvent(d.stream, ev_red(h, b), 0));
+        note_wait(k, 0, ev_red(h, b));
       }
       cbx::LaunchConfig cfg = c->apply_cfg;
       cfg.num_cus = d.num_cus;

@@ -1,13 +1,15 @@
 #!/usr/bin/env python3
-"""Interleaved A/B of the bucketed peer-read form, a fresh process per sample
-(scripts/peer_sweep.py; one process over G "devices" that are all device 0:
-a rehearsal, not an N-GPU measurement): variant "default" against
-"norelay" ($CBX_EXP_PEER_NO_RELAY: kernel B waits on every device's
-reduction itself, in mode 0 too), alternating, `--rounds` times per G, with
-GPU_MAX_HW_QUEUES = 4 streams x G (at most 32) so no two of the devices'
-streams share a hardware queue.  Every sample and a summary (per G and
-configuration: the median of each variant's samples, and each configuration
-against the variant's 1-bucket step) as JSON lines."""
+"""The bucketed peer-read form against its one-bucket step, a fresh process
+per sample (scripts/peer_sweep.py; one process over G "devices" that are all
+device 0: a rehearsal, not an N-GPU measurement), `--rounds` times per G,
+variants (library experiment toggles, scripts/peer_sweep.py) alternating.
+Round 4 compared "default" with "norelay" ($CBX_EXP_PEER_NO_RELAY, since
+removed with the relay it switched off) at GPU_MAX_HW_QUEUES = 4 x G
+(profiles/r04/peer_ab.jsonl: 32 queues at G = 8 made every step ~5x slower,
+the hardware scheduler oversubscribed); the default is now 16.  Every sample
+and a summary (per G and configuration: the median of each variant's
+samples, and each configuration against the variant's 1-bucket step) as
+JSON lines."""
 from __future__ import annotations
 
 import argparse
@@ -25,7 +27,8 @@ def main():
     ap.add_argument("--G", default="2,8")
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--configs", default="1/0/1/1,4/0/1/1,8/0/1/1,4/1/1/1,8/1/1/1,8/1/2/1")
-    ap.add_argument("--variants", default="default,norelay")
+    ap.add_argument("--variants", default="default")
+    ap.add_argument("--hw-queues", type=int, default=16)
     ap.add_argument("--passes", type=int, default=1)
     a = ap.parse_args()
     samples = {}
@@ -33,7 +36,7 @@ def main():
     for G in (int(x) for x in a.G.split(",")):
         for r in range(a.rounds):
             for v in (variants if r % 2 == 0 else variants[::-1]):
-                env = dict(os.environ, GPU_MAX_HW_QUEUES=str(min(32, max(16, 4 * G))))
+                env = dict(os.environ, GPU_MAX_HW_QUEUES=str(a.hw_queues))
                 p = subprocess.run([sys.executable, os.path.join(ROOT, "scripts", "peer_sweep.py"), "--G", str(G),
                                     "--configs", a.configs, "--variants", v, "--passes", str(a.passes)],
                                    env=env, capture_output=True, text=True, timeout=600)

@@ -35,12 +35,13 @@ def main():
     ap.add_argument("--timing", type=int, default=1)
     ap.add_argument("--gap-ms", type=float, default=0.0, help="host sleep between configurations (trace splitting)")
     ap.add_argument("--variants", default="default",
-                    help="comma-separated contexts: 'default', or an experiment toggle set at the context's creation "
-                         "('norelay': CBX_EXP_PEER_NO_RELAY)")
+                    help="comma-separated contexts: 'default', or an experiment toggle of the library set in the "
+                         "environment at the context's creation (none at present; round 4's 'norelay' was "
+                         "CBX_EXP_PEER_NO_RELAY, profiles/r04/peer_ab.jsonl)")
     a = ap.parse_args()
     from crossbow_amd import SYNC_BSP, UPDATE_SMA, TheGPU, _lib
     from crossbow_amd.variables import MODELS, register
-    toggles = {"default": None, "norelay": "CBX_EXP_PEER_NO_RELAY"}
+    toggles = {"default": None}
 
     def make(variant):
         env = toggles[variant]
