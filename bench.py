@@ -43,12 +43,15 @@ import threading
 import time
 
 # Before the HIP runtime starts (it reads this once): ROCclr's hardware
-# queues per device.  16 gives each of the pipeline's streams a queue of its
-# own, the recommended deployment setting (HIP's default 4
-# measured within 3 % on one GPU); an explicit setting by the caller wins.
-# Reported in config.hw_queues either way.
-HW_QUEUES_SET_BY = "caller" if "GPU_MAX_HW_QUEUES" in os.environ else "bench.py default"
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "16")
+# queues per device.  16 gives each of the pipeline's streams (and RCCL's) a
+# queue of its own: the recommended deployment setting (INTEGRATION.md;
+# HIP's default 4 measured within 3 % on one GPU, while more
+# than 16 oversubscribed the hardware scheduler).  bench.py runs the
+# recommended setting whatever the environment says (GPU boxes export HIP's 4)
+# unless --keep-hw-queues; config.hw_queues records both.
+HW_QUEUES_ENV = os.environ.get("GPU_MAX_HW_QUEUES")
+if "--keep-hw-queues" not in sys.argv:
+    os.environ["GPU_MAX_HW_QUEUES"] = "16"
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 if ROOT not in sys.path:
@@ -124,6 +127,9 @@ def parse():
                    help="multiplies every phase deadline of the watchdog (0 = off); on a missed deadline the run "
                         "writes every thread's stack to stderr and exits with code 3")
     p.add_argument("--watchdog-selftest", type=float, default=0.0, help=argparse.SUPPRESS)
+    p.add_argument("--keep-hw-queues", action="store_true",
+                   help="run with the environment's GPU_MAX_HW_QUEUES (HIP's default 4 if unset) instead of the "
+                        "recommended 16")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
                    help="PMC-derived HBM bytes per launch (written by scripts/pmc_traffic.py)")
     return p.parse_args()
@@ -422,6 +428,8 @@ def rccl_tuning_run(args, G, single, cfg, wd):
            "--allreduce-group", str(cfg["group"]), "--allreduce-algorithm", str(cfg["algorithm"])]
     if args.rehearse_one_gpu:
         cmd.append("--rehearse-one-gpu")
+    if args.keep_hw_queues:
+        cmd.append("--keep-hw-queues")
     env = {k: v for k, v in os.environ.items() if not k.startswith(("NCCL_DEBUG", "NCCL_HOSTID"))}
     if single:
         cmd += ["--single-process"]
@@ -658,7 +666,10 @@ def main():
             "tuning_errors": tuning.errors if tuning else None,
             # ROCclr's hardware queues per device (read once at HIP start): the
             # pipeline's streams each need one
-            "hw_queues": {"GPU_MAX_HW_QUEUES": int(os.environ["GPU_MAX_HW_QUEUES"]), "set_by": HW_QUEUES_SET_BY},
+            "hw_queues": {"GPU_MAX_HW_QUEUES": int(os.environ.get("GPU_MAX_HW_QUEUES", "4")),
+                          "environment_had": HW_QUEUES_ENV,
+                          "set_by": "--keep-hw-queues (the environment's)" if args.keep_hw_queues else
+                                    "bench.py (the recommended deployment setting)"},
             "kernel_config": dict(block=args.block, blocks_per_cu=args.blocks_per_cu, policy=args.policy,
                                   unroll=args.unroll, waves_per_cu=args.waves_per_cu, bucket_mb=args.bucket_mb),
         },
