@@ -344,13 +344,19 @@ int main (void) {
 		CHECK (cbx_set_allreduce_algorithm (c, CBX_ALLREDUCE_PEER));
 		CHECK (cbx_set_enqueue_threads (c, threads));
 		CHECK (cbx_set_bucket_elements (c, 4096));
-		for (int clock = 1; clock < 7; ++clock) {
+		for (int clock = 1; clock < 9; ++clock) {
 			if (clock == 4) CHECK (cbx_set_pipeline_mode (c, 1));
+			if (clock == 6) CHECK (cbx_set_timing (c, 1));  /* span records: G x 2 waits per reduction */
 			CHECK (cbx_lock_any (c));
 			CHECK (cbx_synchronise (c, 0, clock, 0, 0));
 			CHECK (cbx_unlock_any (c));
 		}
 		CHECK (cbx_wait (c));
+		{
+			float ms[CBX_T_COUNT], hist[8];
+			CHECK (cbx_last_timing (c, 3, ms));
+			EXPECT (cbx_timing_history (c, 0, CBX_T_ALLREDUCE, hist, 8) == 3);
+		}
 		CHECK (cbx_replica_read (c, 3, CBX_BUF_DATA, host, (size_t) 4 * n));
 		EXPECT (all_finite (host, (size_t) n));
 		CHECK (cbx_free (c));
