@@ -48,9 +48,14 @@ import time
 # HIP's default 4 measured within 3 % on one GPU, while more
 # than 16 oversubscribed the hardware scheduler).  bench.py runs the
 # recommended setting whatever the environment says (GPU boxes export HIP's 4)
-# unless --keep-hw-queues; config.hw_queues records both.
+# unless --keep-hw-queues, or in a one-process-per-rank rehearsal where every
+# rank shares one GPU (16 queues per process then oversubscribe the hardware
+# scheduler: 4 ranks ran ~5x slower, profiles/r04/rehearse_perrank_n4.log);
+# config.hw_queues records both.
 HW_QUEUES_ENV = os.environ.get("GPU_MAX_HW_QUEUES")
-if "--keep-hw-queues" not in sys.argv:
+HW_QUEUES_KEPT = ("--keep-hw-queues" in sys.argv or
+                  ("--rehearse-one-gpu" in sys.argv and int(os.environ.get("WORLD_SIZE", "1")) > 1))
+if not HW_QUEUES_KEPT:
     os.environ["GPU_MAX_HW_QUEUES"] = "16"
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -668,8 +673,8 @@ def main():
             # pipeline's streams each need one
             "hw_queues": {"GPU_MAX_HW_QUEUES": int(os.environ.get("GPU_MAX_HW_QUEUES", "4")),
                           "environment_had": HW_QUEUES_ENV,
-                          "set_by": "--keep-hw-queues (the environment's)" if args.keep_hw_queues else
-                                    "bench.py (the recommended deployment setting)"},
+                          "set_by": ("the environment (--keep-hw-queues, or a per-rank rehearsal on one GPU)"
+                                     if HW_QUEUES_KEPT else "bench.py (the recommended deployment setting)")},
             "kernel_config": dict(block=args.block, blocks_per_cu=args.blocks_per_cu, policy=args.policy,
                                   unroll=args.unroll, waves_per_cu=args.waves_per_cu, bucket_mb=args.bucket_mb),
         },

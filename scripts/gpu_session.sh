@@ -5,6 +5,7 @@
 #   bench      python bench.py $BENCH_ARGS
 #   smoke      __graft_entry__.smoke()
 #   rehearse   bench.py at N = 2 / 4 / 8 in both process forms on one GPU
+#   rehearse-perrank  the same, one process per rank only
 #   enqueue    scripts/host_enqueue_multidev.py (single-process host cost)
 #   rocprof    rocprofv3 --kernel-trace --stats of bench.py $BENCH_ARGS
 #   markers    rocprofv3 --marker-trace --kernel-trace of the single-process rehearsal
@@ -33,6 +34,11 @@ for s in "${STEPS[@]}"; do
     tests:*) run "pytest_${s#tests:}" 600 $PYTEST tests -k "${s#tests:}" ;;
     bench) run bench 600 python bench.py ${BENCH_ARGS:-} ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as e; e.smoke()" ;;
+    rehearse-perrank)
+      for g in 2 4 8; do
+        run "perrank_n$g" 500 python -m torch.distributed.run --nnodes=1 --nproc-per-node $g --master-addr 127.0.0.1 \
+          --master-port $((29600 + g)) bench.py --gpus $g --rehearse-one-gpu --steps 20 --warmup 3 --no-staged
+      done ;;
     rehearse)
       for g in 2 4 8; do
         run "single_n$g" 300 python bench.py --gpus $g --single-process --rehearse-one-gpu --steps 20 --warmup 3 \
