@@ -92,6 +92,9 @@ def parse():
                         "<0 = one bucket")
     p.add_argument("--calib-steps", type=int, default=10,
                    help="G>1: unpipelined steps before warm-up that time kernel A, the all-reduce and kernel B apart")
+    p.add_argument("--tune-steps", type=int, default=10, help="G>1 tuner: timed steps per candidate and pass")
+    p.add_argument("--tune-passes", type=int, default=2,
+                   help="G>1 tuner: interleaved passes over the candidates (each keeps its best pass)")
     p.add_argument("--force-split", action="store_true", help="use kernel A + all-reduce + B even at G=1")
     p.add_argument("--cpu-seconds", type=float, default=10.0)
     p.add_argument("--cpu-elements", type=int, default=0,
@@ -418,6 +421,48 @@ def span_stats(gpu, _lib, locals_, steps):
     return tuple(out)
 
 
+def base_identity(gpu, world):
+    """After the timed region at G > 1: every GPU must hold a bitwise
+    identical base model z and momentum `last`, because every GPU applies the
+    same reduced difference D (sma.c:168-174; the tests' cross-rank check).
+    A digest of each local device's z and last, gathered over the ranks
+    (gloo) and compared, plus a finiteness check: a collective or peer read
+    that ran out of order would show up here, so a fast but wrong
+    configuration cannot pass as a measurement.  No oracle is involved."""
+    import hashlib
+
+    import numpy as np
+    from crossbow_amd import BUF_DATA, BUF_LAST
+    local = []
+    finite = True
+    for g in gpu.local_devices():
+        h = hashlib.blake2b(digest_size=16)
+        for kind in (BUF_DATA, BUF_LAST):
+            a = gpu.base_read(g, kind)
+            finite = finite and bool(np.isfinite(a).all())
+            h.update(a.view(np.uint8))
+        local.append((int(g), h.hexdigest()))
+    every = [local]
+    if world > 1:
+        import torch.distributed as dist
+        every = [None] * world
+        dist.all_gather_object(every, local)
+    digests = {g: d for part in every for g, d in part}
+    finite = all_ranks(finite, world)
+    return {"z_last_identical_on_every_gpu": len(set(digests.values())) == 1, "finite": finite,
+            "gpus_checked": len(digests), "digest": sorted(set(digests.values()))[0] if digests else None,
+            "checked": "blake2b of each GPU's base model z and momentum last after the timed region, compared "
+                       "across every GPU (every GPU applies the same D, sma.c:168-174)"}
+
+
+def all_ranks(flag: bool, world: int) -> bool:
+    """Logical AND of a flag over the ranks."""
+    if world <= 1:
+        return flag
+    from crossbow_amd import dist as D
+    return D.max_over_ranks(0.0 if flag else 1.0, world) == 0.0
+
+
 def rccl_tuning_run(args, G, single, cfg, wd):
     """RCCL's own algorithm / protocol / channel choices for the collectives
     of the chosen configuration, from a separate short run (3 steps) with
@@ -591,6 +636,8 @@ def main():
         # warm-up autotune of the pipeline on the live communicator (same choice on every rank)
         tuning = D.tune_buckets(gpu, n, world, step, progress=(lambda m: log(f"[bench] {m}")) if rank == 0 else None,
                                 ndev=G, peer=single, peer_only=peer_only, threads=single,
+                                steps=max(1, args.tune_steps), passes=max(1, args.tune_passes),
+                                warmup=min(2, max(1, args.tune_steps)),
                                 phase=lambda name: wd.enter(name, 90))
         chosen.update(bucket_elements=tuning.bucket_elements, buckets=tuning.buckets, mode=tuning.mode,
                       stride=tuning.stride, group=tuning.group, algorithm=tuning.algorithm,
@@ -627,6 +674,10 @@ def main():
     el = D.max_over_ranks(el, world)
     wd.enter("timing read-back", 120)
     spans = span_stats(gpu, _lib, nlocal, args.steps) if split else None
+    identity = None
+    if G > 1:
+        wd.enter("cross-GPU identity of z and last", 180)
+        identity = base_identity(gpu, world)
 
     step_bytes, kernel_bytes = alg_bytes(n, args.replicas, args.momentum, 2 if split else 1)
     steps_ms = gpu.timing_history(_lib.T_STEP)[-args.steps:]
@@ -742,6 +793,8 @@ def main():
     result["roofline"]["traffic"] = traffic
     result["roofline"]["traffic_note"] = traffic_note
     result["step_ms_device_median"] = round(statistics.median(steps_ms), 4)
+    if identity is not None:
+        result["identity"] = identity
     if G > 1:
         # Host side of the step (lockAny + synchronise + unlockAny, every local
         # device's enqueue) against the device's step: the single-process form

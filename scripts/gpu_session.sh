@@ -37,7 +37,7 @@ for s in "${STEPS[@]}"; do
     rehearse-perrank)
       for g in 2 4 8; do
         run "perrank_n$g" 500 python -m torch.distributed.run --nnodes=1 --nproc-per-node $g --master-addr 127.0.0.1 \
-          --master-port $((29600 + g)) bench.py --gpus $g --rehearse-one-gpu --steps 20 --warmup 3 --no-staged
+          --master-port $((29600 + g)) bench.py --gpus $g --rehearse-one-gpu --steps 20 --warmup 3 --no-staged --tune-steps 3 --tune-passes 1 --calib-steps 3
       done ;;
     rehearse)
       for g in 2 4 8; do
@@ -46,7 +46,7 @@ for s in "${STEPS[@]}"; do
       done
       for g in 2 4 8; do
         run "perrank_n$g" 500 python -m torch.distributed.run --nnodes=1 --nproc-per-node $g --master-addr 127.0.0.1 \
-          --master-port $((29600 + g)) bench.py --gpus $g --rehearse-one-gpu --steps 20 --warmup 3 --no-staged
+          --master-port $((29600 + g)) bench.py --gpus $g --rehearse-one-gpu --steps 20 --warmup 3 --no-staged --tune-steps 3 --tune-passes 1 --calib-steps 3
       done ;;
     enqueue)
       run enqueue_peer 400 python scripts/host_enqueue_multidev.py --variant peer

@@ -76,6 +76,9 @@ def test_bench_two_ranks_through_the_launcher_prints_one_json_line():
     assert "separate" in ar["rccl_tuning_source"]
     assert d["host"]["enqueue_ms_per_step_timed"] > 0 and d["host"]["devices_per_process"] == 1
     assert d["config"]["hw_queues"]["GPU_MAX_HW_QUEUES"] >= 1
+    # every rank ends the timed region with the same z and last, bit for bit
+    idn = d["identity"]
+    assert idn["z_last_identical_on_every_gpu"] is True and idn["finite"] is True and idn["gpus_checked"] == 2
 
 
 @pytest.mark.timeout(300)
@@ -101,6 +104,7 @@ def test_bench_single_process_two_devices_one_gpu():
     assert c["enqueue_threads"] in (0, 1) and c["buckets"] in (1, 4, 8)
     assert not c["tuning_errors"], c["tuning_errors"]
     assert d["allreduce"]["rccl_tuning"] is None and d["allreduce"]["timed"]["busbw_GBs"] > 0
+    assert d["identity"]["z_last_identical_on_every_gpu"] is True and d["identity"]["gpus_checked"] == 2
 
 
 @pytest.mark.timeout(300)
