@@ -595,6 +595,12 @@ def main():
         gpu.set_allreduce_algorithm(ALLREDUCE_PEER)
     gpu.fill_synthetic(SEED)
     gpu.set_timing(True)
+    peer_ipc = None  # one process per GPU: "mapped", or why the IPC mapping failed
+    if G > 1 and not single:
+        # the peer-read all-reduce needs every rank's buffers mapped through
+        # IPC handles (then it is a tuner candidate, as in the single process)
+        wd.enter("peer-read IPC mapping", 120)
+        peer_ipc = D.setup_peer(gpu, world) or "mapped"
 
     clock = 0
     host_ms = []
@@ -635,7 +641,7 @@ def main():
     if split and not explicit:
         # warm-up autotune of the pipeline on the live communicator (same choice on every rank)
         tuning = D.tune_buckets(gpu, n, world, step, progress=(lambda m: log(f"[bench] {m}")) if rank == 0 else None,
-                                ndev=G, peer=single, peer_only=peer_only, threads=single,
+                                ndev=G, peer=single or peer_ipc == "mapped", peer_only=peer_only, threads=single,
                                 steps=max(1, args.tune_steps), passes=max(1, args.tune_passes),
                                 warmup=min(2, max(1, args.tune_steps)),
                                 phase=lambda name: wd.enter(name, 90))
@@ -729,6 +735,9 @@ def main():
             "allreduce_group": chosen["group"] if split else None,
             "allreduce_algorithm": form if split else None,
             "enqueue_threads": chosen["enqueue_threads"] if single else None,
+            # one process per GPU: whether the peer-read form's IPC mapping
+            # (cbx_peer_export / _import) succeeded on every rank, else why not
+            "peer_ipc": peer_ipc,
             "bucket_tuning_ms_per_step": tuning.table if tuning else None,
             "tuning_errors": tuning.errors if tuning else None,
             # ROCclr's hardware queues per device (read once at HIP start): the

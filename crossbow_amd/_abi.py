@@ -31,6 +31,7 @@ T_KERNEL, T_ALLREDUCE, T_APPLY, T_STEP, T_H2D, T_D2H, T_COUNT = range(7)
 SYNC_BSP, SYNC_SSP, SYNC_ASP = 0, 1, 2
 UPDATE_DEFAULT, UPDATE_WORKER, UPDATE_SYNCHRONOUSEAMSGD, UPDATE_SMA = 0, 1, 3, 7
 ALLREDUCE_RCCL, ALLREDUCE_PEER, ALLREDUCE_RSAG = 0, 1, 2
+PEER_BLOB_BYTES = 256  # CBX_PEER_BLOB_BYTES
 STAGING_ZEROCOPY, STAGING_DMA = 0, 1
 
 
@@ -134,6 +135,8 @@ SIGNATURES = {
     "cbx_set_cross_wait_stride": (_I, [_P, _I]),
     "cbx_set_allreduce_group": (_I, [_P, _I]),
     "cbx_set_allreduce_algorithm": (_I, [_P, _I]),
+    "cbx_peer_export": (_I, [_P, _P, _c.POINTER(_S)]),
+    "cbx_peer_import": (_I, [_P, _P, _I]),
     "cbx_set_staging_mode": (_I, [_P, _I]),
     "cbx_set_bucket_elements": (_I, [_P, _c.c_longlong]),
     "cbx_set_force_split": (_I, [_P, _I]),

@@ -187,6 +187,7 @@ int cbx_init_rank(cbx_context **out, int device, int nranks, int rank, const uns
 int cbx_free(cbx_context *c) {
   if (!c) return CBX_OK;
   c->pool.reset();  // the enqueue threads are idle between calls
+  if (!c->devs.empty()) peer_close(c);  // before any arena goes: the other ranks may still read this one
   for (Replica *r : c->replicas) {
     if (r && r->client && r->local >= 0) {
       (void)hipSetDevice(c->devs[r->local].hip_id);
@@ -1572,12 +1573,23 @@ int cbx_set_allreduce_algorithm(cbx_context *c, int algorithm) {
   if (algorithm == CBX_ALLREDUCE_RSAG && (c->G > cbx::kMaxDevices || cbx::kPadFloat4 % c->G != 0))
     return fail(CBX_ERR_UNSUPPORTED, "the reduce-scatter form needs G dividing %lld (G = %d)",
                 (long long)cbx::kPadFloat4, c->G);
-  if (algorithm == CBX_ALLREDUCE_PEER && c->per_rank && c->G > 1)
-    return fail(CBX_ERR_UNSUPPORTED, "the peer-read all-reduce needs one process over every device (cbx_init)");
+  if (algorithm == CBX_ALLREDUCE_PEER && c->per_rank && c->G > 1 && !c->ipc.ready)
+    return fail(CBX_ERR_STATE, "the peer-read all-reduce with one process per GPU needs cbx_peer_export / "
+                "cbx_peer_import on every rank first");
   if (algorithm == CBX_ALLREDUCE_PEER && c->G > cbx::kMaxDevices)
     return fail(CBX_ERR_UNSUPPORTED, "the peer-read all-reduce takes at most %d devices", cbx::kMaxDevices);
   c->allreduce_algo = algorithm;
   return CBX_OK;
+}
+
+int cbx_peer_export(cbx_context *c, void *blob, size_t *bytes) {
+  TRY(check_ctx(c));
+  return peer_export(c, blob, bytes);
+}
+
+int cbx_peer_import(cbx_context *c, const void *blobs, int nranks) {
+  TRY(check_ctx(c));
+  return peer_import(c, blobs, nranks);
 }
 
 int cbx_set_enqueue_threads(cbx_context *c, int mode) {

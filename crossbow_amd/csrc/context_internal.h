@@ -10,6 +10,7 @@
 
 #include <pthread.h>
 #include <sched.h>
+#include <sys/mman.h>
 #include <sys/stat.h>
 #include <sys/types.h>
 #include <fcntl.h>
@@ -18,6 +19,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <cmath>
 #include <condition_variable>
 #include <cstdarg>
@@ -519,6 +521,35 @@ struct cbx_context {
   // threaded form is measured on distinct devices (bench.py's tuner times both).
   int enqueue_threads = -1;
   std::unique_ptr<cbx::host::EnqueuePool> pool;
+  // The peer-read all-reduce with one process per GPU (cbx_peer_export /
+  // cbx_peer_import, sync_steps.hip): every other rank's acc and D mapped
+  // here through its arena's IPC handle, and one page of completion flags in
+  // POSIX shared memory that every rank pins (hipHostRegister).  Rank h
+  // writes its flags from its streams (hipStreamWriteValue64: the step's
+  // sequence number once kernel A / the reduction of a bucket is done); the
+  // others' streams wait on them (hipStreamWaitValue64 >=).  Flags in device
+  // memory opened through IPC were never seen by a waiting stream on the one
+  // GPU tried (scripts/ipcprobe.hip), so the page is host memory.
+  struct PeerIpc {
+    bool ready = false;
+    bool broken = false;                  // a step failed part-way: the flags were released
+    int me = 0;
+    std::vector<char *> mapped;           // per rank: its arena opened here (own: nullptr)
+    std::vector<const cbx::v4f *> acc;    // per rank: acc data (own: the local arena's)
+    std::vector<const float *> acc_ctrl;  // per rank: acc control block
+    std::vector<const cbx::v4f *> D;      // per rank: D data
+    void *page = nullptr;                 // the flag page, shared by every rank
+    size_t page_bytes = 0;
+    uint64_t *dpage = nullptr;            // the same page as the device sees it
+    bool owner = false;                   // rank 0 created the shared-memory object
+    char shm_name[64] = {};
+    uint64_t seq = 0;                     // split steps run in this form
+  } ipc;
+  // $CBX_FAULT_SKIP_PEER_WAIT (tests only): the per-rank peer-read form skips
+  // its waits on the other ranks' flags, and every rank but 0 runs a 2 ms
+  // idle kernel ahead of each kernel A, so rank 0 reads acc before it is
+  // written (results are then wrong: the test proves the waits matter).
+  bool fault_skip_peer_wait = std::getenv("CBX_FAULT_SKIP_PEER_WAIT") != nullptr;
 };
 
 namespace cbx::host {
@@ -957,5 +988,24 @@ int alloc_host_mirror(cbx_context *c);
 // Stream-order check of one recorded step, and of two consecutive ones.
 int check_order_step(const Device::OrderStep &o);
 int check_order_pair(const Device::OrderStep &p, const Device::OrderStep &q);
+// The per-rank peer-read form's handles (cbx_peer_export / _import) and its
+// teardown (cbx_free: waits until every rank is done with this rank's memory).
+int peer_export(cbx_context *c, void *blob, size_t *bytes);
+int peer_import(cbx_context *c, const void *blobs, int nranks);
+void peer_close(cbx_context *c);
+
+// Completion flags of the per-rank peer-read form, per rank: one word per
+// bucket for "kernel A done", one for "reduction done", and one for "done
+// with the other ranks' memory" (teardown), each holding a step sequence
+// number (monotonic: a waiter waits for >=, so a flag already past it never
+// blocks).  A failed step writes kIpcRelease into its rank's words so no
+// other rank's stream waits forever.
+constexpr int64_t kIpcMaxBuckets = 4096;
+constexpr size_t kIpcRankWords = 2 * kIpcMaxBuckets + 64;  // a[], r[], done + padding (512 B)
+constexpr int kIpcA = 0, kIpcR = 1, kIpcDone = 2;
+constexpr uint64_t kIpcRelease = 1ull << 62;
+inline size_t ipc_word(int rank, int kind, int64_t b) {
+  return (size_t)rank * kIpcRankWords + (kind == kIpcDone ? 2 * kIpcMaxBuckets : (size_t)kind * kIpcMaxBuckets + b);
+}
 
 }  // namespace cbx::host

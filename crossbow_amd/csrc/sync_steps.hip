@@ -143,6 +143,174 @@ int ensure_peer_access(cbx_context *c) {
   return CBX_OK;
 }
 
+// ---------------------------------------------------------------------------
+// The same form with one process per GPU (cbx_init_rank): the other ranks'
+// arenas through IPC handles (dmabuf), and the cross-process order through
+// flags in a shared host page instead of events (cbx_context::PeerIpc in
+// context_internal.h).  The pipeline is SplitStep's, unchanged: where the
+// single-process form waits on device h's event of bucket b, a rank waits
+// for rank h's flag of bucket b to reach this step's sequence number.
+// ---------------------------------------------------------------------------
+namespace {
+
+struct PeerBlob {
+  uint32_t magic;
+  int32_t rank, G, pad;
+  int64_t n4;
+  uint64_t acc_off, acc_ctrl_off, d_off;  // from the arena's base
+  hipIpcMemHandle_t arena;
+  char shm[64];  // rank 0's: the flag page
+};
+static_assert(sizeof(PeerBlob) <= CBX_PEER_BLOB_BYTES, "peer blob size");
+constexpr uint32_t kPeerMagic = 0x50584243u;  // "CBXP"
+
+int map_flag_page(cbx_context *c, bool create) {
+  auto &p = c->ipc;
+  p.page_bytes = ((size_t)c->G * kIpcRankWords * sizeof(uint64_t) + 4095) / 4096 * 4096;
+  const int fd = shm_open(p.shm_name, create ? (O_CREAT | O_EXCL | O_RDWR) : O_RDWR, 0600);
+  if (fd < 0) return fail(CBX_ERR_IO, "shm_open(%s): %s", p.shm_name, strerror(errno));
+  p.owner = create;
+  if (create && ftruncate(fd, (off_t)p.page_bytes) != 0) {
+    close(fd);
+    return fail(CBX_ERR_IO, "ftruncate(%s): %s", p.shm_name, strerror(errno));
+  }
+  void *m = mmap(nullptr, p.page_bytes, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+  close(fd);
+  if (m == MAP_FAILED) return fail(CBX_ERR_IO, "mmap(%s): %s", p.shm_name, strerror(errno));
+  p.page = m;  // a new object reads zero: no flag set yet
+  HIP_TRY(hipSetDevice(c->devs[0].hip_id));
+  HIP_TRY(hipHostRegister(p.page, p.page_bytes, hipHostRegisterMapped | hipHostRegisterPortable));
+  HIP_TRY(hipHostGetDevicePointer(reinterpret_cast<void **>(&p.dpage), p.page, 0));
+  return CBX_OK;
+}
+
+volatile uint64_t *host_word(cbx_context *c, int rank, int kind, int64_t b) {
+  return static_cast<volatile uint64_t *>(c->ipc.page) + ipc_word(rank, kind, b);
+}
+
+// A step that failed part-way: no other rank may wait on this one's flags forever.
+void release_flags(cbx_context *c) {
+  auto &p = c->ipc;
+  if (!p.page) return;
+  for (int64_t b = 0; b < kIpcMaxBuckets; ++b) {
+    *host_word(c, p.me, kIpcA, b) = kIpcRelease;
+    *host_word(c, p.me, kIpcR, b) = kIpcRelease;
+  }
+  __atomic_thread_fence(__ATOMIC_SEQ_CST);
+}
+
+}  // namespace
+
+int peer_export(cbx_context *c, void *blob, size_t *bytes) {
+  if (!c->manager) return fail(CBX_ERR_STATE, "cbx_peer_export: set the model manager first");
+  if (!c->per_rank || c->G < 2)
+    return fail(CBX_ERR_UNSUPPORTED, "cbx_peer_export: one process per GPU with G > 1 only (one process over "
+                "every device reaches its peers directly)");
+  if (c->G > cbx::kMaxDevices) return fail(CBX_ERR_UNSUPPORTED, "the peer-read all-reduce takes at most %d ranks",
+                                           cbx::kMaxDevices);
+  if (!blob || !bytes) return fail(CBX_ERR_INVALID, "cbx_peer_export: null blob");
+  Device &d = c->devs[0];
+  PeerBlob pb;
+  std::memset(&pb, 0, sizeof(pb));
+  pb.magic = kPeerMagic;
+  pb.rank = d.g;
+  pb.G = c->G;
+  pb.n4 = c->n4;
+  pb.acc_off = (uint64_t)(reinterpret_cast<char *>(base_dev(c, d, CBX_BUF_GRADIENT)) - d.arena);
+  pb.acc_ctrl_off = (uint64_t)(reinterpret_cast<char *>(base_ctrl(d, CBX_BUF_GRADIENT)) - d.arena);
+  pb.d_off = (uint64_t)(reinterpret_cast<char *>(base_dev(c, d, CBX_BUF_DIFF)) - d.arena);
+  HIP_TRY(hipSetDevice(d.hip_id));
+  HIP_TRY(hipIpcGetMemHandle(&pb.arena, d.arena));
+  if (d.g == 0 && !c->ipc.page) {
+    std::snprintf(c->ipc.shm_name, sizeof(c->ipc.shm_name), "/cbx_peer_%d_%llx", (int)getpid(),
+                  (unsigned long long)std::chrono::steady_clock::now().time_since_epoch().count());
+    TRY(map_flag_page(c, true));
+  }
+  if (d.g == 0) std::memcpy(pb.shm, c->ipc.shm_name, sizeof(pb.shm));
+  std::memset(blob, 0, CBX_PEER_BLOB_BYTES);
+  std::memcpy(blob, &pb, sizeof(pb));
+  *bytes = CBX_PEER_BLOB_BYTES;
+  return CBX_OK;
+}
+
+int peer_import(cbx_context *c, const void *blobs, int nranks) {
+  auto &p = c->ipc;
+  if (p.ready) return fail(CBX_ERR_STATE, "cbx_peer_import: already imported");
+  if (!c->manager || !c->per_rank || c->G < 2) return fail(CBX_ERR_STATE, "cbx_peer_import: call cbx_peer_export first");
+  if (!blobs || nranks != c->G) return fail(CBX_ERR_INVALID, "cbx_peer_import: need the blobs of all %d ranks", c->G);
+  Device &d = c->devs[0];
+  std::vector<PeerBlob> pb(nranks);
+  for (int h = 0; h < nranks; ++h) {
+    std::memcpy(&pb[h], static_cast<const char *>(blobs) + (size_t)h * CBX_PEER_BLOB_BYTES, sizeof(PeerBlob));
+    if (pb[h].magic != kPeerMagic || pb[h].rank != h || pb[h].G != c->G || pb[h].n4 != c->n4)
+      return fail(CBX_ERR_INVALID, "cbx_peer_import: blob %d is not rank %d's of this job (rank %d, G %d, %lld "
+                  "float4s)", h, h, pb[h].rank, pb[h].G, (long long)pb[h].n4);
+  }
+  p.me = d.g;
+  if (p.me != 0) {
+    std::memcpy(p.shm_name, pb[0].shm, sizeof(p.shm_name));
+    p.shm_name[sizeof(p.shm_name) - 1] = 0;
+    TRY(map_flag_page(c, false));
+  }
+  if (!p.page) return fail(CBX_ERR_STATE, "cbx_peer_import: rank 0 exported no flag page");
+  p.mapped.assign(nranks, nullptr);
+  p.acc.assign(nranks, nullptr);
+  p.acc_ctrl.assign(nranks, nullptr);
+  p.D.assign(nranks, nullptr);
+  HIP_TRY(hipSetDevice(d.hip_id));
+  for (int h = 0; h < nranks; ++h) {
+    char *base = d.arena;
+    if (h != p.me) {
+      void *m = nullptr;
+      hipError_t e = hipIpcOpenMemHandle(&m, pb[h].arena, hipIpcMemLazyEnablePeerAccess);
+      if (e != hipSuccess) {
+        const std::string msg = hipGetErrorString(e);
+        peer_close(c);
+        return fail(CBX_ERR_HIP, "hipIpcOpenMemHandle(rank %d's arena): %s", h, msg.c_str());
+      }
+      p.mapped[h] = base = static_cast<char *>(m);
+    }
+    p.acc[h] = reinterpret_cast<const cbx::v4f *>(base + pb[h].acc_off);
+    p.acc_ctrl[h] = reinterpret_cast<const float *>(base + pb[h].acc_ctrl_off);
+    p.D[h] = reinterpret_cast<const cbx::v4f *>(base + pb[h].d_off);
+  }
+  p.ready = true;
+  return CBX_OK;
+}
+
+void peer_close(cbx_context *c) {
+  auto &p = c->ipc;
+  if (!p.page && p.mapped.empty()) return;
+  Device &d = c->devs[0];
+  (void)hipSetDevice(d.hip_id);
+  if (p.ready) {
+    // Every rank's streams must be done with this rank's memory (and this
+    // rank with theirs) before any arena goes: drain, then meet the others
+    // on the page (at most 60 s: a rank that died never arrives).
+    for (hipStream_t s : {d.stream, d.comm_stream, d.a_stream, d.a_stream2})
+      if (s) (void)hipStreamSynchronize(s);
+    *host_word(c, p.me, kIpcDone, 0) = 1;
+    __atomic_thread_fence(__ATOMIC_SEQ_CST);
+    const auto t0 = std::chrono::steady_clock::now();
+    for (int h = 0; h < c->G; ++h)
+      while (*host_word(c, h, kIpcDone, 0) == 0 &&
+             std::chrono::steady_clock::now() - t0 < std::chrono::seconds(60))
+        sched_yield();
+  }
+  for (char *m : p.mapped)
+    if (m) (void)hipIpcCloseMemHandle(m);
+  p.mapped.clear();
+  if (p.page) {
+    release_flags(c);
+    (void)hipHostUnregister(p.page);
+    munmap(p.page, p.page_bytes);
+    if (p.owner) shm_unlink(p.shm_name);
+  }
+  p.page = nullptr;
+  p.dpage = nullptr;
+  p.ready = false;
+}
+
 // Float4s per device shard of a peer-read bucket of `len4` float4s: whole
 // kPadFloat4 units, so a wave's float4s never straddle two owners.
 inline int64_t peer_shard4(int64_t len4, int G) {
@@ -182,6 +350,12 @@ struct SplitStep {
   bool mom;
   int64_t b4 = 0, nb = 0, wait_stride = 1;
   bool pipelined = false, cross = false, rsag = false, peer = false, ocheck = false, spans = false;
+  // The peer-read form with one process per GPU: the other ranks are
+  // reached through cbx_context::PeerIpc, ordered by its flag page at this
+  // step's sequence number `seq` (ipc_started: flags of this step may have
+  // been enqueued, so a failure must release the other ranks).
+  bool ipc = false, ipc_started = false;
+  uint64_t seq = 0;
   unsigned long long foreign = 0;
   std::vector<char> join;
   // Peer-read steps enqueued by one thread per device: device k's count of
@@ -217,6 +391,32 @@ struct SplitStep {
   hipEvent_t ev_red(size_t k, int64_t b) {
     if (peer && !pipelined) return c->devs[k].peer_r;
     return spans ? tr[k].slot->red[b] : c->devs[k].bucket_red[b];
+  }
+
+  // The peer-read form's participants: the local devices (one process,
+  // ordered by events) or every rank (one process per GPU, ordered by the
+  // flag page); pg(k) is local device k's index among them.
+  int pn() const { return ipc ? c->G : (int)c->devs.size(); }
+  int pg(size_t k) const { return ipc ? c->ipc.me : (int)k; }
+  const cbx::v4f *p_acc(int h) const {
+    return ipc ? c->ipc.acc[h] : reinterpret_cast<const cbx::v4f *>(base_dev(c, c->devs[h], CBX_BUF_GRADIENT));
+  }
+  const float *p_acc_ctrl(int h) const { return ipc ? c->ipc.acc_ctrl[h] : base_ctrl(c->devs[h], CBX_BUF_GRADIENT); }
+  const cbx::v4f *p_D(int h) const {
+    return ipc ? c->ipc.D[h] : reinterpret_cast<const cbx::v4f *>(base_dev(c, c->devs[h], CBX_BUF_DIFF));
+  }
+  // One process per GPU: this rank's flag of bucket b says "done" once the
+  // work queued before it on `st` is; a wait holds `st` until rank h's flag
+  // has reached this step.
+  int put_flag(hipStream_t st, int kind, int64_t b) {
+    if (ipc) HIP_TRY(hipStreamWriteValue64(st, c->ipc.dpage + ipc_word(c->ipc.me, kind, b), seq, 0));
+    return CBX_OK;
+  }
+  int wait_flags(hipStream_t st, int kind, int64_t b) {
+    for (int h = 0; ipc && !c->fault_skip_peer_wait && h < c->G; ++h)
+      if (h != c->ipc.me)
+        HIP_TRY(hipStreamWaitValue64(st, c->ipc.dpage + ipc_word(h, kind, b), seq, hipStreamWaitValueGte, ~0ull));
+    return CBX_OK;
   }
 
   // Peer-read, threaded: publish that device k's event of bucket b is
@@ -321,6 +521,17 @@ struct SplitStep {
     cross = pipelined && c->pipeline_mode == 1;
     rsag = c->allreduce_algo == CBX_ALLREDUCE_RSAG;
     peer = c->allreduce_algo == CBX_ALLREDUCE_PEER && c->G > 1;
+    ipc = peer && c->per_rank;
+    if (ipc) {
+      if (!c->ipc.ready || c->ipc.broken)
+        return fail(CBX_ERR_STATE, c->ipc.broken ? "the per-rank peer-read form failed part-way earlier (flags released)"
+                                                 : "the per-rank peer-read form needs cbx_peer_import");
+      if (nb > kIpcMaxBuckets)
+        return fail(CBX_ERR_UNSUPPORTED, "the per-rank peer-read form takes at most %lld buckets (%lld asked)",
+                    (long long)kIpcMaxBuckets, (long long)nb);
+      seq = ++c->ipc.seq;
+      ipc_started = true;
+    }
     if (peer && threaded(c)) {
       a_seq.reset(new std::atomic<int64_t>[c->devs.size()]);
       r_seq.reset(new std::atomic<int64_t>[c->devs.size()]);
@@ -432,13 +643,21 @@ struct SplitStep {
           HIP_TRY(cbx::launch_delay(st, (uint64_t)khz / 2));
         }
       }
+      if (ipc && c->fault_skip_peer_wait && c->ipc.me != 0) {
+        // Fault injection: this rank's kernel A starts 2 ms late, so a rank
+        // that skips its flag waits reads acc before it is written.
+        int khz = 0;
+        HIP_TRY(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, d.hip_id));
+        HIP_TRY(cbx::launch_delay(st, (uint64_t)khz * 2));
+      }
       if (ocheck) {
         Device::OrderStep &o = d.ord[d.ord_cur];
         HIP_TRY(cbx::launch_order_probe(st, {nullptr, o.pa[b]}));
         o.a1[b] = t.stop;  // with timing on, A always carries a stop event (the pool's or the ring's)
       }
       HIP_TRY(cbx::launch_sma_accumulate(offset_args(args[k], start_of(b), len_of(b)), b == 0, cfg, st, t));
-      if (peer && !pipelined) HIP_TRY(hipEventRecord(d.peer_a, st));  // the other devices' R waits on it
+      if (peer && !pipelined && !ipc) HIP_TRY(hipEventRecord(d.peer_a, st));  // the other devices' R waits on it
+      TRY(put_flag(st, kIpcA, b));  // one process per GPU: the other ranks' R waits on it
       if (spans) tr[k].slot->a_used[b] = t.stop;
       note_dispatch(k, si, Device::SPAN_A, t.stop, b == 0 ? t.start : nullptr);
       publish(a_seq, k, b);
@@ -464,12 +683,14 @@ struct SplitStep {
       for (size_t k = k0; k < k1; ++k) {
         Device &d = c->devs[k];
         HIP_TRY(hipSetDevice(d.hip_id));
-        for (int64_t a = wait_acc; a >= wait_from && a > wait_acc - streams; --a)
+        for (int64_t a = wait_acc; a >= wait_from && a > wait_acc - streams; --a) {
           for (size_t h = peer ? 0 : k; h < (peer ? c->devs.size() : k + 1); ++h) {
             hipEvent_t e = ev_a(h, a);
             HIP_TRY(hipStreamWaitEvent(d.comm_stream, e, 0));
             note_wait(k, 2, e);
           }
+          TRY(wait_flags(d.comm_stream, kIpcA, a));  // one process per GPU: every other rank's
+        }
       }
     } else if (peer && !on_comm) {
       // one bucket, in order on the sync stream: its own kernel A by stream
@@ -480,6 +701,7 @@ struct SplitStep {
         HIP_TRY(hipSetDevice(d.hip_id));
         for (size_t h = 0; h < c->devs.size(); ++h)
           if (h != k) HIP_TRY(hipStreamWaitEvent(d.stream, ev_a(h, b), 0));
+        TRY(wait_flags(d.stream, kIpcA, b));
       }
     }
     for (size_t k = k0; ocheck && k < k1; ++k) {
@@ -491,19 +713,19 @@ struct SplitStep {
       // Peer-read reduction R: device k sums shard k of the bucket from every
       // device's acc into its own D (device order from +0: the oracle's);
       // bucket 0 also sums the control blocks.
-      const int G = (int)c->devs.size();
+      const int G = pn();
       const int64_t sh4 = peer_shard4(len, G);
       for (size_t k = k0; k < k1; ++k) {
         Device &d = c->devs[k];
         HIP_TRY(hipSetDevice(d.hip_id));
-        const int64_t s0 = std::min<int64_t>((int64_t)k * sh4, len);
+        const int64_t s0 = std::min<int64_t>((int64_t)pg(k) * sh4, len);
         cbx::PeerArgs r;
         std::memset(&r, 0, sizeof(r));
         r.G = G;
         r.shard4 = sh4;
         for (int h = 0; h < G; ++h) {
-          r.acc[h] = reinterpret_cast<const cbx::v4f *>(base_dev(c, c->devs[h], CBX_BUF_GRADIENT)) + start + s0;
-          r.ctrl_in[h] = base_ctrl(c->devs[h], CBX_BUF_GRADIENT);
+          r.acc[h] = p_acc(h) + start + s0;
+          r.ctrl_in[h] = p_acc_ctrl(h);
         }
         r.out = reinterpret_cast<cbx::v4f *>(base_dev(c, d, CBX_BUF_DIFF)) + start + s0;
         r.ctrl_out = b == 0 ? base_ctrl(d, CBX_BUF_DIFF) : nullptr;
@@ -578,12 +800,14 @@ struct SplitStep {
         HIP_TRY(hipSetDevice(d.hip_id));
         HIP_TRY(hipEventRecord(ev_red(k, b), d.comm_stream));
         note_dispatch(k, 2, Device::SPAN_COLL, ev_red(k, b), nullptr);
+        TRY(put_flag(d.comm_stream, kIpcR, b));
       }
     } else if (peer) {
       for (size_t k = k0; k < k1; ++k) {  // the other devices' kernels B wait on it
         Device &d = c->devs[k];
         HIP_TRY(hipSetDevice(d.hip_id));
-        HIP_TRY(hipEventRecord(ev_red(k, b), d.stream));
+        if (ipc) TRY(put_flag(d.stream, kIpcR, b));
+        else HIP_TRY(hipEventRecord(ev_red(k, b), d.stream));
       }
     }
     for (size_t k = k0; k < k1; ++k) publish(r_seq, k, b);
@@ -605,6 +829,7 @@ struct SplitStep {
         HIP_TRY(hipStreamWaitEvent(d.stream, ev_red(h, b), 0));
         note_wait(k, 0, ev_red(h, b));
       }
+      TRY(wait_flags(d.stream, kIpcR, b));  // one process per GPU: every other rank's reduction
       cbx::LaunchConfig cfg = c->apply_cfg;
       cfg.num_cus = d.num_cus;
       cbx::Timing t;
@@ -630,10 +855,9 @@ struct SplitStep {
       if (peer) {
         cbx::PeerArgs p;
         std::memset(&p, 0, sizeof(p));
-        p.G = (int)c->devs.size();
+        p.G = pn();
         p.shard4 = peer_shard4(len_of(b), p.G);
-        for (int h = 0; h < p.G; ++h)
-          p.D[h] = reinterpret_cast<const cbx::v4f *>(base_dev(c, c->devs[h], CBX_BUF_DIFF)) + start_of(b);
+        for (int h = 0; h < p.G; ++h) p.D[h] = p_D(h) + start_of(b);
         HIP_TRY(cbx::launch_sma_peer_apply(a, p, mom, cfg, d.stream, t));
       } else {
         HIP_TRY(cbx::launch_sma_apply(a, mom && !rsag, cfg, d.stream, t));
@@ -729,7 +953,7 @@ int sma_step(cbx_context *c, int first) {
   }
 
   if (c->G > 1 ? c->allreduce_algo != CBX_ALLREDUCE_PEER : c->force_split) TRY(ensure_comms(c));
-  if (c->allreduce_algo == CBX_ALLREDUCE_PEER && c->G > 1) TRY(ensure_peer_access(c));
+  if (c->allreduce_algo == CBX_ALLREDUCE_PEER && c->G > 1 && !c->per_rank) TRY(ensure_peer_access(c));
   if (c->G == 1 && !c->force_split) {
     // Single GPU: Phase B is the identity, so A + C (+ D) fuse into one pass.
     // (sma.c:63 waits on base->updated; every producer of z is this stream,
@@ -754,6 +978,13 @@ int sma_step(cbx_context *c, int first) {
       for (Device &d : c->devs) {
         d.cross_valid = false;
         d.span_last = -1;
+      }
+      if (split.ipc_started) {
+        // and the other ranks may already wait on flags it will never write
+        const std::string msg = g_last_error;
+        release_flags(c);
+        c->ipc.broken = true;
+        g_last_error = msg;
       }
       return rc;
     }

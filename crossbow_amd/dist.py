@@ -70,6 +70,37 @@ def max_over_ranks(value: float, world: int) -> float:
     return float(t.item())
 
 
+def setup_peer(gpu, world: int) -> Optional[str]:
+    """One process per GPU: map every rank's buffers for the peer-read
+    all-reduce.  Every rank exports its handles (cbx_peer_export), the blobs
+    are all-gathered over the control group in rank order, and every rank
+    imports them (cbx_peer_import).  Returns None when every rank succeeded,
+    else why not; the ranks agree, so either all of them may use the form or
+    none does."""
+    if world <= 1:
+        return "one rank"
+    import torch.distributed as dist
+    why = None
+    blob = b""
+    try:
+        blob = gpu.peer_export()
+    except CbxError as e:
+        why = str(e)
+    blobs = [None] * world
+    dist.all_gather_object(blobs, blob)
+    if why is None:
+        if all(isinstance(b, (bytes, bytearray)) and b for b in blobs):
+            try:
+                gpu.peer_import([bytes(b) for b in blobs])
+            except CbxError as e:
+                why = str(e)
+        else:
+            why = "another rank could not export its handles"
+    if max_over_ranks(0.0 if why is None else 1.0, world) > 0.0:
+        return why or "failed on another rank"
+    return None
+
+
 @dataclass
 class Tuning:
     """What ``tune_buckets`` chose (already set on the context) and why."""
@@ -113,9 +144,10 @@ def tune_buckets(gpu, n: int, world: int, step: Callable[[], None], candidates=(
     where G divides 1024, reduce-scatter + base momentum on the rank's shard
     + all-gather, which moves the same link bytes in two collectives per
     bucket and saves kernel B's momentum pass on (G-1)/G of the model; with
-    one process over every device (``peer``) also the peer-read form at
-    ``peer_candidates`` buckets (``peer_only``: that form alone, e.g. when
-    RCCL refuses the device selection).  Then the all-reduce grouping of the
+    one process over every device, or per rank after ``setup_peer``
+    (``peer``), also the peer-read form at ``peer_candidates`` buckets
+    (``peer_only``: that form alone, e.g. when RCCL refuses the device
+    selection).  Then the all-reduce grouping of the
     winner (``gpu.set_allreduce_group``, 4-9 % in mode 0,
     profiles/r01/allreduce_group_ab.json) and, with ``threads`` (one process
     over several devices), the winner with one enqueue thread per device

@@ -422,9 +422,24 @@ class TheGPU:
         check(self._L.cbx_set_enqueue_threads(self._ctx, mode))
 
     def set_allreduce_algorithm(self, algorithm: int) -> None:
-        """ALLREDUCE_RCCL (default), ALLREDUCE_PEER (one process over every device: peer reads over xGMI,
-        bucketed like the all-reduce) or ALLREDUCE_RSAG (reduce-scatter, momentum on the shard, all-gather)."""
+        """ALLREDUCE_RCCL (default), ALLREDUCE_PEER (peer reads over xGMI, bucketed like the all-reduce: one
+        process over every device, or one process per GPU after peer_export / peer_import) or ALLREDUCE_RSAG
+        (reduce-scatter, momentum on the shard, all-gather)."""
         check(self._L.cbx_set_allreduce_algorithm(self._ctx, algorithm))
+
+    def peer_export(self) -> bytes:
+        """One process per GPU: this rank's IPC handles for the peer-read all-reduce (cbx_peer_export)."""
+        buf = ctypes.create_string_buffer(_lib.PEER_BLOB_BYTES)
+        n = ctypes.c_size_t(0)
+        check(self._L.cbx_peer_export(self._ctx, buf, ctypes.byref(n)))
+        return buf.raw[:n.value]
+
+    def peer_import(self, blobs: Sequence[bytes]) -> None:
+        """Every rank's peer_export() blob, in rank order (cbx_peer_import)."""
+        if any(len(b) != _lib.PEER_BLOB_BYTES for b in blobs):
+            raise CbxError(_lib.CBX_ERR_INVALID, "peer_import: every blob must be PEER_BLOB_BYTES long")
+        joined = b"".join(blobs)
+        check(self._L.cbx_peer_import(self._ctx, joined, len(blobs)))
 
     def set_staging_mode(self, mode: int) -> None:
         """synchronise_staged: STAGING_ZEROCOPY (kernels read / write the pinned mirror) or STAGING_DMA (copies)."""

@@ -384,9 +384,11 @@ int cbx_set_allreduce_group (cbx_context *ctx, int group);
 /* How the SMA step's all-reduce crosses devices (G > 1):
  *   CBX_ALLREDUCE_RCCL (0, default): grouped ncclAllReduce, bucketed and
  *     pipelined as configured above (synch/common.c:3-57);
- *   CBX_ALLREDUCE_PEER (1): one process over every device only (cbx_init
- *     with G devices).  No RCCL pass: after hipDeviceEnablePeerAccess,
- *     device g sums shard g of every device's acc by direct peer reads, then
+ *   CBX_ALLREDUCE_PEER (1): one process over every device (cbx_init with G
+ *     devices), or one process per GPU once cbx_peer_import has mapped every
+ *     rank's buffers (below).  No RCCL pass: after hipDeviceEnablePeerAccess
+ *     (or the IPC mapping), device g sums shard g of every device's acc by
+ *     direct peer reads, then
  *     kernel B on each device reads every shard of D from its owner
  *     (two-shot over all xGMI links at once; the reference's non-NCCL path
  *     copies peer buffers, common.c:64-95).  Bucketed and pipelined like
@@ -405,11 +407,37 @@ int cbx_set_allreduce_group (cbx_context *ctx, int group);
  *     with the same z and last (SURVEY 8(e) variant 1).  G must divide 1024
  *     (powers of two up to 16).  The host-staged step and S-SGD keep the
  *     all-reduce.
- * CBX_ERR_UNSUPPORTED for PEER on a one-process-per-GPU context.          */
+ * CBX_ERR_STATE for PEER on a one-process-per-GPU context before
+ * cbx_peer_import.                                                         */
 #define CBX_ALLREDUCE_RCCL 0
 #define CBX_ALLREDUCE_PEER 1
 #define CBX_ALLREDUCE_RSAG 2
 int cbx_set_allreduce_algorithm (cbx_context *ctx, int algorithm);
+/* The peer-read all-reduce with one process per GPU (cbx_init_rank, G > 1;
+ * no reference counterpart: the reference runs one process over every GPU,
+ * executioncontext.c:185-201, and its non-NCCL path copies peer buffers,
+ * common.c:64-95).  After cbx_set_model_manager on every rank:
+ *   1. cbx_peer_export(ctx, blob, &bytes) writes this rank's handles into
+ *      `blob` (CBX_PEER_BLOB_BYTES): its model arena's IPC handle
+ *      (hipIpcGetMemHandle) and where acc and D sit in it; rank 0 also
+ *      creates the page of completion flags (POSIX shared memory) and names
+ *      it in its blob;
+ *   2. the caller gathers every rank's blob, in rank order, over its own
+ *      control plane (bench.py: gloo all_gather);
+ *   3. cbx_peer_import(ctx, blobs, nranks) maps every other rank's arena
+ *      (hipIpcOpenMemHandle) and pins the flag page (hipHostRegister).
+ * Then CBX_ALLREDUCE_PEER is accepted.  The ranks' streams order each
+ * other through the flags: a rank writes the step's sequence number after
+ * its kernel A / reduction of a bucket (hipStreamWriteValue64), the others
+ * wait for it (hipStreamWaitValue64 >=); the pipeline, its modes, strides,
+ * groups and the sums' device order are the single-process form's.  Same
+ * results bit for bit.  At most 4096 buckets.  cbx_free then waits (up to
+ * 60 s) until every rank is done with this rank's memory.  Every rank calls
+ * export, import and free; a step that fails part-way releases the other
+ * ranks' waits and leaves the form unusable (CBX_ERR_STATE).             */
+#define CBX_PEER_BLOB_BYTES 256
+int cbx_peer_export (cbx_context *ctx, void *blob, size_t *bytes);
+int cbx_peer_import (cbx_context *ctx, const void *blobs, int nranks);
 /* How cbx_synchronise_staged moves the model between the pinned host mirror
  * and the device (north_star: the path starts and ends in host memory):
  *   CBX_STAGING_ZEROCOPY (0, default): the SMA kernels read their inputs

@@ -184,14 +184,18 @@ def setup_model(g: Ctx, A, n: int, R: int, mom: float, utype: int, sync: int, wp
     g("cbx_set_model_manager", R, sync)
 
 
-def run_case(g: Ctx, world: int, local: List[int], case: Case) -> dict:
+def run_case(g: Ctx, world: int, local: List[int], case: Case, after_setup=None) -> dict:
     """One case on the devices `local` of a G = `world` job.  Returns
-    {"bad": [...], "digest": {device: sha of z and last}, "differs": n}."""
+    {"bad": [...], "digest": {device: sha of z and last}, "differs": n}.
+    `after_setup(g)` runs once the model manager exists (the per-rank
+    peer-read form maps the other ranks' buffers there)."""
     O = oracle()
     A = g.A
     n, R, mom = case.n, case.R, case.mom
     wpc = 2 * world * R
     setup_model(g, A, n, R, mom, case.utype, A.SYNC_SSP if case.held else A.SYNC_BSP, wpc)
+    if after_setup:
+        after_setup(g)
     if case.bucket:
         g("cbx_set_bucket_elements", ctypes.c_longlong(case.bucket))
     g("cbx_set_pipeline_mode", case.mode)
@@ -285,17 +289,20 @@ def run_case(g: Ctx, world: int, local: List[int], case: Case) -> dict:
     return {"bad": check.bad, "digest": dig, "differs": check.differs}
 
 
-def run_golden(g: Ctx, world: int, local: List[int], gcase: dict, algo: int = 0, exact: bool = True) -> List[str]:
+def run_golden(g: Ctx, world: int, local: List[int], gcase: dict, algo: int = 0, exact: bool = True,
+               after_setup=None) -> List[str]:
     """One committed fixture (tests/golden/, G = world): one step, bit for bit
     (or, with `exact` False, within the G > 1 tolerance: real RCCL's order)."""
     A = g.A
-    if algo:
-        g("cbx_set_allreduce_algorithm", algo)
     st = gcase["state"]
     n = st.n
     R = st.size // st.G
     held = [int(i) for i in np.nonzero(st.locked == 0)[0]]
     setup_model(g, A, n, R, st.momentum, 7, A.SYNC_SSP if held else A.SYNC_BSP, 2 * st.size, alpha=st.alpha)
+    if after_setup:
+        after_setup(g)
+    if algo:
+        g("cbx_set_allreduce_algorithm", algo)
     mine = [i for i in range(st.size) if i % world in local]
     for d in local:
         g.write("cbx_base_write", d, A.BUF_DATA, st.z[d])

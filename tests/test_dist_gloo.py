@@ -353,3 +353,73 @@ def test_bucket_tuning_drops_a_failing_candidate_on_every_rank():
     assert "injected failure" in r1[6]["4/0"] and r0[6]["4/0"] == "failed on another rank"
     assert threads in (0, 1) and set_threads == threads
     assert (nb, mode) != (4, 0)
+
+
+class _FakePeerGpu:
+    """Stands in for TheGPU in dist.setup_peer: export returns a rank-stamped
+    blob (or fails), import records what it was handed (or fails)."""
+
+    def __init__(self, rank, fail=None):
+        self.rank, self.fail, self.imported = rank, fail, None
+
+    def peer_export(self):
+        from crossbow_amd._abi import PEER_BLOB_BYTES, CbxError
+        if self.fail == "export":
+            raise CbxError(-8, f"injected export failure on rank {self.rank}")
+        return bytes([self.rank + 1]) * PEER_BLOB_BYTES
+
+    def peer_import(self, blobs):
+        from crossbow_amd._abi import CbxError
+        if self.fail == "import":
+            raise CbxError(-3, f"injected import failure on rank {self.rank}")
+        self.imported = [b[0] for b in blobs]
+
+
+def _peer_main(rank, world, port, fail_rank, fail, q):
+    import sys
+    sys.path.insert(0, ROOT)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    try:
+        from crossbow_amd import dist as D
+        D.init(world, rank, backend="gloo")
+        g = _FakePeerGpu(rank, fail if rank == fail_rank else None)
+        why = D.setup_peer(g, world)
+        q.put((rank, (why, g.imported), None))
+        D.finalize(world)
+    except Exception:  # pragma: no cover
+        import traceback
+        q.put((rank, None, traceback.format_exc()))
+
+
+@pytest.mark.parametrize("fail_rank,fail", [(None, None), (1, "export"), (0, "import")])
+def test_peer_ipc_setup_gathers_in_rank_order_and_agrees(fail_rank, fail):
+    # dist.setup_peer: every rank imports every rank's blob in rank order;
+    # a failure on ONE rank (its export or its import) makes every rank
+    # report it, so no rank ever runs the peer-read form alone.
+    import torch.multiprocessing as mp
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_peer_main, args=(r, world, port, fail_rank, fail, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = {}
+    try:
+        for _ in range(world):
+            rank, res, err = q.get(timeout=240)
+            out[rank] = (res, err)
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
+    for rank in range(world):
+        assert out[rank][1] is None, out[rank][1]
+    (why0, imp0), (why1, imp1) = out[0][0], out[1][0]
+    if fail is None:
+        assert why0 is None and why1 is None
+        assert imp0 == imp1 == [1, 2]  # rank order
+    else:
+        assert why0 and why1, (why0, why1)
+        assert f"injected {fail} failure" in (why0 if fail_rank == 0 else why1)

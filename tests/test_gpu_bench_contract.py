@@ -55,6 +55,7 @@ def test_bench_two_ranks_through_the_launcher_prints_one_json_line():
     _check(d, 2)
     assert d["config"]["parallelism"] == "sma-dp2" and "allreduce" in d and "rehearsal" in d
     assert d["config"]["process_form"] == "per-rank"
+    assert d["config"]["peer_ipc"] == "mapped"  # the peer-read form's IPC mapping worked on both ranks
     # N > 1: the roofline of the kernels as they ran in the timed region
     # (summed busy spans beside the collectives), the calibration's apart
     r = d["roofline"]

@@ -1,0 +1,225 @@
+"""The peer-read all-reduce with ONE PROCESS PER GPU (cbx_peer_export /
+cbx_peer_import), G = 2, 4, 8 rank processes on ONE GPU, the real library.
+
+Each rank maps every other rank's model arena through its IPC handle
+(hipIpcOpenMemHandle, dmabuf) and pins rank 0's page of completion flags
+(POSIX shared memory); the ranks' streams then order each other through the
+flags (hipStreamWriteValue64 after kernel A / the reduction of a bucket,
+hipStreamWaitValue64 >= this step's sequence number before reading another
+rank's acc or D).  Each rank also holds a real RCCL communicator
+(cbx_init_rank, sockets over loopback as in test_gpu_realrccl.py), which the
+peer form never uses.
+
+The reduction sums in rank order from +0, the oracle's order, so every case
+is bit for bit against the oracle with the same G and the committed G > 1
+golden fixtures, and z / last are identical on every rank.  Also: the
+stream-order check with the form, a randomised run that switches between it,
+the all-reduce and the reduce-scatter form between steps, C4 at the full
+ResNet-50 size, and a fault-injection run that drops the flag waits
+($CBX_FAULT_SKIP_PEER_WAIT, with every rank but 0 starting its kernels A 2 ms
+late) and must then come out WRONG, so the waits are known to be what keeps
+it right.  Every "device" is device 0: this pins the algorithm and the
+cross-process ordering, not xGMI speed.
+"""
+from __future__ import annotations
+
+import ctypes
+import dataclasses
+import os
+import tempfile
+
+import numpy as np
+import pytest
+
+from tests import multidev_common as C
+from tests.test_gpu_multirank import CASES, N_RESNET50
+from tests.test_gpu_realrccl import _spawn, load_real, rank_env, run_order, run_random, share_uid
+
+pytestmark = pytest.mark.gpu
+
+PEER = 1
+
+
+def exchange(g, rank: int, world: int, d: str, tag: str) -> None:
+    """cbx_peer_export on every rank, the blobs through files, cbx_peer_import."""
+    buf = ctypes.create_string_buffer(g.A.PEER_BLOB_BYTES)
+    n = ctypes.c_size_t(0)
+    g("cbx_peer_export", buf, ctypes.byref(n))
+    assert n.value == g.A.PEER_BLOB_BYTES
+    path = os.path.join(d, f"peer_{tag}_{rank}.bin")
+    with open(path + ".tmp", "wb") as f:
+        f.write(buf.raw)
+    os.replace(path + ".tmp", path)
+    paths = [os.path.join(d, f"peer_{tag}_{r}.bin") for r in range(world)]
+    C.wait_files(paths)
+    blobs = b"".join(open(p, "rb").read() for p in paths)
+    g("cbx_peer_import", blobs, world)
+
+
+def _cases(world):
+    names = {2: ("sma", "sma-copy-ssp", "sma-5-buckets", "sma-5-buckets-cross", "sma-5-buckets-cross-stride",
+                 "sma-no-momentum"),
+             4: ("sma-copy-ssp", "sma-5-buckets", "sma-5-buckets-cross-stride"),
+             8: ("sma-copy-ssp", "sma-5-buckets-cross-stride")}[world]
+    return [dataclasses.replace(c, name=c.name + "-peer", algo=PEER, order="rank") for c in CASES if c.name in names]
+
+
+def _jobs(world):
+    jobs = [("case", c.name) for c in _cases(world)]
+    jobs += [("golden", gc["name"]) for gc in C.golden_cases(world)]
+    jobs += [("order", "order-peer")]
+    if world <= 4:
+        jobs += [("random", "random-peer-rccl-rsag")]
+    return jobs
+
+
+def _rank_main(rank, world, jobs, d, q):
+    rank_env(rank)
+    try:
+        L, A = load_real()
+        cases = {c.name: c for c in _cases(world)}
+        goldens = {gc["name"]: gc for gc in C.golden_cases(world)}
+        out = []
+        for j, (kind, name) in enumerate(jobs):
+            g = C.init_rank(L, A, rank, world, share_uid(L, rank, os.path.join(d, f"uid_{j}")))
+            hook = lambda g_, j=j: exchange(g_, rank, world, d, str(j))  # noqa: E731
+            try:
+                if kind == "case":
+                    res = C.run_case(g, world, [rank], cases[name], after_setup=hook)
+                elif kind == "golden":
+                    res = {"bad": C.run_golden(g, world, [rank], goldens[name], algo=PEER, after_setup=hook)}
+                elif kind == "order":
+                    res = {"bad": run_order(g, world, PEER, after_setup=hook)}
+                else:
+                    bad, dig, differs = run_random(g, world, rank, steps=30, algos=(0, 1, 1, 2), after_setup=hook)
+                    res = {"bad": bad, "digest": {rank: dig}, "differs": differs}
+            finally:
+                g.free()
+            out.append((name, res))
+        q.put((rank, out, None))
+    except Exception:  # pragma: no cover - reported to the parent
+        import traceback
+        q.put((rank, None, traceback.format_exc()))
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_peer_read_one_process_per_gpu_vs_oracle(world):
+    jobs = _jobs(world)
+    with tempfile.TemporaryDirectory(dir=C.loopback_dir()) as d:
+        res = _spawn(world, _rank_main, lambda r: (r, world, jobs, d), timeout=280)
+    for rank in range(world):
+        assert [name for name, _ in res[rank]] == [name for _, name in jobs]
+        failures = [(name, r["bad"]) for name, r in res[rank] if r["bad"]]
+        assert not failures, f"rank {rank}: {failures}"
+    for j, (kind, name) in enumerate(jobs):
+        if kind not in ("case", "random"):
+            continue
+        digests = {res[r][j][1]["digest"][r] for r in range(world)}
+        assert len(digests) == 1, f"{name}: z / last differ across ranks"
+        if kind == "case":  # rank-order sums: the oracle's, bit for bit
+            assert all(res[r][j][1]["differs"] == 0 for r in range(world)), name
+
+
+def _fault_main(rank, world, fault, d, q):
+    rank_env(rank)
+    if fault:
+        os.environ["CBX_FAULT_SKIP_PEER_WAIT"] = "1"  # read at context creation
+    try:
+        L, A = load_real()
+        g = C.init_rank(L, A, rank, world, share_uid(L, rank, os.path.join(d, "uid")))
+        try:
+            case = dataclasses.replace(next(c for c in CASES if c.name == "sma-5-buckets"), algo=PEER)
+            res = C.run_case(g, world, [rank], case, after_setup=lambda g_: exchange(g_, rank, world, d, "f"))
+        finally:
+            g.free()
+        q.put((rank, res, None))
+    except Exception:  # pragma: no cover - reported to the parent
+        import traceback
+        q.put((rank, None, traceback.format_exc()))
+
+
+@pytest.mark.timeout(200)
+@pytest.mark.parametrize("fault", [True, False])
+def test_peer_read_flag_waits_are_what_orders_the_ranks(fault):
+    # With the waits dropped and rank 1's kernels A started 2 ms late, rank 0
+    # reduces rank 1's acc before it is written: the result must be wrong.
+    # The same run with the waits is bit for bit against the oracle.
+    world = 2
+    with tempfile.TemporaryDirectory(dir=C.loopback_dir()) as d:
+        res = _spawn(world, _fault_main, lambda r: (r, world, fault, d), timeout=180)
+    if fault:
+        assert any(res[r]["bad"] for r in range(world)), "the race went unseen: the fault switch did nothing"
+    else:
+        assert not any(res[r]["bad"] for r in range(world)), [res[r]["bad"] for r in range(world)]
+        assert len({res[r]["digest"][r] for r in range(world)}) == 1
+
+
+def _full_size_main(rank, world, R, steps, d, q):
+    rank_env(rank)
+    try:
+        L, A = load_real()
+        O = C.oracle()
+        g = C.init_rank(L, A, rank, world, share_uid(L, rank, os.path.join(d, "uid")))
+        try:
+            n = N_RESNET50
+            C.setup_model(g, A, n, R, 0.9, 7, A.SYNC_BSP, 2 * world * R)
+            exchange(g, rank, world, d, "full")
+            g("cbx_set_pipeline_mode", 1)
+            g("cbx_set_allreduce_algorithm", PEER)
+            g("cbx_fill_synthetic", O.SEED)
+            size = world * R
+            mine = [i for i in range(size) if i % world == rank]
+            rng = np.random.default_rng(12)
+            idx = np.unique(np.concatenate([rng.integers(0, n, 60_000), np.arange(4), np.arange(n - 4, n),
+                                            np.arange(6_389_000, 6_391_000)]))  # across the 4 ranks' shards
+            z0 = g.read("cbx_base_read", rank, A.BUF_DATA, n)[idx]
+            l0 = g.read("cbx_base_read", rank, A.BUF_LAST, n)[idx]
+            s0 = np.stack([g.read("cbx_replica_read", i, A.BUF_DIFF, n)[idx] for i in mine])
+            w0 = np.stack([g.read("cbx_replica_read", i, A.BUF_DATA, n)[idx] for i in mine])
+            tmp = os.path.join(d, f"in_{rank}.tmp.npz")
+            np.savez(tmp, z=z0, last=l0, s=s0, w=w0, ids=np.array(mine))
+            os.replace(tmp, os.path.join(d, f"in_{rank}.npz"))
+            for step in range(steps):
+                g("cbx_lock_any")
+                g("cbx_synchronise", 0, step + 1, 0, 0)
+                g("cbx_unlock_any")
+            g("cbx_wait")
+            z1 = g.read("cbx_base_read", rank, A.BUF_DATA, n)
+            l1 = g.read("cbx_base_read", rank, A.BUF_LAST, n)
+            dig = C.digest(z1, l1)
+            w1 = {i: g.read("cbx_replica_read", i, A.BUF_DATA, n)[idx] for i in mine}
+        finally:
+            g.free()
+        C.wait_files([os.path.join(d, f"in_{r}.npz") for r in range(world)])
+        ins = [np.load(os.path.join(d, f"in_{r}.npz")) for r in range(world)]
+        s, w = [None] * size, [None] * size
+        for f in ins:
+            for k, i in enumerate(f["ids"]):
+                s[int(i)], w[int(i)] = f["s"][k].copy(), f["w"][k].copy()
+        st = O.SmaState(world, size, idx.size, 0.1, 0.9, [f["z"].copy() for f in ins],
+                        [f["last"].copy() for f in ins], s, w)
+        for _ in range(steps):
+            O.sma_step(st)
+        check = C.Checker(exact=True)
+        check("z sample", z1[idx], st.z[rank])
+        check("last sample", l1[idx], st.last[rank])
+        for i in mine:
+            check(f"w[{i}] sample", w1[i], st.w[i])
+        q.put((rank, {"bad": check.bad, "digest": dig}, None))
+    except Exception:  # pragma: no cover - reported to the parent
+        import traceback
+        q.put((rank, None, traceback.format_exc()))
+
+
+@pytest.mark.timeout(300)
+def test_peer_read_one_process_per_gpu_resnet50_c4():
+    # C4 (2 replicas/GPU x 4) at the full ResNet-50 size, cross-step pipeline,
+    # 8 buckets (the library default at G > 1): sampled bit for bit, z and
+    # last identical on every rank.
+    world, R = 4, 2
+    with tempfile.TemporaryDirectory(dir=C.loopback_dir(1 << 30)) as d:
+        res = _spawn(world, _full_size_main, lambda r: (r, world, R, 3, d), timeout=280)
+    for r in range(world):
+        assert not res[r]["bad"], f"rank {r}: {res[r]['bad']}"
+    assert len({res[r]["digest"] for r in range(world)}) == 1, "z / last differ across ranks at full size"

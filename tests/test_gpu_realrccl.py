@@ -82,7 +82,7 @@ def _jobs(world):
     return jobs + [("bn", "bn"), ("autotune", "autotune")]
 
 
-def run_random(g, world, rank, steps=40):
+def run_random(g, world, rank, steps=40, algos=(0, 2), after_setup=None):
     """A long randomised run under real RCCL: every few steps the bucket size,
     pipeline mode, wait stride, all-reduce group or the collective's form
     changes (the same choice on every rank, from a shared seed), replicas
@@ -94,6 +94,8 @@ def run_random(g, world, rank, steps=40):
     A = g.A
     n, R = 200_003, 2
     C.setup_model(g, A, n, R, 0.9, 7, A.SYNC_SSP, 4 * world)
+    if after_setup:
+        after_setup(g)
     g("cbx_set_order_check", 1)
     size = world * R
     mine = [i for i in range(size) if i % world == rank]
@@ -126,7 +128,7 @@ def run_random(g, world, rank, steps=40):
             g("cbx_set_cross_wait_stride", rng.choice([1, 2, 3]))
             g("cbx_set_allreduce_group", rng.choice([1, 2, 4]))
         elif u < 0.5:
-            g("cbx_set_allreduce_algorithm", rng.choice([0, 2]))
+            g("cbx_set_allreduce_algorithm", rng.choice(list(algos)))
         elif u < 0.55:
             i = rng.randrange(size)
             new = O.fill_normal(n, 7000 + step, 0.05)
@@ -152,13 +154,15 @@ def run_random(g, world, rank, steps=40):
     return bad + check.bad, C.digest(z, last), check.differs
 
 
-def run_order(g, world, algo):
+def run_order(g, world, algo, after_setup=None):
     """The stream-order check (cbx_set_order_check) under real RCCL, whose
     collective runs asynchronously beside kernels A and B: bucketed, cross-step
     pipeline with wait stride 2 and all-reduce groups of 2, checked after every
     two back-to-back steps."""
     A = g.A
     C.setup_model(g, A, 300_007, 2, 0.9, 7, A.SYNC_BSP, 4 * world)
+    if after_setup:
+        after_setup(g)
     g("cbx_set_bucket_elements", ctypes.c_longlong(65_536))
     g("cbx_set_pipeline_mode", 1)
     g("cbx_set_cross_wait_stride", 2)
