@@ -375,6 +375,12 @@ struct Device {
   // Arena: [base data][base gradient(ctrl+acc)][base diff(ctrl+D)][base last]
   //        then per replica [data][diff][last][gradient].
   char *arena = nullptr;
+  // The base model's acc (gradient) and D (diff) slots in allocations of
+  // their own, once cbx_peer_export has run (one process per GPU): the other
+  // ranks map exactly these two through IPC handles, not the whole arena (an
+  // IPC open of a 2 GB allocation hung under HIP 7.0).  Null:
+  // the arena's slots 1 and 2.
+  char *xslot[2] = {nullptr, nullptr};
   char *host = nullptr;  // pinned mirror, same layout (lazy)
   size_t arena_bytes = 0;
   size_t stride = 0;  // bytes per buffer slot
@@ -522,8 +528,8 @@ struct cbx_context {
   int enqueue_threads = -1;
   std::unique_ptr<cbx::host::EnqueuePool> pool;
   // The peer-read all-reduce with one process per GPU (cbx_peer_export /
-  // cbx_peer_import, sync_steps.hip): every other rank's acc and D mapped
-  // here through its arena's IPC handle, and one page of completion flags in
+  // cbx_peer_import, sync_steps.hip): every other rank's acc and D slots
+  // (Device::xslot) mapped here through IPC handles, and one page of completion flags in
   // POSIX shared memory that every rank pins (hipHostRegister).  Rank h
   // writes its flags from its streams (hipStreamWriteValue64: the step's
   // sequence number once kernel A / the reduction of a bucket is done); the
@@ -534,7 +540,7 @@ struct cbx_context {
     bool ready = false;
     bool broken = false;                  // a step failed part-way: the flags were released
     int me = 0;
-    std::vector<char *> mapped;           // per rank: its arena opened here (own: nullptr)
+    std::vector<char *> mapped;           // 2 per rank: its acc and D slots opened here (own: nullptr)
     std::vector<const cbx::v4f *> acc;    // per rank: acc data (own: the local arena's)
     std::vector<const float *> acc_ctrl;  // per rank: acc control block
     std::vector<const cbx::v4f *> D;      // per rank: D data
@@ -611,13 +617,20 @@ inline float *slot_ptr(char *arena, const Device &d, size_t slot, bool ctrl) {
 
 inline bool base_has(const cbx_context *c, int kind) { return kind != CBX_BUF_LAST || c->has_last; }
 
+// A base-model slot: in the arena, or (acc / D after cbx_peer_export) in its own allocation.
+inline char *base_slot(const Device &d, int kind) {
+  const size_t s = slot_index_base(kind);
+  if ((s == 1 || s == 2) && d.xslot[s - 1]) return d.xslot[s - 1];
+  return d.arena + s * d.stride;
+}
+
 inline float *base_dev(const cbx_context *c, const Device &d, int kind) {
   const bool ctrl = (kind == CBX_BUF_GRADIENT || kind == CBX_BUF_DIFF);
-  return slot_ptr(d.arena, d, slot_index_base(kind), ctrl);
+  return reinterpret_cast<float *>(base_slot(d, kind) + data_offset(ctrl));
 }
 
 inline float *base_ctrl(const Device &d, int kind) {
-  return reinterpret_cast<float *>(d.arena + slot_index_base(kind) * d.stride);
+  return reinterpret_cast<float *>(base_slot(d, kind));
 }
 
 inline size_t replica_kind_index(int kind) { return slot_index_replica(0, kind) - kBaseSlots; }
@@ -766,6 +779,8 @@ inline void close_device(Device &d) {
   if (d.comm_stream) (void)hipStreamSynchronize(d.comm_stream);
   if (d.comm) (void)ncclCommDestroy(d.comm);
   if (d.arena) (void)hipFree(d.arena);
+  for (char *&x : d.xslot)
+    if (x) (void)hipFree(x);
   for (char *p : d.extra)
     if (p) (void)hipFree(p);
   for (char *p : d.extra_host)
@@ -1002,10 +1017,15 @@ void peer_close(cbx_context *c);
 // other rank's stream waits forever.
 constexpr int64_t kIpcMaxBuckets = 4096;
 constexpr size_t kIpcRankWords = 2 * kIpcMaxBuckets + 64;  // a[], r[], done + padding (512 B)
-constexpr int kIpcA = 0, kIpcR = 1, kIpcDone = 2;
+constexpr int kIpcA = 0, kIpcR = 1, kIpcDone = 2, kIpcOpened = 3;  // kIpcOpened: this rank's imports are done
 constexpr uint64_t kIpcRelease = 1ull << 62;
+// The largest buffer the per-rank peer-read form maps: IPC opens of 512 MB
+// allocations worked under HIP 7.0 (torch's runtime) on MI355X, of 2 GB ones
+// hung (scripts/ipc_torch_probe.py).  ResNet-50's acc is 102 MB.
+constexpr size_t kIpcMaxSlotBytes = 512ull << 20;
 inline size_t ipc_word(int rank, int kind, int64_t b) {
-  return (size_t)rank * kIpcRankWords + (kind == kIpcDone ? 2 * kIpcMaxBuckets : (size_t)kind * kIpcMaxBuckets + b);
+  return (size_t)rank * kIpcRankWords +
+         (kind >= kIpcDone ? 2 * kIpcMaxBuckets + (size_t)(kind - kIpcDone) : (size_t)kind * kIpcMaxBuckets + b);
 }
 
 }  // namespace cbx::host

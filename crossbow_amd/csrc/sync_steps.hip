@@ -157,9 +157,9 @@ struct PeerBlob {
   uint32_t magic;
   int32_t rank, G, pad;
   int64_t n4;
-  uint64_t acc_off, acc_ctrl_off, d_off;  // from the arena's base
-  hipIpcMemHandle_t arena;
-  char shm[64];  // rank 0's: the flag page
+  uint64_t slot_bytes;
+  hipIpcMemHandle_t acc, D;  // the base model's acc and D slots (control block first)
+  char shm[64];              // rank 0's: the flag page
 };
 static_assert(sizeof(PeerBlob) <= CBX_PEER_BLOB_BYTES, "peer blob size");
 constexpr uint32_t kPeerMagic = 0x50584243u;  // "CBXP"
@@ -182,6 +182,15 @@ int map_flag_page(cbx_context *c, bool create) {
   HIP_TRY(hipHostRegister(p.page, p.page_bytes, hipHostRegisterMapped | hipHostRegisterPortable));
   HIP_TRY(hipHostGetDevicePointer(reinterpret_cast<void **>(&p.dpage), p.page, 0));
   return CBX_OK;
+}
+
+std::string fmt_msg(const char *f, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, f);
+  vsnprintf(buf, sizeof(buf), f, ap);
+  va_end(ap);
+  return buf;
 }
 
 volatile uint64_t *host_word(cbx_context *c, int rank, int kind, int64_t b) {
@@ -210,17 +219,38 @@ int peer_export(cbx_context *c, void *blob, size_t *bytes) {
                                            cbx::kMaxDevices);
   if (!blob || !bytes) return fail(CBX_ERR_INVALID, "cbx_peer_export: null blob");
   Device &d = c->devs[0];
+  if (d.stride > kIpcMaxSlotBytes)
+    return fail(CBX_ERR_UNSUPPORTED, "the per-rank peer-read form maps at most %zu MiB per buffer (%zu asked): an IPC "
+                "open of a 2 GB allocation hung under HIP 7.0", kIpcMaxSlotBytes >> 20, d.stride >> 20);
+  HIP_TRY(hipSetDevice(d.hip_id));
+  if (!d.xslot[0]) {
+    // acc and D move out of the arena into allocations of their own, which
+    // is all the other ranks map (contents kept: the step may be mid-run)
+    for (hipStream_t s : {d.stream, d.comm_stream, d.a_stream, d.a_stream2})
+      if (s) HIP_TRY(hipStreamSynchronize(s));
+    char *x[2] = {nullptr, nullptr};
+    for (int k = 0; k < 2; ++k) {
+      hipError_t e = hipMalloc(reinterpret_cast<void **>(&x[k]), d.stride);
+      if (e == hipSuccess) e = hipMemcpy(x[k], d.arena + (size_t)(k + 1) * d.stride, d.stride, hipMemcpyDeviceToDevice);
+      if (e != hipSuccess) {
+        for (char *p : x)
+          if (p) (void)hipFree(p);
+        return fail(CBX_ERR_HIP, "cbx_peer_export: the acc / D slots: %s", hipGetErrorString(e));
+      }
+    }
+    d.xslot[0] = x[0];
+    d.xslot[1] = x[1];
+    c->foreign_ops.fetch_add(1, std::memory_order_acq_rel);  // a cross-step pipeline rejoins
+  }
   PeerBlob pb;
   std::memset(&pb, 0, sizeof(pb));
   pb.magic = kPeerMagic;
   pb.rank = d.g;
   pb.G = c->G;
   pb.n4 = c->n4;
-  pb.acc_off = (uint64_t)(reinterpret_cast<char *>(base_dev(c, d, CBX_BUF_GRADIENT)) - d.arena);
-  pb.acc_ctrl_off = (uint64_t)(reinterpret_cast<char *>(base_ctrl(d, CBX_BUF_GRADIENT)) - d.arena);
-  pb.d_off = (uint64_t)(reinterpret_cast<char *>(base_dev(c, d, CBX_BUF_DIFF)) - d.arena);
-  HIP_TRY(hipSetDevice(d.hip_id));
-  HIP_TRY(hipIpcGetMemHandle(&pb.arena, d.arena));
+  pb.slot_bytes = d.stride;
+  HIP_TRY(hipIpcGetMemHandle(&pb.acc, d.xslot[0]));
+  HIP_TRY(hipIpcGetMemHandle(&pb.D, d.xslot[1]));
   if (d.g == 0 && !c->ipc.page) {
     std::snprintf(c->ipc.shm_name, sizeof(c->ipc.shm_name), "/cbx_peer_%d_%llx", (int)getpid(),
                   (unsigned long long)std::chrono::steady_clock::now().time_since_epoch().count());
@@ -242,7 +272,8 @@ int peer_import(cbx_context *c, const void *blobs, int nranks) {
   std::vector<PeerBlob> pb(nranks);
   for (int h = 0; h < nranks; ++h) {
     std::memcpy(&pb[h], static_cast<const char *>(blobs) + (size_t)h * CBX_PEER_BLOB_BYTES, sizeof(PeerBlob));
-    if (pb[h].magic != kPeerMagic || pb[h].rank != h || pb[h].G != c->G || pb[h].n4 != c->n4)
+    if (pb[h].magic != kPeerMagic || pb[h].rank != h || pb[h].G != c->G || pb[h].n4 != c->n4 ||
+        pb[h].slot_bytes != d.stride)
       return fail(CBX_ERR_INVALID, "cbx_peer_import: blob %d is not rank %d's of this job (rank %d, G %d, %lld "
                   "float4s)", h, h, pb[h].rank, pb[h].G, (long long)pb[h].n4);
   }
@@ -253,26 +284,80 @@ int peer_import(cbx_context *c, const void *blobs, int nranks) {
     TRY(map_flag_page(c, false));
   }
   if (!p.page) return fail(CBX_ERR_STATE, "cbx_peer_import: rank 0 exported no flag page");
-  p.mapped.assign(nranks, nullptr);
+  p.mapped.assign(2 * (size_t)nranks, nullptr);
   p.acc.assign(nranks, nullptr);
   p.acc_ctrl.assign(nranks, nullptr);
   p.D.assign(nranks, nullptr);
   HIP_TRY(hipSetDevice(d.hip_id));
-  for (int h = 0; h < nranks; ++h) {
-    char *base = d.arena;
-    if (h != p.me) {
-      void *m = nullptr;
-      hipError_t e = hipIpcOpenMemHandle(&m, pb[h].arena, hipIpcMemLazyEnablePeerAccess);
-      if (e != hipSuccess) {
-        const std::string msg = hipGetErrorString(e);
-        peer_close(c);
-        return fail(CBX_ERR_HIP, "hipIpcOpenMemHandle(rank %d's arena): %s", h, msg.c_str());
+  // The ranks open the others' handles one rank at a time, while every
+  // other rank waits inside a blocking HIP call (a stream wait on the
+  // opener's "opened" word, then hipStreamSynchronize).  An open of a
+  // handle completed only while its exporting process sat in such a call:
+  // with the exporter blocked outside the runtime (a pipe read, a gloo
+  // barrier) or opening handles of its own, it hung
+  // (scripts/ipcprobe.hip, scripts/ipc_torch_probe.py).
+  // A rank that never takes its turn (it failed before, or died) must not
+  // park the others forever: after 120 s a timer thread writes the awaited
+  // word itself, and the import fails.
+  hipStream_t park = nullptr;
+  HIP_TRY(hipStreamCreateWithFlags(&park, hipStreamNonBlocking));
+  std::string err;
+  std::atomic<int> waiting_for{-1};
+  std::atomic<bool> finished{false}, timed_out{false};
+  std::thread timer([&] {
+    int r = -1;
+    auto since = std::chrono::steady_clock::now();
+    while (!finished.load(std::memory_order_acquire)) {
+      std::this_thread::sleep_for(std::chrono::milliseconds(10));
+      const int w = waiting_for.load(std::memory_order_acquire);
+      if (w != r) {
+        r = w;
+        since = std::chrono::steady_clock::now();
+      } else if (r >= 0 && std::chrono::steady_clock::now() - since > std::chrono::seconds(120)) {
+        timed_out.store(true, std::memory_order_release);
+        *host_word(c, r, kIpcOpened, 0) = kIpcRelease;
+        __atomic_thread_fence(__ATOMIC_SEQ_CST);
+        r = -1;
       }
-      p.mapped[h] = base = static_cast<char *>(m);
     }
-    p.acc[h] = reinterpret_cast<const cbx::v4f *>(base + pb[h].acc_off);
-    p.acc_ctrl[h] = reinterpret_cast<const float *>(base + pb[h].acc_ctrl_off);
-    p.D[h] = reinterpret_cast<const cbx::v4f *>(base + pb[h].d_off);
+  });
+  for (int r = 0; r < nranks; ++r) {
+    if (r != p.me) {
+      waiting_for.store(r, std::memory_order_release);
+      hipError_t e = hipStreamWaitValue64(park, p.dpage + ipc_word(r, kIpcOpened, 0), 1, hipStreamWaitValueGte, ~0ull);
+      if (e == hipSuccess) e = hipStreamSynchronize(park);
+      waiting_for.store(-1, std::memory_order_release);
+      if (e != hipSuccess && err.empty()) err = fmt_msg("waiting for rank %d's turn: %s", r, hipGetErrorString(e));
+      if (timed_out.load(std::memory_order_acquire) && err.empty())
+        err = fmt_msg("rank %d did not open its handles within 120 s", r);
+      continue;
+    }
+    for (int h = 0; h < nranks && err.empty(); ++h) {
+      char *slot[2] = {d.xslot[0], d.xslot[1]};
+      for (int k = 0; k < 2 && h != p.me; ++k) {
+        void *m = nullptr;
+        hipError_t e = hipIpcOpenMemHandle(&m, k == 0 ? pb[h].acc : pb[h].D, hipIpcMemLazyEnablePeerAccess);
+        if (e != hipSuccess) {
+          err = fmt_msg("hipIpcOpenMemHandle(rank %d's %s): %s", h, k == 0 ? "acc" : "D", hipGetErrorString(e));
+          break;
+        }
+        p.mapped[2 * (size_t)h + k] = slot[k] = static_cast<char *>(m);
+      }
+      if (!err.empty()) break;
+      const size_t data = (size_t)cbx::kCtrlFloats * sizeof(float);  // the control block comes first
+      p.acc[h] = reinterpret_cast<const cbx::v4f *>(slot[0] + data);
+      p.acc_ctrl[h] = reinterpret_cast<const float *>(slot[0]);
+      p.D[h] = reinterpret_cast<const cbx::v4f *>(slot[1] + data);
+    }
+    *host_word(c, p.me, kIpcOpened, 0) = 1;  // the next rank's turn, success or not
+    __atomic_thread_fence(__ATOMIC_SEQ_CST);
+  }
+  finished.store(true, std::memory_order_release);
+  timer.join();
+  (void)hipStreamDestroy(park);
+  if (!err.empty()) {
+    peer_close(c);
+    return fail(CBX_ERR_HIP, "cbx_peer_import: %s", err.c_str());
   }
   p.ready = true;
   return CBX_OK;

@@ -418,14 +418,18 @@ int cbx_set_allreduce_algorithm (cbx_context *ctx, int algorithm);
  * executioncontext.c:185-201, and its non-NCCL path copies peer buffers,
  * common.c:64-95).  After cbx_set_model_manager on every rank:
  *   1. cbx_peer_export(ctx, blob, &bytes) writes this rank's handles into
- *      `blob` (CBX_PEER_BLOB_BYTES): its model arena's IPC handle
- *      (hipIpcGetMemHandle) and where acc and D sit in it; rank 0 also
- *      creates the page of completion flags (POSIX shared memory) and names
- *      it in its blob;
+ *      `blob` (CBX_PEER_BLOB_BYTES): the IPC handles (hipIpcGetMemHandle)
+ *      of its acc and D buffers, which move out of the model arena into
+ *      allocations of their own (at most 512 MiB each: an IPC open of a 2 GB
+ *      allocation hung under HIP 7.0; CBX_ERR_UNSUPPORTED above); rank 0
+ *      also creates the page of completion flags (POSIX shared memory) and
+ *      names it in its blob;
  *   2. the caller gathers every rank's blob, in rank order, over its own
  *      control plane (bench.py: gloo all_gather);
- *   3. cbx_peer_import(ctx, blobs, nranks) maps every other rank's arena
- *      (hipIpcOpenMemHandle) and pins the flag page (hipHostRegister).
+ *   3. cbx_peer_import(ctx, blobs, nranks) maps every other rank's acc and
+ *      D (hipIpcOpenMemHandle; the ranks open in turn, the others waiting
+ *      inside a HIP call, up to 120 s each) and pins the flag page
+ *      (hipHostRegister).
  * Then CBX_ALLREDUCE_PEER is accepted.  The ranks' streams order each
  * other through the flags: a rank writes the step's sequence number after
  * its kernel A / reduction of a bucket (hipStreamWriteValue64), the others

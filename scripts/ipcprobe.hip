@@ -98,6 +98,7 @@ int main(int argc, char **argv) {
     if (write(wfd, &fh, sizeof(fh)) != (ssize_t)sizeof(fh)) return 2;
     if (read(rfd, &fh, sizeof(fh)) != (ssize_t)sizeof(fh)) return 2;
     CK(hipIpcOpenMemHandle(reinterpret_cast<void **>(&peerflag), fh, hipIpcMemLazyEnablePeerAccess));
+    std::fprintf(stderr, "%s: opened the peer's flag\n", producer ? "producer" : "consumer");
   }
   if (producer) {
     CK(hipMalloc(reinterpret_cast<void **>(&buf), (size_t)(n ? n : 1) * 4));
@@ -110,6 +111,7 @@ int main(int argc, char **argv) {
     hipIpcMemHandle_t h;
     if (read(pfd[0], &h, sizeof(h)) != (ssize_t)sizeof(h)) return 2;
     CK(hipIpcOpenMemHandle(reinterpret_cast<void **>(&buf), h, hipIpcMemLazyEnablePeerAccess));
+    std::fprintf(stderr, "consumer: opened the buffer\n");
     CK(hipMalloc(reinterpret_cast<void **>(&bad), 64 * sizeof(unsigned)));
     CK(hipMemset(bad, 0, 64 * sizeof(unsigned)));
   }
@@ -117,6 +119,9 @@ int main(int argc, char **argv) {
   uint64_t *flagA_w = devflags ? myflag : dflags + 0, *flagB_w = devflags ? myflag : dflags + 8;
   uint64_t *flagA_r = devflags ? peerflag : dflags + 0, *flagB_r = devflags ? peerflag : dflags + 8;
   CK(hipDeviceSynchronize());
+  int rtv = 0;
+  CK(hipRuntimeGetVersion(&rtv));
+  std::fprintf(stderr, "%s: loop starts (HIP runtime %d)\n", producer ? "producer" : "consumer", rtv);
   const auto t0 = std::chrono::steady_clock::now();
   for (int i = 1; i <= iters; ++i) {
     if (producer) {
