@@ -848,8 +848,13 @@ def main():
                 return {"ms": round(ms, 4) if ms else ms, "timed_in": timed_in}
             algbw = 4 * n / (ms * 1e-3) / 1e9
             busbw = algbw * ((G - 1) / G if ar_algo == ALLREDUCE_PEER else 2 * (G - 1) / G)
-            return {"ms": round(ms, 4), "algbw_GBs": round(algbw, 1), "busbw_GBs": round(busbw, 1),
-                    "xgmi_frac": round(busbw / ((G - 1) * XGMI_LINK_GBS), 4), "timed_in": timed_in}
+            out = {"ms": round(ms, 4), "algbw_GBs": round(algbw, 1), "busbw_GBs": round(busbw, 1),
+                   "xgmi_frac": round(busbw / ((G - 1) * XGMI_LINK_GBS), 4), "timed_in": timed_in}
+            if args.rehearse_one_gpu:
+                # every rank on one GPU: the bytes never cross a link, so a
+                # fraction of the xGMI bound would mean nothing
+                out.update(xgmi_frac=None, note="rehearsal: every rank on one GPU, no xGMI link crossed")
+            return out
         ar_ms = statistics.median(calib["allreduce"])
         unp = link(ar_ms, "calibration steps (one bucket, in order: the collective alone)")
         unp.update(apply_ms_median=round(statistics.median(calib["apply"]), 4),
