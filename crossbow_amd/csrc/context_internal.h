@@ -533,9 +533,8 @@ struct cbx_context {
   // POSIX shared memory that every rank pins (hipHostRegister).  Rank h
   // writes its flags from its streams (hipStreamWriteValue64: the step's
   // sequence number once kernel A / the reduction of a bucket is done); the
-  // others' streams wait on them (hipStreamWaitValue64 >=).  Flags in device
-  // memory opened through IPC were never seen by a waiting stream on the one
-  // GPU tried (scripts/ipcprobe.hip), so the page is host memory.
+  // others' streams wait on them (hipStreamWaitValue64 >=).  The page is
+  // host memory: it needs no IPC mapping of its own (scripts/ipcprobe.hip).
   struct PeerIpc {
     bool ready = false;
     bool broken = false;                  // a step failed part-way: the flags were released
