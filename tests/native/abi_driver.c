@@ -203,6 +203,12 @@ int main (void) {
 	EXPECT (cbx_replica_lock (c, 99) == CBX_ERR_INVALID);
 	EXPECT (cbx_synchronise_staged (c, 0, 7, 0, 0) == CBX_ERR_INVALID);
 	EXPECT (cbx_set_kernel_config (c, 96, 0, 1, 1) == CBX_ERR_INVALID);
+	{	/* the per-rank peer-read form's handles: one process over its devices has none to export */
+		unsigned char blob[CBX_PEER_BLOB_BYTES];
+		size_t bytes = 0;
+		EXPECT (cbx_peer_export (c, blob, &bytes) == CBX_ERR_UNSUPPORTED);
+		EXPECT (cbx_peer_import (c, blob, 1) == CBX_ERR_STATE);
+	}
 	CHECK (cbx_set_kernel_config (c, 64, 0, 1, 2));
 	CHECK (cbx_set_aux_kernel_config (c, 128, 2, 4));
 	barrier (c, 7, 0);
