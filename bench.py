@@ -455,6 +455,58 @@ def base_identity(gpu, world):
                        "across every GPU (every GPU applies the same D, sma.c:168-174)"}
 
 
+def form_agreement(gpu, world, step, chosen, one_bucket, algorithm_name):
+    """After the timed region at G > 1, when the measured configuration is not
+    the reference's own collective: one more step in that configuration, and
+    the same step from the same state through one RCCL all-reduce of the
+    whole buffer, in order (synch/common.c:3-57).  z and last must agree
+    within the G > 1 tolerance (rtol 1e-5, atol 1e-6, BASELINE.md 2.5: the
+    collectives sum in different orders; a peer-read sum and a 2-rank
+    all-reduce are the same sum, so G = 2 is bit for bit).  The state is
+    put back afterwards.  With `identity` this catches a configuration that
+    is fast because it is wrong, on the hardware it ran on, without the
+    oracle."""
+    import numpy as np
+    from crossbow_amd import BUF_DATA, BUF_LAST
+    devs, reps = list(gpu.local_devices()), list(gpu.local_replicas())
+    gpu.wait()
+    base = {(g, k): gpu.base_read(g, k) for g in devs for k in (BUF_DATA, BUF_LAST)}
+    ws = {i: gpu.replica_read(i, BUF_DATA) for i in reps}
+
+    def restore():
+        for (g, k), a in base.items():
+            gpu.base_write(g, k, a)
+        for i, a in ws.items():
+            gpu.replica_write(i, BUF_DATA, a)
+
+    def result():
+        return {(g, k): gpu.base_read(g, k) for g in devs for k in (BUF_DATA, BUF_LAST)}
+
+    step()
+    gpu.wait()
+    got = result()
+    restore()
+    gpu.set_allreduce_algorithm(0)
+    gpu.set_bucket_elements(one_bucket)
+    gpu.set_pipeline_mode(0)
+    step()
+    gpu.wait()
+    ref = result()
+    restore()
+    gpu.set_allreduce_algorithm(chosen["algorithm"])
+    gpu.set_bucket_elements(chosen["bucket_elements"])
+    gpu.set_pipeline_mode(chosen["mode"])
+    gpu.wait()
+    diff = max(float(np.max(np.abs(got[key].astype(np.float64) - ref[key]))) for key in got)
+    close = all(np.allclose(got[key], ref[key], rtol=1e-5, atol=1e-6) for key in got)
+    same = all(np.array_equal(got[key].view(np.uint32), ref[key].view(np.uint32)) for key in got)
+    from crossbow_amd import dist as D
+    return {"configuration": f"{algorithm_name}, {chosen['buckets']} bucket(s), mode {chosen['mode']}",
+            "against": "one RCCL all-reduce of the whole buffer, in order (synch/common.c:3-57)",
+            "max_abs_diff": D.max_over_ranks(diff, world), "within_tolerance": all_ranks(close, world),
+            "bitwise_equal": all_ranks(same, world), "tolerance": "rtol 1e-5, atol 1e-6 (BASELINE.md 2.5)"}
+
+
 def all_ranks(flag: bool, world: int) -> bool:
     """Logical AND of a flag over the ranks."""
     if world <= 1:
@@ -815,6 +867,9 @@ def main():
     result["step_ms_device_median"] = round(statistics.median(steps_ms), 4)
     if identity is not None:
         result["identity"] = identity
+        if not peer_only and (ar_algo != 0 or chosen["buckets"] != 1):
+            wd.enter("agreement with the all-reduce", 300)
+            identity["vs_all_reduce"] = form_agreement(gpu, world, step, chosen, one_bucket, form)
     if G > 1:
         # Host side of the step (lockAny + synchronise + unlockAny, every local
         # device's enqueue) against the device's step: the single-process form

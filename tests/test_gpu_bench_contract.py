@@ -81,6 +81,8 @@ def test_bench_two_ranks_through_the_launcher_prints_one_json_line():
     # every rank ends the timed region with the same z and last, bit for bit
     idn = d["identity"]
     assert idn["z_last_identical_on_every_gpu"] is True and idn["finite"] is True and idn["gpus_checked"] == 2
+    # the measured (bucketed) configuration against one in-order all-reduce of the same step
+    assert idn["vs_all_reduce"]["within_tolerance"] is True, idn["vs_all_reduce"]
 
 
 @pytest.mark.timeout(300)
