@@ -90,8 +90,9 @@ def _rank_main(rank, world, jobs, uids, fake_dir, q):
             os.environ["FAKE_RCCL_ORDER"] = case.order if (kind == "case") else "rank"
             g = C.init_rank(L, A, rank, world, uid)
             try:
-                # the peer-read all-reduce needs one process over every device
-                assert L.cbx_set_allreduce_algorithm(g.c, A.ALLREDUCE_PEER) == A.CBX_ERR_UNSUPPORTED
+                # one process per GPU: the peer-read all-reduce needs the other
+                # ranks' buffers mapped first (cbx_peer_import, test_gpu_peer_ipc.py)
+                assert L.cbx_set_allreduce_algorithm(g.c, A.ALLREDUCE_PEER) == A.CBX_ERR_STATE
                 if kind == "case":
                     res = C.run_case(g, world, [rank], case)
                 elif kind.startswith("golden"):
