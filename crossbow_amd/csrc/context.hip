@@ -1589,6 +1589,7 @@ int cbx_peer_export(cbx_context *c, void *blob, size_t *bytes) {
 
 int cbx_peer_import(cbx_context *c, const void *blobs, int nranks) {
   TRY(check_ctx(c));
+  TraceRange trace("cbx_peer_import");  // the ranks open each other's handles in turn: seconds, not microseconds
   return peer_import(c, blobs, nranks);
 }
 
