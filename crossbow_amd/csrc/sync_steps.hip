@@ -368,14 +368,18 @@ void peer_close(cbx_context *c) {
   if (!p.page && p.mapped.empty()) return;
   Device &d = c->devs[0];
   (void)hipSetDevice(d.hip_id);
-  if (p.ready) {
-    // Every rank's streams must be done with this rank's memory (and this
-    // rank with theirs) before any arena goes: drain, then meet the others
-    // on the page (at most 60 s: a rank that died never arrives).
+  if (p.page) {
+    // done with the others' memory (also when this rank's import failed, so
+    // a rank whose import succeeded does not wait for it in vain)
     for (hipStream_t s : {d.stream, d.comm_stream, d.a_stream, d.a_stream2})
       if (s) (void)hipStreamSynchronize(s);
     *host_word(c, p.me, kIpcDone, 0) = 1;
     __atomic_thread_fence(__ATOMIC_SEQ_CST);
+  }
+  if (p.ready) {
+    // Every rank's streams must be done with this rank's memory (and this
+    // rank with theirs) before any buffer goes: drained above, then meet the
+    // others on the page (at most 60 s: a rank that died never arrives).
     const auto t0 = std::chrono::steady_clock::now();
     for (int h = 0; h < c->G; ++h)
       while (*host_word(c, h, kIpcDone, 0) == 0 &&
