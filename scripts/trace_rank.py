@@ -4,7 +4,8 @@ transport, NCCL_HOSTID per rank), for a kernel trace of the bucketed
 pipeline with an asynchronous collective beside kernels A and B.
 
 Launched once per rank by scripts/trace_real_rccl.sh, each under its own
-rocprofv3 (the profiler wraps this program directly).  Ranks meet through
+rocprofv3 (the profiler wraps this program directly).  algo 1: the per-rank
+peer-read form (cbx_peer_export / _import through files in $TRACE_DIR).  Ranks meet through
 files in $TRACE_DIR.  Usage: trace_rank.py RANK WORLD [buckets] [mode] [algo]
 """
 from __future__ import annotations
@@ -34,6 +35,9 @@ def main():
     try:
         n, R = 25_557_032, 8
         C.setup_model(g, A, n, R, 0.9, 7, A.SYNC_BSP, 2 * world * R)
+        if algo == 1:  # the per-rank peer-read form: map the other ranks' acc / D first
+            from tests.test_gpu_peer_ipc import exchange
+            exchange(g, rank, world, d, "trace")
         g("cbx_fill_synthetic", 20190701)
         g("cbx_set_bucket_elements", ctypes.c_longlong(-(-n // buckets)))
         g("cbx_set_pipeline_mode", mode)
