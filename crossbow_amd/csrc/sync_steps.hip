@@ -905,6 +905,7 @@ struct SplitStep {
 
   // Kernel B (Phase C, + D on copy) of bucket b on devices [k0, k1).
   int apply(int64_t b, size_t k0, size_t k1) {
+    const int64_t ar_group = std::max(1, c->allreduce_group);
     if (peer) TRY(await_all(r_seq, b));
     for (size_t k = k0; k < k1; ++k) {
       Device &d = c->devs[k];
@@ -918,7 +919,14 @@ struct SplitStep {
         HIP_TRY(hipStreamWaitEvent(d.stream, ev_red(h, b), 0));
         note_wait(k, 0, ev_red(h, b));
       }
-      TRY(wait_flags(d.stream, kIpcR, b));  // one process per GPU: every other rank's reduction
+      // One process per GPU: every other rank's reduction.  With all-reduce
+      // groups, once per group, on the group's last bucket: each rank's
+      // reductions run in order on its comm stream, so that flag implies the
+      // group's earlier ones, and every R of the group is enqueued before
+      // its first B (fewer cross-process hand-offs, ~19 us each when the
+      // wait blocks: profiles/r04/ipc/).
+      if (!pipelined || b % ar_group == 0)
+        TRY(wait_flags(d.stream, kIpcR, pipelined ? std::min<int64_t>(b + ar_group - 1, nb - 1) : b));
       cbx::LaunchConfig cfg = c->apply_cfg;
       cfg.num_cus = d.num_cus;
       cbx::Timing t;
