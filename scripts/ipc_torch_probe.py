@@ -46,6 +46,9 @@ def main():
     dist.all_gather_object(blobs, blob)
     say("gathered; importing" + (" one rank at a time" if serial else ""))
     if serial:
+        # the round-4 experiment that found the open-in-turn rule; since then
+        # cbx_peer_import runs the turns itself (every rank must call it at
+        # once), so this form now ends in the library's 120 s turn timeout
         for r in range(world):
             if r == rank:
                 gpu.peer_import(blobs)
