@@ -651,7 +651,7 @@ def main():
     if G > 1 and not single:
         # the peer-read all-reduce needs every rank's buffers mapped through
         # IPC handles (then it is a tuner candidate, as in the single process)
-        wd.enter("peer-read IPC mapping", 120)
+        wd.enter("peer-read IPC mapping", 300)  # the library gives up on a missing rank after 120 s
         peer_ipc = D.setup_peer(gpu, world) or "mapped"
 
     clock = 0

@@ -297,27 +297,23 @@ int peer_import(cbx_context *c, const void *blobs, int nranks) {
   // barrier) or opening handles of its own, it hung
   // (scripts/ipcprobe.hip, scripts/ipc_torch_probe.py).
   // A rank that never takes its turn (it failed before, or died) must not
-  // park the others forever: after 120 s a timer thread writes the awaited
-  // word itself, and the import fails.
+  // park the others forever: 120 s after the import began (it takes
+  // seconds) a timer thread writes every awaited word itself, and the
+  // import fails.
   hipStream_t park = nullptr;
   HIP_TRY(hipStreamCreateWithFlags(&park, hipStreamNonBlocking));
   std::string err;
   std::atomic<int> waiting_for{-1};
   std::atomic<bool> finished{false}, timed_out{false};
+  const auto deadline = std::chrono::steady_clock::now() + std::chrono::seconds(120);
   std::thread timer([&] {
-    int r = -1;
-    auto since = std::chrono::steady_clock::now();
     while (!finished.load(std::memory_order_acquire)) {
       std::this_thread::sleep_for(std::chrono::milliseconds(10));
       const int w = waiting_for.load(std::memory_order_acquire);
-      if (w != r) {
-        r = w;
-        since = std::chrono::steady_clock::now();
-      } else if (r >= 0 && std::chrono::steady_clock::now() - since > std::chrono::seconds(120)) {
+      if (w >= 0 && std::chrono::steady_clock::now() > deadline) {
         timed_out.store(true, std::memory_order_release);
-        *host_word(c, r, kIpcOpened, 0) = kIpcRelease;
+        *host_word(c, w, kIpcOpened, 0) = kIpcRelease;
         __atomic_thread_fence(__ATOMIC_SEQ_CST);
-        r = -1;
       }
     }
   });
@@ -329,7 +325,7 @@ int peer_import(cbx_context *c, const void *blobs, int nranks) {
       waiting_for.store(-1, std::memory_order_release);
       if (e != hipSuccess && err.empty()) err = fmt_msg("waiting for rank %d's turn: %s", r, hipGetErrorString(e));
       if (timed_out.load(std::memory_order_acquire) && err.empty())
-        err = fmt_msg("rank %d did not open its handles within 120 s", r);
+        err = fmt_msg("rank %d had not opened its handles 120 s into the import", r);
       continue;
     }
     for (int h = 0; h < nranks && err.empty(); ++h) {

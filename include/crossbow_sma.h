@@ -428,7 +428,8 @@ int cbx_set_allreduce_algorithm (cbx_context *ctx, int algorithm);
  *      control plane (bench.py: gloo all_gather);
  *   3. cbx_peer_import(ctx, blobs, nranks) maps every other rank's acc and
  *      D (hipIpcOpenMemHandle; the ranks open in turn, the others waiting
- *      inside a HIP call, up to 120 s each) and pins the flag page
+ *      inside a HIP call; a rank that has not opened its handles 120 s into
+ *      the import fails everyone's import) and pins the flag page
  *      (hipHostRegister).
  * Then CBX_ALLREDUCE_PEER is accepted.  The ranks' streams order each
  * other through the flags: a rank writes the step's sequence number after
