@@ -498,12 +498,14 @@ def form_agreement(gpu, world, step, chosen, one_bucket, algorithm_name):
     gpu.set_pipeline_mode(chosen["mode"])
     gpu.wait()
     diff = max(float(np.max(np.abs(got[key].astype(np.float64) - ref[key]))) for key in got)
+    scale = max(float(np.max(np.abs(ref[key]))) for key in ref)  # the diff's yardstick
     close = all(np.allclose(got[key], ref[key], rtol=1e-5, atol=1e-6) for key in got)
     same = all(np.array_equal(got[key].view(np.uint32), ref[key].view(np.uint32)) for key in got)
     from crossbow_amd import dist as D
     return {"configuration": f"{algorithm_name}, {chosen['buckets']} bucket(s), mode {chosen['mode']}",
             "against": "one RCCL all-reduce of the whole buffer, in order (synch/common.c:3-57)",
-            "max_abs_diff": D.max_over_ranks(diff, world), "within_tolerance": all_ranks(close, world),
+            "max_abs_diff": D.max_over_ranks(diff, world), "max_abs_value": D.max_over_ranks(scale, world),
+            "within_tolerance": all_ranks(close, world),
             "bitwise_equal": all_ranks(same, world), "tolerance": "rtol 1e-5, atol 1e-6 (BASELINE.md 2.5)"}
 
 
