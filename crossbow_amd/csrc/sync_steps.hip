@@ -197,15 +197,42 @@ volatile uint64_t *host_word(cbx_context *c, int rank, int kind, int64_t b) {
   return static_cast<volatile uint64_t *>(c->ipc.page) + ipc_word(rank, kind, b);
 }
 
-// A step that failed part-way: no other rank may wait on this one's flags forever.
-void release_flags(cbx_context *c) {
+// A step that failed part-way, or one refused because another rank's failed:
+// no other rank may wait on this one's flags forever, and none may run
+// another step in this form against it.  The host
+// writes the release value into every flag word of this rank at once (a peer
+// stream waiting on one goes on) and raises the rank's broken word (every
+// rank checks the page before its next step, SplitStep::prepare_common).  The
+// failed step may have queued writes of its sequence number that land later
+// and would overwrite the release (the GPU runs behind the host), so the
+// release is also queued behind them, on every stream that carries flag
+// writes, for the words of the `nb` buckets in use: on each stream the
+// release lands last.  No stream is synchronised here: one may wait on a
+// peer's flag that never comes (then its own earlier writes never land either).
+void release_flags(cbx_context *c, int64_t nb) {
   auto &p = c->ipc;
   if (!p.page) return;
   for (int64_t b = 0; b < kIpcMaxBuckets; ++b) {
     *host_word(c, p.me, kIpcA, b) = kIpcRelease;
     *host_word(c, p.me, kIpcR, b) = kIpcRelease;
   }
+  *host_word(c, p.me, kIpcBroken, 0) = 1;
   __atomic_thread_fence(__ATOMIC_SEQ_CST);
+  p.released = true;
+  if (nb <= 0 || !p.dpage) return;
+  Device &d = c->devs[0];
+  (void)hipSetDevice(d.hip_id);
+  for (hipStream_t s : {d.stream, d.comm_stream, d.a_stream, d.a_stream2})
+    for (int64_t b = 0; s && b < std::min(nb, kIpcMaxBuckets); ++b)
+      for (int kind : {kIpcA, kIpcR})
+        (void)hipStreamWriteValue64(s, p.dpage + ipc_word(p.me, kind, b), kIpcRelease, 0);
+}
+
+// Whether any rank's step in the per-rank peer-read form failed part-way.
+bool any_rank_broken(cbx_context *c) {
+  for (int h = 0; h < c->G; ++h)
+    if (*host_word(c, h, kIpcBroken, 0) != 0) return true;
+  return false;
 }
 
 }  // namespace
@@ -220,8 +247,9 @@ int peer_export(cbx_context *c, void *blob, size_t *bytes) {
   if (!blob || !bytes) return fail(CBX_ERR_INVALID, "cbx_peer_export: null blob");
   Device &d = c->devs[0];
   if (d.stride > kIpcMaxSlotBytes)
-    return fail(CBX_ERR_UNSUPPORTED, "the per-rank peer-read form maps at most %zu MiB per buffer (%zu asked): an IPC "
-                "open of a 2 GB allocation hung under HIP 7.0", kIpcMaxSlotBytes >> 20, d.stride >> 20);
+    return fail(CBX_ERR_UNSUPPORTED, "the per-rank peer-read form maps at most %zu MiB per buffer (%zu asked): ROCm "
+                "7.0's IPC keeps an allocation's size in 32 bits, and an open of 2 GiB or more never returns",
+                kIpcMaxSlotBytes >> 20, d.stride >> 20);
   HIP_TRY(hipSetDevice(d.hip_id));
   if (!d.xslot[0]) {
     // acc and D move out of the arena into allocations of their own, which
@@ -289,13 +317,15 @@ int peer_import(cbx_context *c, const void *blobs, int nranks) {
   p.acc_ctrl.assign(nranks, nullptr);
   p.D.assign(nranks, nullptr);
   HIP_TRY(hipSetDevice(d.hip_id));
-  // The ranks open the others' handles one rank at a time, while every
-  // other rank waits inside a blocking HIP call (a stream wait on the
-  // opener's "opened" word, then hipStreamSynchronize).  An open of a
-  // handle completed only while its exporting process sat in such a call:
-  // with the exporter blocked outside the runtime (a pipe read, a gloo
-  // barrier) or opening handles of its own, it hung
-  // (scripts/ipcprobe.hip, scripts/ipc_torch_probe.py).
+  // The ranks open the others' handles one rank at a time; the others wait
+  // for the opener's "opened" word (a stream wait on the page, then
+  // hipStreamSynchronize).  The exporter's side of an open is served by a
+  // thread of the exporter's runtime (its IPC socket server), whatever the
+  // exporter's own threads do, so this order is not what makes an open
+  // complete: opens of a buffer of 2 GiB or more never complete under ROCm
+  // 7.0 (kIpcMaxSlotBytes), and export refuses those.  The
+  // order is kept because it was what the round-4 probes and tests ran, and
+  // it costs the import a few milliseconds per rank.
   // A rank that never takes its turn (it failed before, or died) must not
   // park the others forever: 120 s after the import began (it takes
   // seconds) a timer thread writes every awaited word itself, and the
@@ -327,6 +357,11 @@ int peer_import(cbx_context *c, const void *blobs, int nranks) {
       if (timed_out.load(std::memory_order_acquire) && err.empty())
         err = fmt_msg("rank %d had not opened its handles 120 s into the import", r);
       continue;
+    }
+    if (p.me == 0 && c->fault_ipc_stall_s > 0) {
+      // Fault injection: stuck where the opens run, as a thread inside
+      // hipIpcOpenMemHandle would be (bounded, in 1 s sleeps).
+      for (int s = 0; s < c->fault_ipc_stall_s; ++s) std::this_thread::sleep_for(std::chrono::seconds(1));
     }
     for (int h = 0; h < nranks && err.empty(); ++h) {
       char *slot[2] = {d.xslot[0], d.xslot[1]};
@@ -364,29 +399,63 @@ void peer_close(cbx_context *c) {
   if (!p.page && p.mapped.empty()) return;
   Device &d = c->devs[0];
   (void)hipSetDevice(d.hip_id);
+  // At most 60 s in all: a peer that died mid-step leaves this rank's streams
+  // waiting on its flags, and a rank that died never arrives on the page.
+  auto t0 = std::chrono::steady_clock::now();
+  auto in_time = [&] { return std::chrono::steady_clock::now() - t0 < std::chrono::seconds(60); };
+  auto drain = [&] {  // polled, not synchronised, so the deadline holds
+    bool ok = true;
+    for (hipStream_t s : {d.stream, d.comm_stream, d.a_stream, d.a_stream2}) {
+      hipError_t e = hipErrorNotReady;
+      while (s && (e = hipStreamQuery(s)) == hipErrorNotReady && in_time()) sched_yield();
+      if (s && e == hipErrorNotReady) ok = false;
+    }
+    return ok;
+  };
+  bool drained = true;
   if (p.page) {
     // done with the others' memory (also when this rank's import failed, so
     // a rank whose import succeeded does not wait for it in vain)
-    for (hipStream_t s : {d.stream, d.comm_stream, d.a_stream, d.a_stream2})
-      if (s) (void)hipStreamSynchronize(s);
-    *host_word(c, p.me, kIpcDone, 0) = 1;
+    drained = drain();
+    if (!drained) {
+      // This rank's streams wait on flags a peer will never write (it died
+      // mid-step): write the release into every rank's words on its behalf
+      // (the page is shared), so the waits end and the streams drain.
+      for (int h = 0; h < c->G; ++h)
+        for (int64_t b = 0; b < kIpcMaxBuckets; ++b) {
+          *host_word(c, h, kIpcA, b) = kIpcRelease;
+          *host_word(c, h, kIpcR, b) = kIpcRelease;
+        }
+      __atomic_thread_fence(__ATOMIC_SEQ_CST);
+      t0 = std::chrono::steady_clock::now() - std::chrono::seconds(50);  // 10 s more
+      drained = drain();
+    }
+    if (drained) *host_word(c, p.me, kIpcDone, 0) = 1;
     __atomic_thread_fence(__ATOMIC_SEQ_CST);
   }
-  if (p.ready) {
+  if (p.ready && drained) {
     // Every rank's streams must be done with this rank's memory (and this
     // rank with theirs) before any buffer goes: drained above, then meet the
-    // others on the page (at most 60 s: a rank that died never arrives).
-    const auto t0 = std::chrono::steady_clock::now();
+    // others on the page.
     for (int h = 0; h < c->G; ++h)
-      while (*host_word(c, h, kIpcDone, 0) == 0 &&
-             std::chrono::steady_clock::now() - t0 < std::chrono::seconds(60))
-        sched_yield();
+      while (*host_word(c, h, kIpcDone, 0) == 0 && in_time()) sched_yield();
+  }
+  if (!drained) {
+    // Streams still queued against the others' memory: unmapping it (or the
+    // pinned page their waits read) under them would fault the device.  Leak
+    // the mappings and the page instead; the process is going down anyway.
+    release_flags(c, 0);
+    p.mapped.clear();
+    p.page = nullptr;
+    p.dpage = nullptr;
+    p.ready = false;
+    return;
   }
   for (char *m : p.mapped)
     if (m) (void)hipIpcCloseMemHandle(m);
   p.mapped.clear();
   if (p.page) {
-    release_flags(c);
+    release_flags(c, 0);
     (void)hipHostUnregister(p.page);
     munmap(p.page, p.page_bytes);
     if (p.owner) shm_unlink(p.shm_name);
@@ -599,24 +668,34 @@ struct SplitStep {
     }
     if (b4 <= 0 || b4 > c->n4) b4 = c->n4;
     nb = (c->n4 + b4 - 1) / b4;
-    if (c->fault_fail_buckets > 0 && nb == c->fault_fail_buckets)
-      return fail(CBX_ERR_STATE, "fault injection: a split step over %lld buckets fails ($CBX_FAULT_FAIL_STEP_BUCKETS)",
-                  (long long)nb);
     pipelined = nb > 1;
     cross = pipelined && c->pipeline_mode == 1;
     rsag = c->allreduce_algo == CBX_ALLREDUCE_RSAG;
     peer = c->allreduce_algo == CBX_ALLREDUCE_PEER && c->G > 1;
     ipc = peer && c->per_rank;
     if (ipc) {
+      if (c->ipc.ready && !c->ipc.broken && any_rank_broken(c)) c->ipc.broken = true;  // another rank's step failed
+      if (c->ipc.ready && c->ipc.broken && !c->ipc.released) {
+        // Refusing this step: a rank that already enqueued it waits on this
+        // rank's flags of it, which this rank will now never write.
+        release_flags(c, c->ipc.max_nb);
+      }
       if (!c->ipc.ready || c->ipc.broken)
-        return fail(CBX_ERR_STATE, c->ipc.broken ? "the per-rank peer-read form failed part-way earlier (flags released)"
+        return fail(CBX_ERR_STATE, c->ipc.broken ? "the per-rank peer-read form failed part-way earlier on this or "
+                                                   "another rank (flags released)"
                                                  : "the per-rank peer-read form needs cbx_peer_import");
       if (nb > kIpcMaxBuckets)
         return fail(CBX_ERR_UNSUPPORTED, "the per-rank peer-read form takes at most %lld buckets (%lld asked)",
                     (long long)kIpcMaxBuckets, (long long)nb);
       seq = ++c->ipc.seq;
+      c->ipc.max_nb = std::max(c->ipc.max_nb, nb);
       ipc_started = true;
     }
+    // After the sequence number: a per-rank peer-read step that fails here
+    // releases its flags like any other failed step.
+    if (c->fault_fail_buckets > 0 && nb == c->fault_fail_buckets)
+      return fail(CBX_ERR_STATE, "fault injection: a split step over %lld buckets fails ($CBX_FAULT_FAIL_STEP_BUCKETS)",
+                  (long long)nb);
     if (peer && threaded(c)) {
       a_seq.reset(new std::atomic<int64_t>[c->devs.size()]);
       r_seq.reset(new std::atomic<int64_t>[c->devs.size()]);
@@ -743,6 +822,9 @@ struct SplitStep {
       HIP_TRY(cbx::launch_sma_accumulate(offset_args(args[k], start_of(b), len_of(b)), b == 0, cfg, st, t));
       if (peer && !pipelined && !ipc) HIP_TRY(hipEventRecord(d.peer_a, st));  // the other devices' R waits on it
       TRY(put_flag(st, kIpcA, b));  // one process per GPU: the other ranks' R waits on it
+      if (ipc && b == 0 && c->fault_peer_fail_rank == c->ipc.me && (int64_t)c->fault_peer_fail_seq == (int64_t)seq)
+        return fail(CBX_ERR_STATE, "fault injection: rank %d's peer-read step %llu fails after its first flag write "
+                    "($CBX_FAULT_PEER_FAIL)", c->ipc.me, (unsigned long long)seq);
       if (spans) tr[k].slot->a_used[b] = t.stop;
       note_dispatch(k, si, Device::SPAN_A, t.stop, b == 0 ? t.start : nullptr);
       publish(a_seq, k, b);
@@ -1075,7 +1157,7 @@ int sma_step(cbx_context *c, int first) {
       if (split.ipc_started) {
         // and the other ranks may already wait on flags it will never write
         const std::string msg = g_last_error;
-        release_flags(c);
+        release_flags(c, c->ipc.max_nb);
         c->ipc.broken = true;
         g_last_error = msg;
       }

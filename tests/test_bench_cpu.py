@@ -83,3 +83,122 @@ def test_rccl_tuning_run_repeats_the_chosen_configuration(monkeypatch):
     cmd = seen["cmd"]
     assert cmd[1].endswith("bench.py") and "--single-process" in cmd
     assert cmd[cmd.index("--enqueue-threads") + 1] == "1"
+
+
+def test_watchdog_prints_the_line_when_a_later_phase_stalls():
+    # Once the first timed region has produced the line, a later phase that
+    # misses its deadline (e.g. the per-rank peer-read form's IPC mapping)
+    # must not cost it: the watchdog prints exactly that one line, naming the
+    # phase that did not finish, with every thread's kernel-side state on
+    # stderr, and the run exits 0 (VERDICT r04 Next #1).
+    import json
+    p = subprocess.run([sys.executable, "bench.py", "--watchdog-selftest-result", "1"], cwd=ROOT,
+                       capture_output=True, text=True, timeout=120)
+    assert p.returncode == 0, (p.returncode, p.stderr[-2000:])
+    lines = [ln for ln in p.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1, p.stdout
+    d = json.loads(lines[0])
+    assert d["value"] == 1.0 and d["incomplete_phase"]["phase"] == "selftest post-timed stall"
+    assert "WATCHDOG" in p.stderr and " wchan=" in p.stderr and " syscall=" in p.stderr, p.stderr[-2000:]
+
+
+def test_watchdog_names_a_stalled_ipc_mapping_in_the_line():
+    # The line the watchdog prints for a stalled IPC mapping says so in
+    # config.peer_ipc (the field the driver's N > 1 line carries).
+    sys.path.insert(0, ROOT)
+    import json
+
+    import bench
+    wd = bench.Watchdog(0, 0)
+    wd.publish({"metric": bench.METRIC, "value": 5.0, "config": {"peer_ipc": "mapping"}}, None)
+    d = json.loads(wd._line("peer-read IPC mapping", 300.0, "agreement with the all-reduce"))
+    assert d["config"]["peer_ipc"].startswith("failed: 'peer-read IPC mapping' missed its 300 s deadline")
+    assert d["incomplete_phase"]["last_completed"] == "agreement with the all-reduce" and d["value"] == 5.0
+
+
+def test_thread_states_lists_every_thread():
+    sys.path.insert(0, ROOT)
+    import threading
+
+    import bench
+    ev = threading.Event()
+    t = threading.Thread(target=ev.wait, name="waiter", daemon=True)
+    t.start()
+    try:
+        out = bench.thread_states()
+    finally:
+        ev.set()
+    rows = [ln for ln in out.splitlines() if ln.strip().startswith("tid ")]
+    assert len(rows) >= 2 and all(" wchan=" in r and " syscall=" in r for r in rows), out
+
+
+class _FakeGpu:
+    """Just enough of TheGPU for bench.form_agreement on the CPU: z and last of
+    one device, replicas' w, and a 'step' that moves z by a fixed amount
+    (the measured form) or by that amount plus `skew` (the reference form)."""
+
+    def __init__(self, z, skew=0.0):
+        import numpy as np
+        self.np = np
+        self.z = np.asarray(z, dtype=np.float32)
+        self.last = np.zeros_like(self.z)
+        self.w = {0: np.ones_like(self.z)}
+        self.algo, self.skew = 1, skew
+
+    def local_devices(self):
+        return [0]
+
+    def local_replicas(self):
+        return [0]
+
+    def wait(self):
+        pass
+
+    def base_read(self, g, kind):
+        return (self.z if kind == 0 else self.last).copy()
+
+    def base_write(self, g, kind, a):
+        if kind == 0:
+            self.z = a.copy()
+        else:
+            self.last = a.copy()
+
+    def replica_read(self, i, kind):
+        return self.w[i].copy()
+
+    def replica_write(self, i, kind, a):
+        self.w[i] = a.copy()
+
+    def set_allreduce_algorithm(self, a):
+        self.algo = a
+
+    def set_bucket_elements(self, b):
+        pass
+
+    def set_pipeline_mode(self, m):
+        pass
+
+    def step(self):
+        self.z = (self.z + self.np.float32(0.5) + (self.np.float32(self.skew) if self.algo == 0 else 0)).astype(
+            self.np.float32)
+
+
+def test_agreement_check_is_vacuous_at_blown_up_values():
+    # The G > 1 agreement check compares the measured form's step with one
+    # in-order all-reduce of the same step within rtol 1e-5: at |z| ~ 1.7e13
+    # that forgives 1.7e8, so a large diff would pass.  Above 1e3 the check
+    # reports itself vacuous and not within tolerance (VERDICT r04 Weak #3).
+    sys.path.insert(0, ROOT)
+    import bench
+    from crossbow_amd import BUF_DATA, BUF_LAST
+    assert (BUF_DATA, BUF_LAST) == (0, 1) or True
+    chosen = {"algorithm": 1, "bucket_elements": 1 << 20, "mode": 1, "buckets": 4}
+    big = _FakeGpu([1.6e13, -3.0, 2.0], skew=1.0e6)
+    r = bench.form_agreement(big, 1, big.step, chosen, 1 << 62, "peer-read two-shot")
+    assert r["vacuous"] is True and r["within_tolerance"] is False and r["max_abs_value"] > 1e13
+    small = _FakeGpu([0.25, -0.1, 0.05])
+    r = bench.form_agreement(small, 1, small.step, chosen, 1 << 62, "peer-read two-shot")
+    assert r["vacuous"] is False and r["within_tolerance"] is True and r["bitwise_equal"] is True
+    skewed = _FakeGpu([0.25, -0.1, 0.05], skew=1e-3)
+    r = bench.form_agreement(skewed, 1, skewed.step, chosen, 1 << 62, "peer-read two-shot")
+    assert r["vacuous"] is False and r["within_tolerance"] is False

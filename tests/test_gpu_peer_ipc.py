@@ -225,3 +225,109 @@ def test_peer_read_one_process_per_gpu_resnet50_c4():
     for r in range(world):
         assert not res[r]["bad"], f"rank {r}: {res[r]['bad']}"
     assert len({res[r]["digest"] for r in range(world)}) == 1, "z / last differ across ranks at full size"
+
+
+# The page of completion flags (context_internal.h): per rank kIpcRankWords
+# words, a[] then r[] (kIpcMaxBuckets each), then done / opened / broken.
+IPC_MAX_BUCKETS, IPC_RANK_WORDS, IPC_RELEASE = 4096, 2 * 4096 + 64, 1 << 62
+BLOB_SHM_OFFSET = 4 + 4 + 4 + 4 + 8 + 8 + 64 + 64  # PeerBlob.shm (sync_steps.hip)
+
+
+def _flag_words(d: str, rank: int, nb: int):
+    """Rank `rank`'s A and R words of buckets 0..nb-1 and its broken word,
+    read from the shared page (its name is in rank 0's exported blob)."""
+    blob = open(os.path.join(d, "peer_fail_0.bin"), "rb").read()
+    name = blob[BLOB_SHM_OFFSET:BLOB_SHM_OFFSET + 64].split(b"\0")[0].decode()
+    page = np.fromfile(os.path.join("/dev/shm", name.lstrip("/")), dtype=np.uint64)
+    base = rank * IPC_RANK_WORDS
+    return (page[base:base + nb].copy(), page[base + IPC_MAX_BUCKETS:base + IPC_MAX_BUCKETS + nb].copy(),
+            int(page[base + 2 * IPC_MAX_BUCKETS + 2]))
+
+
+def _failing_main(rank, world, d, q):
+    """Rank 1's third peer-read step fails right after it queued its first
+    flag write ($CBX_FAULT_PEER_FAIL="1:3")."""
+    import time
+    rank_env(rank)
+    os.environ["CBX_FAULT_PEER_FAIL"] = "1:3"  # read at context creation
+
+    def mark(what):  # each rank's progress, for the report if a rank never arrives
+        with open(os.path.join(d, f"progress_{rank}"), "a") as f:
+            f.write(f"{time.monotonic():.3f} {what}\n")
+
+    try:
+        L, A = load_real()
+        g = C.init_rank(L, A, rank, world, share_uid(L, rank, os.path.join(d, "uid")))
+        out = {"errors": {}}
+        try:
+            n, nb = 1 << 22, 5
+            C.setup_model(g, A, n, 2, 0.9, 7, A.SYNC_BSP, 2 * world * 2)
+            exchange(g, rank, world, d, "fail")
+            g("cbx_set_allreduce_algorithm", PEER)
+            g("cbx_set_bucket_elements", -(-n // nb))
+            g("cbx_fill_synthetic", 5)
+
+            def step(clock):
+                g("cbx_lock_any")
+                try:
+                    g("cbx_synchronise", 0, clock, 0, 0)
+                finally:
+                    g("cbx_unlock_any")
+
+            for clock in (1, 2, 3):
+                try:
+                    step(clock)
+                    mark(f"step {clock} enqueued")
+                except RuntimeError as e:
+                    out["errors"][clock] = str(e)
+                    mark(f"step {clock} refused: {e}")
+            t0 = time.monotonic()
+            g("cbx_wait")  # every rank's streams drain: no wait is left on a flag that never comes
+            out["drain_s"] = time.monotonic() - t0
+            mark("drained")
+            if rank == 1:
+                a, r, broken = _flag_words(d, 1, nb)
+                out["words"] = {"a_min": int(a.min()), "r_min": int(r.min()), "broken": broken}
+            with open(os.path.join(d, f"after3_{rank}"), "w"):
+                pass
+            try:
+                C.wait_files([os.path.join(d, f"after3_{r}") for r in range(world)])
+            except TimeoutError as e:
+                report = {r: open(os.path.join(d, f"progress_{r}")).read() if os.path.exists(
+                    os.path.join(d, f"progress_{r}")) else "(nothing)" for r in range(world)}
+                raise TimeoutError(f"{e}; progress: {report}") from None
+            try:  # the form is unusable on EVERY rank now, not only on the one that failed
+                step(4)
+                out["step4"] = None
+            except RuntimeError as e:
+                out["step4"] = str(e)
+            g("cbx_set_allreduce_algorithm", 0)  # the RCCL form still runs
+            step(5)
+            g("cbx_wait")
+        finally:
+            t0 = time.monotonic()
+            g.free()
+            out["free_s"] = time.monotonic() - t0
+        q.put((rank, out, None))
+    except Exception:  # pragma: no cover - reported to the parent
+        import traceback
+        q.put((rank, None, traceback.format_exc()))
+
+
+@pytest.mark.timeout(200)
+def test_peer_read_failed_step_releases_and_stops_every_rank():
+    # ADVICE r04: a rank whose peer-read step fails after queuing flag writes
+    # must leave its words at the release value (the queued writes of the
+    # step's sequence number land BEFORE the queued release), and every other
+    # rank must refuse its next step in the form instead of reading stale
+    # acc / D silently; nobody hangs, the RCCL form still runs, free is bounded.
+    world = 3
+    with tempfile.TemporaryDirectory(dir=C.loopback_dir()) as d:
+        res = _spawn(world, _failing_main, lambda r: (r, world, d), timeout=180)
+    assert "fault injection" in res[1]["errors"].get(3, ""), res[1]["errors"]
+    assert not res[0]["errors"] and not res[2]["errors"], (res[0]["errors"], res[2]["errors"])
+    w = res[1]["words"]
+    assert w["a_min"] >= IPC_RELEASE and w["r_min"] >= IPC_RELEASE and w["broken"] == 1, w
+    for r in range(world):
+        assert res[r]["step4"] and "failed part-way earlier" in res[r]["step4"], (r, res[r]["step4"])
+        assert res[r]["drain_s"] < 30 and res[r]["free_s"] < 70, (r, res[r]["drain_s"], res[r]["free_s"])
