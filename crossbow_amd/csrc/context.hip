@@ -187,6 +187,7 @@ int cbx_init_rank(cbx_context **out, int device, int nranks, int rank, const uns
 int cbx_free(cbx_context *c) {
   if (!c) return CBX_OK;
   c->pool.reset();  // the enqueue threads are idle between calls
+  (void)flush_task_waits(c);  // close_device drains the sync streams: updates on callers' streams too
   if (!c->devs.empty()) peer_close(c);  // before any arena goes: the other ranks may still read this one
   for (Replica *r : c->replicas) {
     if (r && r->client && r->local >= 0) {
@@ -519,6 +520,7 @@ static int synchronise_impl(cbx_context *c, int first, int clock, int autotune, 
   TraceRange trace(staged ? "cbx_synchronise_staged" : "cbx_synchronise");
   TRY(check_manager_q(c));
   if (first < 0 || first > c->size) return fail(CBX_ERR_INVALID, "first replica %d out of range", first);
+  TRY(flush_task_waits(c));  // the replicas' updates on callers' streams come first
   // executioncontext.c:2287-2315: SYNCHRONOUSEAMSGD (3) routes to SMA because
   // ELASTIC_AVERAGE is #undef'd; SMA is 7.  The other update models are not
   // this library's path.
@@ -691,6 +693,7 @@ int cbx_register_batchnorm_stats(cbx_context *c, int op, int elements, float *co
 // unlockAny releases it.
 int cbx_add_model(cbx_context *c) {
   TRY(check_manager(c));
+  TRY(flush_task_waits(c));
   if (c->R + 1 > cbx::kMaxReplicas) return fail(CBX_ERR_UNSUPPORTED, "at most %d replicas per device", cbx::kMaxReplicas);
   const int size_ = c->size + c->G;
   const int slot = c->R;  // id / G of every new replica
@@ -748,6 +751,7 @@ int cbx_add_model(cbx_context *c) {
 // of every device (ids size-G .. size-1).
 int cbx_del_model(cbx_context *c) {
   TRY(check_manager(c));
+  TRY(flush_task_waits(c));
   if (c->R <= 1) return fail(CBX_ERR_STATE, "cannot delete the last replica of a device");  // :511
   const int size_ = c->size - c->G;
   // crossbowThetaQueueShrink (:537): the slots leave the rotation first, so
@@ -935,6 +939,7 @@ static int replica_optimise_impl(cbx_context *c, int id, int task, void *stream)
   a.wd = conf.weightDecay;
   HIP_TRY(hipSetDevice(d.hip_id));
   hipStream_t st = stream ? reinterpret_cast<hipStream_t>(stream) : d.stream;
+  if (st == d.stream) TRY(flush_task_waits(c));  // in order after updates made on other streams
   cbx::LaunchConfig cfg = c->aux_cfg;
   cfg.num_cus = d.num_cus;
   cfg.blocks_per_cu = 0;
@@ -942,12 +947,9 @@ static int replica_optimise_impl(cbx_context *c, int id, int task, void *stream)
   // it (the reference's forward kernels wait on replica->updated).
   if (st != d.stream && d.step_event) HIP_TRY(hipStreamWaitEvent(st, d.step_event, 0));
   HIP_TRY(cbx::launch_sma_optimise(a, cfg, st, {}));
-  if (st != d.stream) {
-    // sma.cu:79-81: the synchronisation stream waits for the updated replica.
-    if (!r.client) HIP_TRY(hipEventCreateWithFlags(&r.client, hipEventDisableTiming));
-    HIP_TRY(hipEventRecord(r.client, st));
-    HIP_TRY(hipStreamWaitEvent(d.stream, r.client, 0));
-  }
+  // sma.cu:79-81: the synchronisation stream waits for the updated replica,
+  // from its next use by the library on (flush_task_waits).
+  if (st != d.stream) TRY(defer_task_wait(d, st));
   return CBX_OK;
 }
 
@@ -955,6 +957,34 @@ static int replica_optimise_impl(cbx_context *c, int id, int task, void *stream)
 }  // extern "C"
 
 namespace cbx::host {
+
+int defer_task_wait(Device &d, hipStream_t st) {
+  std::lock_guard<std::mutex> l(*d.task_mu);
+  auto it = std::find_if(d.task_waits.begin(), d.task_waits.end(),
+                         [st](const Device::TaskWait &w) { return w.stream == st; });
+  if (it == d.task_waits.end()) {
+    hipEvent_t e = nullptr;
+    HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    d.task_waits.push_back({st, e, false});
+    it = d.task_waits.end() - 1;
+  }
+  HIP_TRY(hipEventRecord(it->event, st));
+  it->pending = true;
+  return CBX_OK;
+}
+
+int flush_task_waits(cbx_context *c) {
+  for (Device &d : c->devs) {
+    std::lock_guard<std::mutex> l(*d.task_mu);
+    for (Device::TaskWait &w : d.task_waits)
+      if (w.pending) {
+        HIP_TRY(hipSetDevice(d.hip_id));
+        HIP_TRY(hipStreamWaitEvent(d.stream, w.event, 0));
+        w.pending = false;
+      }
+  }
+  return CBX_OK;
+}
 
 int grow_device_buffer(void **p, size_t *have, size_t need) {
   if (*have >= need) return CBX_OK;
@@ -1249,6 +1279,7 @@ int cbx_base_buffer(cbx_context *c, int g, int kind, void **dev_ptr) {
 static int copy_io(cbx_context *c, Device *d, void *dst, const void *src, size_t bytes, hipMemcpyKind kind) {
   if (bytes != (size_t)c->n * 4)
     return fail(CBX_ERR_INVALID, "buffer is %lld bytes, got %zu", (long long)c->n * 4, bytes);
+  TRY(flush_task_waits(c));
   HIP_TRY(hipSetDevice(d->hip_id));
   HIP_TRY(hipStreamSynchronize(d->stream));
   HIP_TRY(hipMemcpy(dst, src, bytes, kind));
@@ -1287,6 +1318,7 @@ int cbx_base_read(cbx_context *c, int g, int kind, void *dst, size_t bytes) {
 int cbx_stage_in(cbx_context *c) {
   TraceRange trace("cbx_stage_in");
   TRY(check_manager(c));
+  TRY(flush_task_waits(c));
   TRY(alloc_host_mirror(c));
   const size_t bytes = (size_t)c->n * 4;
   for (Device &d : c->devs) {
@@ -1308,6 +1340,7 @@ int cbx_stage_in(cbx_context *c) {
 int cbx_stage_out(cbx_context *c) {
   TraceRange trace("cbx_stage_out");
   TRY(check_manager(c));
+  TRY(flush_task_waits(c));
   TRY(alloc_host_mirror(c));
   const size_t bytes = (size_t)c->n * 4;
   for (Device &d : c->devs) {
@@ -1345,6 +1378,7 @@ int cbx_base_host_buffer(cbx_context *c, int g, int kind, void **host_ptr) {
 
 int cbx_wait(cbx_context *c) {
   TRY(check_ctx_q(c));
+  TRY(flush_task_waits(c));
   for (Device &d : c->devs) {
     HIP_TRY(hipSetDevice(d.hip_id));
     HIP_TRY(hipStreamSynchronize(d.stream));
@@ -1623,6 +1657,7 @@ int cbx_set_force_split(cbx_context *c, int force) {
 
 int cbx_fill_synthetic(cbx_context *c, unsigned long long seed) {
   TRY(check_manager(c));
+  TRY(flush_task_waits(c));
   const int64_t n = c->n;
   for (Device &d : c->devs) {
     HIP_TRY(hipSetDevice(d.hip_id));

@@ -337,6 +337,22 @@ struct Device {
   hipStream_t a_stream = nullptr;
   hipStream_t a_stream2 = nullptr;
   std::vector<hipEvent_t> bucket_b;
+  // The sync stream's wait for replica updates made on callers' streams
+  // (cbx_replica_optimise with a stream of its own: sma.cu:79-81), deferred
+  // to the next operation of the library on this device (flush_task_waits):
+  // per caller stream an event recorded after its latest update.  A wait
+  // queued at once stays pending on the sync stream's hardware queue while
+  // the update runs, and a kernel on a hardware queue of its own runs about a
+  // third slower while another queue of the process holds a wait on it
+  // (scripts/queue_wait_probe.hip).  Task threads add entries
+  // concurrently, hence the lock.
+  struct TaskWait {
+    hipStream_t stream;
+    hipEvent_t event;
+    bool pending;
+  };
+  std::vector<TaskWait> task_waits;
+  std::unique_ptr<std::mutex> task_mu = std::make_unique<std::mutex>();
   hipEvent_t cross_entry = nullptr;
   float *decision = nullptr;           // 2 floats: the Phase-D decision, by step parity
   bool cross_valid = false;            // the last step was cross-pipelined ...
@@ -821,6 +837,8 @@ inline void close_device(Device &d) {
   if (d.a_stream2) (void)hipStreamSynchronize(d.a_stream2);
   for (hipEvent_t e : d.bucket_b) (void)hipEventDestroy(e);
   if (d.cross_entry) (void)hipEventDestroy(d.cross_entry);
+  for (Device::TaskWait &w : d.task_waits) (void)hipEventDestroy(w.event);
+  d.task_waits.clear();
   for (auto &pool : d.ord_pool)
     for (hipEvent_t e : pool) (void)hipEventDestroy(e);
   if (d.peer_a) (void)hipEventDestroy(d.peer_a);
@@ -1021,6 +1039,12 @@ int alloc_host_mirror(cbx_context *c);
 // Stream-order check of one recorded step, and of two consecutive ones.
 int check_order_step(const Device::OrderStep &o);
 int check_order_pair(const Device::OrderStep &p, const Device::OrderStep &q);
+// A replica update enqueued on a caller's stream `st`: the sync stream must
+// wait for it before the library next uses the replica (defer_task_wait), and
+// does so at its next operation on the device (flush_task_waits).
+int defer_task_wait(Device &d, hipStream_t st);
+int flush_task_waits(cbx_context *c);
+
 // The per-rank peer-read form's handles (cbx_peer_export / _import) and its
 // teardown (cbx_free: waits until every rank is done with this rank's memory).
 int peer_export(cbx_context *c, void *blob, size_t *bytes);
