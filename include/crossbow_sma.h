@@ -243,7 +243,11 @@ int cbx_replica_set_disabled (cbx_context *ctx, int id, int flag);
  * averages.  The learning rate comes from the replica's solver
  * configuration (may raise its _copy flag, solverconfiguration.c:133,147).
  * Enqueued on `stream` (a hipStream_t; NULL = the replica device's sync
- * stream); the sync stream then waits for it (sma.cu:79-81).  Nesterov
+ * stream); the sync stream waits for it (sma.cu:79-81) from the library's
+ * next call that works on the device (synchronise, wait, staging, reads,
+ * writes, add / del, free): the wait is queued then, not at once, so it is
+ * not pending on another hardware queue while the update runs.
+ * Nesterov
  * momentum is CBX_ERR_UNSUPPORTED, as in the reference (sma.cu:46-48).
  * Under update model WORKER the step is crossbowKernelOptimiserSynchronousSGD
  * (synchronoussgd.cu:3-56) instead: weight decay, then the lr-scaled
@@ -420,16 +424,17 @@ int cbx_set_allreduce_algorithm (cbx_context *ctx, int algorithm);
  *   1. cbx_peer_export(ctx, blob, &bytes) writes this rank's handles into
  *      `blob` (CBX_PEER_BLOB_BYTES): the IPC handles (hipIpcGetMemHandle)
  *      of its acc and D buffers, which move out of the model arena into
- *      allocations of their own (at most 512 MiB each: an IPC open of a 2 GB
- *      allocation hung under HIP 7.0; CBX_ERR_UNSUPPORTED above); rank 0
+ *      allocations of their own (below 2 GiB - 2 MiB each: ROCm 7.0's IPC
+ *      keeps an allocation's size in 32 bits, and an open of 2 GiB or more
+ *      never returns; CBX_ERR_UNSUPPORTED above); rank 0
  *      also creates the page of completion flags (POSIX shared memory) and
  *      names it in its blob;
  *   2. the caller gathers every rank's blob, in rank order, over its own
  *      control plane (bench.py: gloo all_gather);
  *   3. cbx_peer_import(ctx, blobs, nranks) maps every other rank's acc and
- *      D (hipIpcOpenMemHandle; the ranks open in turn, the others waiting
- *      inside a HIP call; a rank that has not opened its handles 120 s into
- *      the import fails everyone's import) and pins the flag page
+ *      D (hipIpcOpenMemHandle; the ranks open in turn; a rank that has not
+ *      opened its handles 120 s into the import fails everyone's import) and
+ *      pins the flag page
  *      (hipHostRegister).
  * Then CBX_ALLREDUCE_PEER is accepted.  The ranks' streams order each
  * other through the flags: a rank writes the step's sequence number after
@@ -437,9 +442,15 @@ int cbx_set_allreduce_algorithm (cbx_context *ctx, int algorithm);
  * wait for it (hipStreamWaitValue64 >=); the pipeline, its modes, strides,
  * groups and the sums' device order are the single-process form's.  Same
  * results bit for bit.  At most 4096 buckets.  cbx_free then waits (up to
- * 60 s) until every rank is done with this rank's memory.  Every rank calls
- * export, import and free; a step that fails part-way releases the other
- * ranks' waits and leaves the form unusable (CBX_ERR_STATE).             */
+ * 60 s in all, streams polled) until every rank is done with this rank's
+ * memory; if a dead peer left this rank's streams waiting, it writes the
+ * release into every rank's flags itself.  Every rank calls export, import
+ * and free.  A step that fails part-way, on any rank, releases that rank's
+ * flags (from the host and behind its queued flag writes) and marks it
+ * broken on the page; every rank then refuses further steps in this form
+ * (CBX_ERR_STATE, releasing its own flags too), so no stream waits forever
+ * and no rank reads a failed rank's stale buffers.  The other collective
+ * forms keep working.                                                     */
 #define CBX_PEER_BLOB_BYTES 256
 int cbx_peer_export (cbx_context *ctx, void *blob, size_t *bytes);
 int cbx_peer_import (cbx_context *ctx, const void *blobs, int nranks);
