@@ -140,6 +140,7 @@ def parse():
     p.add_argument("--peer-ipc-deadline", type=float, default=300.0,
                    help="watchdog deadline (s, times --watchdog-scale) of the peer-read form's IPC mapping")
     p.add_argument("--watchdog-selftest-result", type=float, default=0.0, help=argparse.SUPPRESS)
+    p.add_argument("--selftest-raise", action="store_true", help=argparse.SUPPRESS)
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
                    help="PMC-derived HBM bytes per launch (written by scripts/pmc_traffic.py)")
     return p.parse_args()
@@ -215,8 +216,23 @@ class Watchdog:
         with self.lock:
             self.deadline = None
 
-    def _line(self, phase, secs, done):
-        """The published line with the phase that missed its deadline."""
+    def fail_now(self, error: str) -> None:
+        """A phase after the first timed region raised: print the published
+        line (rank 0) naming the phase and the error, and leave with 0, as
+        for a missed deadline.  Before the line exists, re-raise instead."""
+        with self.lock:
+            phase, done, published = self.phase, self.last_done, self.result is not None
+            self.deadline = None
+        if not published:
+            raise
+        sys.stderr.write(f"[bench] rank {self.rank}: phase '{phase}' failed: {error}\n")
+        sys.stderr.flush()
+        if self.rank == 0:
+            print(self._line(phase, 0.0, done, error), file=self.out, flush=True)
+        os._exit(0)
+
+    def _line(self, phase, secs, done, error=None):
+        """The published line with the phase that missed its deadline (or raised)."""
         import copy
         for _ in range(5):  # the main thread may be adding a key right now
             try:
@@ -226,13 +242,14 @@ class Watchdog:
                 time.sleep(0.05)
         else:
             r = {k: self.result[k] for k in ("metric", "value", "unit") if k in self.result}
+        how = f"raised {error}" if error else f"missed its {secs:.0f} s deadline"
         r["incomplete_phase"] = {
-            "phase": phase, "deadline_s": round(secs, 1), "last_completed": done,
-            "note": "this phase came after the timed region that set `value` and missed its deadline; the run "
-                    "ended here (bench.py watchdog), so later fields are absent"}
+            "phase": phase, "deadline_s": None if error else round(secs, 1), "error": error, "last_completed": done,
+            "note": f"this phase came after the timed region that set `value` and {how}; the run ended here "
+                    "(bench.py), so later fields are absent"}
         c = r.get("config", {})
         if "IPC mapping" in str(phase) and c.get("peer_ipc") in ("mapping", "pending (after the timed region)", None):
-            c["peer_ipc"] = f"failed: '{phase}' missed its {secs:.0f} s deadline (watchdog)"
+            c["peer_ipc"] = f"failed: '{phase}' {how}" + ("" if error else " (watchdog)")
         return json.dumps(r)
 
     def _watch(self) -> None:
@@ -880,11 +897,17 @@ def main():
     sys.stdout.flush()
     result_out = os.fdopen(os.dup(1), "w")
     os.dup2(2, 1)
-    if args.watchdog_selftest_result > 0:
+    if args.watchdog_selftest_result > 0 or args.selftest_raise:
         # CPU test: a line is assembled (as after the first timed region),
-        # then a later phase stalls; the watchdog must print that line
+        # then a later phase stalls (or raises); that line must still come out
         wd = Watchdog(1.0, 0)
         wd.publish({"metric": METRIC, "value": 1.0, "unit": "GB/s", "config": {"peer_ipc": "mapping"}}, result_out)
+        if args.selftest_raise:
+            wd.enter("peer-read IPC mapping", 60)
+            try:
+                raise RuntimeError("selftest: a later phase raised")
+            except Exception as e:  # noqa: BLE001
+                wd.fail_now(f"{type(e).__name__}: {e}")
         wd.enter("selftest post-timed stall", args.watchdog_selftest_result)
         time.sleep(args.watchdog_selftest_result * 20 + 10)
         raise SystemExit("watchdog did not fire")
@@ -1073,162 +1096,107 @@ def main():
     # From here on the line exists: a later phase that misses its deadline
     # makes the watchdog print it (with `incomplete_phase`) instead of nothing.
     wd.publish(result, result_out)
-    if G > 1:
-        wd.enter("cross-GPU identity of z and last", 180)
-        result["identity"] = block_identity(gpu, world, step, chosen, one_bucket, peer_only, ALLREDUCE_PEER, wd)
+    try:
+        if G > 1:
+            wd.enter("cross-GPU identity of z and last", 180)
+            result["identity"] = block_identity(gpu, world, step, chosen, one_bucket, peer_only, ALLREDUCE_PEER, wd)
 
-    reported = chosen
-    if per_rank and split and not explicit and not args.no_peer_ipc:
-        # The per-rank peer-read form, as a second block after the RCCL forms'.
-        result["config"]["peer_ipc"] = "mapping"
-        wd.enter("peer-read IPC mapping", args.peer_ipc_deadline)
-        why = D.setup_peer(gpu, world)
-        result["config"]["peer_ipc"] = peer_ipc = why or "mapped"
-        if why is None:
-            ptuning = D.tune_buckets(gpu, n, world, step,
-                                     progress=(lambda m: log(f"[bench] {m}")) if rank == 0 else None,
-                                     ndev=G, peer=True, peer_only=True, threads=False,
-                                     steps=max(1, args.tune_steps), passes=max(1, args.tune_passes),
-                                     warmup=min(2, max(1, args.tune_steps)),
-                                     phase=lambda name: wd.enter(name, 90))
-            best_rccl, best_peer = min(tuning.table.values()), min(ptuning.table.values())
-            pchosen = dict(chosen, bucket_elements=ptuning.bucket_elements, buckets=ptuning.buckets,
-                           mode=ptuning.mode, stride=ptuning.stride, group=ptuning.group,
-                           algorithm=ptuning.algorithm)
-            if best_peer < best_rccl:
-                # the tuner's best peer-read candidate beat RCCL's best: time it
-                pblk = timed_block(gpu, torch, D, args, world, step, wd, refill=True, label=" (peer-read form)")
-                pfields = block_fields(gpu, D, args, world, n, G, nlocal, split, pblk, pchosen, ptuning, calib,
-                                       args.rehearse_one_gpu)
-                wd.enter("cross-GPU identity of z and last (peer-read form)", 180)
-                pident = block_identity(gpu, world, step, pchosen, one_bucket, False, ALLREDUCE_PEER, wd)
-                if pfields["value"] > result["value"] and pident.get("trusted", False):
-                    other = block_summary({k: result[k] for k in pfields}, result["identity"])
-                    merge_block(result, pfields)
-                    result["identity"] = pident
-                    result["other_form"] = other
-                    reported = pchosen
+        reported = chosen
+        if per_rank and split and not explicit and not args.no_peer_ipc:
+            # The per-rank peer-read form, as a second block after the RCCL forms'.
+            result["config"]["peer_ipc"] = "mapping"
+            wd.enter("peer-read IPC mapping", args.peer_ipc_deadline)
+            why = D.setup_peer(gpu, world)
+            result["config"]["peer_ipc"] = peer_ipc = why or "mapped"
+            if why is None:
+                ptuning = D.tune_buckets(gpu, n, world, step,
+                                         progress=(lambda m: log(f"[bench] {m}")) if rank == 0 else None,
+                                         ndev=G, peer=True, peer_only=True, threads=False,
+                                         steps=max(1, args.tune_steps), passes=max(1, args.tune_passes),
+                                         warmup=min(2, max(1, args.tune_steps)),
+                                         phase=lambda name: wd.enter(name, 90))
+                best_rccl, best_peer = min(tuning.table.values()), min(ptuning.table.values())
+                pchosen = dict(chosen, bucket_elements=ptuning.bucket_elements, buckets=ptuning.buckets,
+                               mode=ptuning.mode, stride=ptuning.stride, group=ptuning.group,
+                               algorithm=ptuning.algorithm)
+                if best_peer < best_rccl:
+                    # the tuner's best peer-read candidate beat RCCL's best: time it
+                    pblk = timed_block(gpu, torch, D, args, world, step, wd, refill=True, label=" (peer-read form)")
+                    pfields = block_fields(gpu, D, args, world, n, G, nlocal, split, pblk, pchosen, ptuning, calib,
+                                           args.rehearse_one_gpu)
+                    wd.enter("cross-GPU identity of z and last (peer-read form)", 180)
+                    pident = block_identity(gpu, world, step, pchosen, one_bucket, False, ALLREDUCE_PEER, wd)
+                    if pfields["value"] > result["value"] and pident.get("trusted", False):
+                        other = block_summary({k: result[k] for k in pfields}, result["identity"])
+                        merge_block(result, pfields)
+                        result["identity"] = pident
+                        result["other_form"] = other
+                        reported = pchosen
+                    else:
+                        result["other_form"] = block_summary(pfields, pident)
                 else:
-                    result["other_form"] = block_summary(pfields, pident)
-            else:
-                result["other_form"] = {
-                    "config": {"allreduce_algorithm": "peer-read two-shot",
-                               "bucket_tuning_ms_per_step": ptuning.table, "tuning_errors": ptuning.errors},
-                    "timed": (f"not timed: the tuner's best peer-read candidate ({best_peer:.4f} ms per step) was "
-                              f"slower than RCCL's best ({best_rccl:.4f} ms)")}
-        apply_config(gpu, reported, single)
-    ar_algo = reported["algorithm"]
+                    result["other_form"] = {
+                        "config": {"allreduce_algorithm": "peer-read two-shot",
+                                   "bucket_tuning_ms_per_step": ptuning.table, "tuning_errors": ptuning.errors},
+                        "timed": (f"not timed: the tuner's best peer-read candidate ({best_peer:.4f} ms per step) was "
+                                  f"slower than RCCL's best ({best_rccl:.4f} ms)")}
+            apply_config(gpu, reported, single)
+        ar_algo = reported["algorithm"]
 
-    if G > 1:
-        # Host side of the step (lockAny + synchronise + unlockAny, every local
-        # device's enqueue) against the device's step: the single-process form
-        # enqueues all G devices' kernels and collectives from one thread.
-        wd.enter("host enqueue (idle GPU)", 120)
-        idle = []
-        for _ in range(5):
-            gpu.wait()
-            h0 = time.perf_counter()
-            step()
-            idle.append((time.perf_counter() - h0) * 1e3)
-        gpu.wait()
-        result["host"].update(
-            enqueue_ms_per_step_idle_gpu=round(statistics.median(idle), 4),
-            note="perf_counter around lockAny+synchronise+unlockAny; 'idle_gpu' after a wait, so no queue "
-                 "back-pressure; host-bound when it exceeds ms_per_step")
-    if args.rehearse_one_gpu:
-        result["rehearsal"] = (f"{G} ranks on ONE GPU over RCCL's socket transport (NCCL_HOSTID per rank): "
-                               "a check of the N > 1 code path, not an N-GPU measurement" if not single else
-                               f"{G} devices of one process that are all device 0, peer-read all-reduce (RCCL "
-                               "refuses a repeated device): the single-process form's host side and code path, "
-                               "not an N-GPU measurement")
-    if split and rccl_log:
-        gpu.wait()
-        result["allreduce"]["rccl_tuning"] = rccl_tuning(rccl_log)
-        try:
-            os.remove(rccl_log)
-        except OSError:
-            pass
-        result["allreduce"]["rccl_tuning_source"] = (
-            "RCCL's own log (NCCL_DEBUG=INFO, NCCL_DEBUG_SUBSYS=TUNING) of THIS run (--rccl-tuning-log): every "
-            "collective of calibration, tuning and the timed region")
-
-    step_bytes, _ = alg_bytes(n, args.replicas, args.momentum, 2 if split else 1)
-    if G > 1 and not args.no_staged and peer_only:
-        result["host_staged"] = {"skipped": "the host-staged step's collective is RCCL's, which refuses a repeated device"}
-    elif G > 1 and not args.no_staged:
-        # Host-staged rate at N > 1 (north_star: the path starts and ends in
-        # host memory): each GPU's replicas live in its own pinned mirror and
-        # cross its own PCIe link; zero-copy staging kernels, kernel A /
-        # all-reduce / kernel B per bucket.  Max over ranks of the median of 3.
-        # The pinned mirror is allocated first (no collective); every rank
-        # must have one before any rank enters the staged step's collectives.
-        wd.enter("host-staged step", 300)
-        why = None
-        try:
-            gpu.stage_in()
-            gpu.wait()
-        except CbxError as e:
-            why = str(e)
-        if D.max_over_ranks(0.0 if why is None else 1.0, world) > 0.0:
-            result["host_staged"] = {"skipped": f"pinned host mirror unavailable on some rank ({why or 'another rank'})"}
-        else:
-            gpu.set_staging_mode(_lib.STAGING_ZEROCOPY)
-            runs = []
-            for _ in range(3):
-                clock += 1
-                gpu.lockAny()
-                gpu.synchronise_staged(0, clock, 0, args.staged_buckets)
-                gpu.unlockAny()
+        if G > 1:
+            # Host side of the step (lockAny + synchronise + unlockAny, every local
+            # device's enqueue) against the device's step: the single-process form
+            # enqueues all G devices' kernels and collectives from one thread.
+            wd.enter("host enqueue (idle GPU)", 120)
+            idle = []
+            for _ in range(5):
                 gpu.wait()
-                runs.append(max(gpu.last_timing(k)[_lib.T_STEP] for k in range(nlocal)))
-            ms = D.max_over_ranks(sorted(runs)[1], world)
-            result["host_staged"] = {"zerocopy": {
-                "buckets": args.staged_buckets, "step_ms": round(ms, 3),
-                "end_to_end_GBs": round(step_bytes * G / (ms * 1e-3) / 1e9, 2),
-                "per_gpu_GBs": round(step_bytes / (ms * 1e-3) / 1e9, 2),
-                "timed": "HIP events per device (staged step: host in, host and device out), max over devices"}}
-
-    if rank == 0 and G == 1 and not args.no_optimiser:
-        wd.enter("replica optimiser step", 120)
-        result["replica_optimiser"] = bench_optimiser(gpu, torch, n, args)
-    if rank == 0 and G == 1 and not args.no_seam:
-        wd.enter("sma.c seam", 180)
-        result["seam"] = bench_seam(torch, n, args)
-
-    if rank == 0 and G == 1:
-        if not args.no_copy_ceiling:
-            wd.enter("copy ceiling", 120)
-            result["copy_ceiling_GBs"] = round(gpu.bench_copy(1 << 30, 20), 1)
-        if not args.no_staged:
-            # Host-staged rate (north_star): pinned H2D of z, last, s_i, w_i,
-            # the step, pinned D2H of z, last, w_i.  Reported, never `value`.
-            wd.enter("host-staged step", 300)
-            samples = []
-            for _ in range(3):
-                gpu.stage_in()
+                h0 = time.perf_counter()
                 step()
-                gpu.stage_out()
+                idle.append((time.perf_counter() - h0) * 1e3)
+            gpu.wait()
+            result["host"].update(
+                enqueue_ms_per_step_idle_gpu=round(statistics.median(idle), 4),
+                note="perf_counter around lockAny+synchronise+unlockAny; 'idle_gpu' after a wait, so no queue "
+                     "back-pressure; host-bound when it exceeds ms_per_step")
+        if args.rehearse_one_gpu:
+            result["rehearsal"] = (f"{G} ranks on ONE GPU over RCCL's socket transport (NCCL_HOSTID per rank): "
+                                   "a check of the N > 1 code path, not an N-GPU measurement" if not single else
+                                   f"{G} devices of one process that are all device 0, peer-read all-reduce (RCCL "
+                                   "refuses a repeated device): the single-process form's host side and code path, "
+                                   "not an N-GPU measurement")
+        if split and rccl_log:
+            gpu.wait()
+            result["allreduce"]["rccl_tuning"] = rccl_tuning(rccl_log)
+            try:
+                os.remove(rccl_log)
+            except OSError:
+                pass
+            result["allreduce"]["rccl_tuning_source"] = (
+                "RCCL's own log (NCCL_DEBUG=INFO, NCCL_DEBUG_SUBSYS=TUNING) of THIS run (--rccl-tuning-log): every "
+                "collective of calibration, tuning and the timed region")
+
+        step_bytes, _ = alg_bytes(n, args.replicas, args.momentum, 2 if split else 1)
+        if G > 1 and not args.no_staged and peer_only:
+            result["host_staged"] = {"skipped": "the host-staged step's collective is RCCL's, which refuses a repeated device"}
+        elif G > 1 and not args.no_staged:
+            # Host-staged rate at N > 1 (north_star: the path starts and ends in
+            # host memory): each GPU's replicas live in its own pinned mirror and
+            # cross its own PCIe link; zero-copy staging kernels, kernel A /
+            # all-reduce / kernel B per bucket.  Max over ranks of the median of 3.
+            # The pinned mirror is allocated first (no collective); every rank
+            # must have one before any rank enters the staged step's collectives.
+            wd.enter("host-staged step", 300)
+            why = None
+            try:
+                gpu.stage_in()
                 gpu.wait()
-                samples.append(gpu.last_timing(0))
-            t = sorted(samples, key=lambda x: x[_lib.T_H2D] + x[_lib.T_KERNEL] + x[_lib.T_D2H])[1]
-            m = 1 if args.momentum > 0 else 0
-            h2d = (2 * args.replicas + 1 + m) * 4 * n
-            d2h = (args.replicas + 1 + m) * 4 * n
-            tot = (t[_lib.T_H2D] + t[_lib.T_KERNEL] + t[_lib.T_D2H]) * 1e-3
-            result["host_staged"] = {
-                "h2d_ms": round(t[_lib.T_H2D], 3), "kernel_ms": round(t[_lib.T_KERNEL], 4),
-                "d2h_ms": round(t[_lib.T_D2H], 3),
-                "h2d_GBs": round(h2d / (t[_lib.T_H2D] * 1e-3) / 1e9, 2),
-                "d2h_GBs": round(d2h / (t[_lib.T_D2H] * 1e-3) / 1e9, 2),
-                "end_to_end_GBs": round(step_bytes / tot / 1e9, 2),
-            }
-            # The same step through cbx_synchronise_staged, both staging modes:
-            # DMA (uploads, kernels and downloads pipelined over buckets on
-            # three streams) and zero-copy (the kernels read and write the
-            # pinned mirror over PCIe themselves; the library default).
-            def staged(mode):
-                nonlocal clock
-                gpu.set_staging_mode(mode)
+            except CbxError as e:
+                why = str(e)
+            if D.max_over_ranks(0.0 if why is None else 1.0, world) > 0.0:
+                result["host_staged"] = {"skipped": f"pinned host mirror unavailable on some rank ({why or 'another rank'})"}
+            else:
+                gpu.set_staging_mode(_lib.STAGING_ZEROCOPY)
                 runs = []
                 for _ in range(3):
                     clock += 1
@@ -1236,54 +1204,114 @@ def main():
                     gpu.synchronise_staged(0, clock, 0, args.staged_buckets)
                     gpu.unlockAny()
                     gpu.wait()
-                    runs.append(gpu.last_timing(0))
-                return sorted(runs, key=lambda x: x[_lib.T_STEP])[1]
-            p = staged(_lib.STAGING_DMA)
-            result["host_staged"]["pipelined"] = {
-                "buckets": args.staged_buckets, "step_ms": round(p[_lib.T_STEP], 3),
-                "h2d_ms": round(p[_lib.T_H2D], 3), "d2h_ms": round(p[_lib.T_D2H], 3),
-                "end_to_end_GBs": round(step_bytes / (p[_lib.T_STEP] * 1e-3) / 1e9, 2),
-                "timed": "HIP events: sync stream at entry to sync stream after the last download"}
-            z = staged(_lib.STAGING_ZEROCOPY)
-            result["host_staged"]["zerocopy"] = {
-                "step_ms": round(z[_lib.T_STEP], 3),
-                "end_to_end_GBs": round(step_bytes / (z[_lib.T_STEP] * 1e-3) / 1e9, 2),
-                "pcie_GBs_both_ways": round((h2d + d2h) / (z[_lib.T_STEP] * 1e-3) / 1e9, 2),
-                "timed": "HIP events on the fused staged kernel's own dispatch (one launch: host in, host + device out)"}
-        if not args.no_cpu_baseline:
-            # multithreaded first: OpenBLAS's pool must not start out bound to core 0
-            wd.enter("CPU baseline", 4 * args.cpu_seconds + 240)
-            threads = max(1, min(16, len(os.sched_getaffinity(0))))
-            mt = cpu_baseline_threads(args, n, threads)
-            result["cpu_baseline"] = cpu_baseline(args, n)
-            result["cpu_baseline"]["cpu_model"] = mt["cpu_model"] = cpu_model()
-            result["cpu_baseline_multithread"] = mt
-            result["cpu_c1_lenet"] = cpu_c1()
-        else:
-            result["cpu_baseline"] = None
+                    runs.append(max(gpu.last_timing(k)[_lib.T_STEP] for k in range(nlocal)))
+                ms = D.max_over_ranks(sorted(runs)[1], world)
+                result["host_staged"] = {"zerocopy": {
+                    "buckets": args.staged_buckets, "step_ms": round(ms, 3),
+                    "end_to_end_GBs": round(step_bytes * G / (ms * 1e-3) / 1e9, 2),
+                    "per_gpu_GBs": round(step_bytes / (ms * 1e-3) / 1e9, 2),
+                    "timed": "HIP events per device (staged step: host in, host and device out), max over devices"}}
 
-    wd.enter("free", 120)
-    gpu.free()
-    if split and G > 1 and not rccl_log:
-        # RCCL's algorithm / protocol / channel choices, from a separate short
-        # run of the chosen configuration with RCCL's tuning log on (rank 0
-        # launches it once this run's buffers are freed; the others wait).
-        if peer_only or ar_algo == ALLREDUCE_PEER:
-            entries, source = None, "no RCCL collective in the chosen form"
-        elif args.no_rccl_tuning_run:
-            entries, source = None, "--no-rccl-tuning-run"
-        elif args.rehearse_one_gpu and not single and 2 * G + 2 > 16:
-            # the separate run's ranks would join this run's on the one GPU
-            entries, source = None, f"not run: a {G}-rank rehearsal plus {G} more ranks exceeds 16 processes on one GPU"
-        elif rank == 0:
-            entries, source = rccl_tuning_run(args, G, single, reported, wd)
-        else:
-            wd.enter("rccl tuning run (rank 0's)", 420)
-            entries, source = None, None
-        if world > 1:
-            D.barrier(world)
-        result["allreduce"]["rccl_tuning"] = entries
-        result["allreduce"]["rccl_tuning_source"] = source
+        if rank == 0 and G == 1 and not args.no_optimiser:
+            wd.enter("replica optimiser step", 120)
+            result["replica_optimiser"] = bench_optimiser(gpu, torch, n, args)
+        if rank == 0 and G == 1 and not args.no_seam:
+            wd.enter("sma.c seam", 180)
+            result["seam"] = bench_seam(torch, n, args)
+
+        if rank == 0 and G == 1:
+            if not args.no_copy_ceiling:
+                wd.enter("copy ceiling", 120)
+                result["copy_ceiling_GBs"] = round(gpu.bench_copy(1 << 30, 20), 1)
+            if not args.no_staged:
+                # Host-staged rate (north_star): pinned H2D of z, last, s_i, w_i,
+                # the step, pinned D2H of z, last, w_i.  Reported, never `value`.
+                wd.enter("host-staged step", 300)
+                samples = []
+                for _ in range(3):
+                    gpu.stage_in()
+                    step()
+                    gpu.stage_out()
+                    gpu.wait()
+                    samples.append(gpu.last_timing(0))
+                t = sorted(samples, key=lambda x: x[_lib.T_H2D] + x[_lib.T_KERNEL] + x[_lib.T_D2H])[1]
+                m = 1 if args.momentum > 0 else 0
+                h2d = (2 * args.replicas + 1 + m) * 4 * n
+                d2h = (args.replicas + 1 + m) * 4 * n
+                tot = (t[_lib.T_H2D] + t[_lib.T_KERNEL] + t[_lib.T_D2H]) * 1e-3
+                result["host_staged"] = {
+                    "h2d_ms": round(t[_lib.T_H2D], 3), "kernel_ms": round(t[_lib.T_KERNEL], 4),
+                    "d2h_ms": round(t[_lib.T_D2H], 3),
+                    "h2d_GBs": round(h2d / (t[_lib.T_H2D] * 1e-3) / 1e9, 2),
+                    "d2h_GBs": round(d2h / (t[_lib.T_D2H] * 1e-3) / 1e9, 2),
+                    "end_to_end_GBs": round(step_bytes / tot / 1e9, 2),
+                }
+                # The same step through cbx_synchronise_staged, both staging modes:
+                # DMA (uploads, kernels and downloads pipelined over buckets on
+                # three streams) and zero-copy (the kernels read and write the
+                # pinned mirror over PCIe themselves; the library default).
+                def staged(mode):
+                    nonlocal clock
+                    gpu.set_staging_mode(mode)
+                    runs = []
+                    for _ in range(3):
+                        clock += 1
+                        gpu.lockAny()
+                        gpu.synchronise_staged(0, clock, 0, args.staged_buckets)
+                        gpu.unlockAny()
+                        gpu.wait()
+                        runs.append(gpu.last_timing(0))
+                    return sorted(runs, key=lambda x: x[_lib.T_STEP])[1]
+                p = staged(_lib.STAGING_DMA)
+                result["host_staged"]["pipelined"] = {
+                    "buckets": args.staged_buckets, "step_ms": round(p[_lib.T_STEP], 3),
+                    "h2d_ms": round(p[_lib.T_H2D], 3), "d2h_ms": round(p[_lib.T_D2H], 3),
+                    "end_to_end_GBs": round(step_bytes / (p[_lib.T_STEP] * 1e-3) / 1e9, 2),
+                    "timed": "HIP events: sync stream at entry to sync stream after the last download"}
+                z = staged(_lib.STAGING_ZEROCOPY)
+                result["host_staged"]["zerocopy"] = {
+                    "step_ms": round(z[_lib.T_STEP], 3),
+                    "end_to_end_GBs": round(step_bytes / (z[_lib.T_STEP] * 1e-3) / 1e9, 2),
+                    "pcie_GBs_both_ways": round((h2d + d2h) / (z[_lib.T_STEP] * 1e-3) / 1e9, 2),
+                    "timed": "HIP events on the fused staged kernel's own dispatch (one launch: host in, host + device out)"}
+            if not args.no_cpu_baseline:
+                # multithreaded first: OpenBLAS's pool must not start out bound to core 0
+                wd.enter("CPU baseline", 4 * args.cpu_seconds + 240)
+                threads = max(1, min(16, len(os.sched_getaffinity(0))))
+                mt = cpu_baseline_threads(args, n, threads)
+                result["cpu_baseline"] = cpu_baseline(args, n)
+                result["cpu_baseline"]["cpu_model"] = mt["cpu_model"] = cpu_model()
+                result["cpu_baseline_multithread"] = mt
+                result["cpu_c1_lenet"] = cpu_c1()
+            else:
+                result["cpu_baseline"] = None
+
+        wd.enter("free", 120)
+        gpu.free()
+        if split and G > 1 and not rccl_log:
+            # RCCL's algorithm / protocol / channel choices, from a separate short
+            # run of the chosen configuration with RCCL's tuning log on (rank 0
+            # launches it once this run's buffers are freed; the others wait).
+            if peer_only or ar_algo == ALLREDUCE_PEER:
+                entries, source = None, "no RCCL collective in the chosen form"
+            elif args.no_rccl_tuning_run:
+                entries, source = None, "--no-rccl-tuning-run"
+            elif args.rehearse_one_gpu and not single and 2 * G + 2 > 16:
+                # the separate run's ranks would join this run's on the one GPU
+                entries, source = None, f"not run: a {G}-rank rehearsal plus {G} more ranks exceeds 16 processes on one GPU"
+            elif rank == 0:
+                entries, source = rccl_tuning_run(args, G, single, reported, wd)
+            else:
+                wd.enter("rccl tuning run (rank 0's)", 420)
+                entries, source = None, None
+            if world > 1:
+                D.barrier(world)
+            result["allreduce"]["rccl_tuning"] = entries
+            result["allreduce"]["rccl_tuning_source"] = source
+    except Exception as e:  # noqa: BLE001 -- a later phase must not cost the measured line
+        import traceback
+        traceback.print_exc()
+        wd.fail_now(f"{type(e).__name__}: {e}")
     wd.stop()
     if rank == 0:
         print(json.dumps(result), file=result_out, flush=True)

@@ -202,3 +202,19 @@ def test_agreement_check_is_vacuous_at_blown_up_values():
     skewed = _FakeGpu([0.25, -0.1, 0.05], skew=1e-3)
     r = bench.form_agreement(skewed, 1, skewed.step, chosen, 1 << 62, "peer-read two-shot")
     assert r["vacuous"] is False and r["within_tolerance"] is False
+
+
+def test_a_later_phase_that_raises_still_prints_the_line():
+    # An exception in a phase after the first timed region (the peer-read
+    # form's mapping, its tuner, the host-staged leg, ...) ends the run with
+    # the measured line, naming the phase and the error, exit 0.
+    import json
+    p = subprocess.run([sys.executable, "bench.py", "--selftest-raise"], cwd=ROOT, capture_output=True, text=True,
+                       timeout=120)
+    assert p.returncode == 0, (p.returncode, p.stderr[-2000:])
+    lines = [ln for ln in p.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1, p.stdout
+    d = json.loads(lines[0])
+    inc = d["incomplete_phase"]
+    assert inc["phase"] == "peer-read IPC mapping" and "selftest: a later phase raised" in inc["error"], inc
+    assert d["config"]["peer_ipc"].startswith("failed: 'peer-read IPC mapping' raised RuntimeError"), d["config"]
