@@ -673,13 +673,15 @@ struct SplitStep {
     rsag = c->allreduce_algo == CBX_ALLREDUCE_RSAG;
     peer = c->allreduce_algo == CBX_ALLREDUCE_PEER && c->G > 1;
     ipc = peer && c->per_rank;
+    if (c->ipc.ready && !c->ipc.released && any_rank_broken(c)) {
+      // Another rank's peer-read step failed part-way.  A rank that had
+      // already enqueued its next peer-read step waits on this rank's flags
+      // of it, which this rank will now never write (this step refuses the
+      // form, or takes another): release them, whatever form this step takes.
+      c->ipc.broken = true;
+      release_flags(c, c->ipc.max_nb);
+    }
     if (ipc) {
-      if (c->ipc.ready && !c->ipc.broken && any_rank_broken(c)) c->ipc.broken = true;  // another rank's step failed
-      if (c->ipc.ready && c->ipc.broken && !c->ipc.released) {
-        // Refusing this step: a rank that already enqueued it waits on this
-        // rank's flags of it, which this rank will now never write.
-        release_flags(c, c->ipc.max_nb);
-      }
       if (!c->ipc.ready || c->ipc.broken)
         return fail(CBX_ERR_STATE, c->ipc.broken ? "the per-rank peer-read form failed part-way earlier on this or "
                                                    "another rank (flags released)"

@@ -447,8 +447,9 @@ int cbx_set_allreduce_algorithm (cbx_context *ctx, int algorithm);
  * release into every rank's flags itself.  Every rank calls export, import
  * and free.  A step that fails part-way, on any rank, releases that rank's
  * flags (from the host and behind its queued flag writes) and marks it
- * broken on the page; every rank then refuses further steps in this form
- * (CBX_ERR_STATE, releasing its own flags too), so no stream waits forever
+ * broken on the page; every rank's next step (in any form) releases its own
+ * flags, and further steps in this form are refused (CBX_ERR_STATE), so no
+ * stream waits forever
  * and no rank reads a failed rank's stale buffers.  The other collective
  * forms keep working.                                                     */
 #define CBX_PEER_BLOB_BYTES 256
