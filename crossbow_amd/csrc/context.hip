@@ -80,15 +80,15 @@ int load_buffer(float *dev, size_t bytes, const std::string &path, std::vector<c
 }  // namespace
 
 
-// Hardware queues.  ROCclr maps a process's streams onto GPU_MAX_HW_QUEUES
-// hardware queues per device (default 4), shared once that many exist; a
-// stream wait queued on a shared queue holds back everything behind it.  A
-// device here has four streams of its own (sync, comm, two for kernels A),
-// created together in open_device so they take the first queues.  At HIP's
-// default 4 the bucket pipeline measured within 3 % of 16 queues on one GPU
-// (profiles/r04/hw_queues_ab.jsonl), so the library leaves the
-// setting to the deployment (16 recommended) and never
-// changes the process environment itself.
+// Hardware queues.  ROCclr maps a process's streams round robin onto
+// GPU_MAX_HW_QUEUES hardware queues per device (default 4).  A device here
+// has four streams of its own (sync, comm, two for kernels A), created
+// together in open_device so they take the first queues, which sit on four
+// distinct pipes.  With more than 4 queues a later stream (a caller's task
+// stream) lands on a pipe with one of them, and a stream wait pending on one
+// queue of a pipe slows kernels on the other by about a third;
+// so HIP's default 4 is the recommended setting, and the
+// library never changes the process environment itself.
 
 // ===========================================================================
 // C-ABI
