@@ -949,7 +949,7 @@ static int replica_optimise_impl(cbx_context *c, int id, int task, void *stream)
   HIP_TRY(cbx::launch_sma_optimise(a, cfg, st, {}));
   // sma.cu:79-81: the synchronisation stream waits for the updated replica,
   // from its next use by the library on (flush_task_waits).
-  if (st != d.stream) TRY(defer_task_wait(d, st));
+  if (st != d.stream && !c->fault_skip_task_wait) TRY(defer_task_wait(d, st));
   return CBX_OK;
 }
 

@@ -584,6 +584,11 @@ struct cbx_context {
   // inside hipIpcOpenMemHandle would (no timer of the library reaches it):
   // bench.py must still print its line (VERDICT r04 Next #1).
   int fault_ipc_stall_s = std::getenv("CBX_FAULT_IPC_STALL") ? std::atoi(std::getenv("CBX_FAULT_IPC_STALL")) : 0;
+  // $CBX_FAULT_SKIP_TASK_WAIT (tests only): cbx_replica_optimise on a
+  // caller's stream queues no wait for the sync stream at all, so a barrier
+  // right behind a busy task stream reads stale replicas (the test proves the
+  // deferred wait is what orders them).
+  bool fault_skip_task_wait = std::getenv("CBX_FAULT_SKIP_TASK_WAIT") != nullptr;
 
   static int fault_pair(const char *s, int which) {
     int v[2] = {-1, -1};

@@ -142,6 +142,96 @@ def test_clock_loop_bitexact(momentum):
         g.free()
 
 
+def _busy(torch, stream, ms=2.0):
+    """Hold `stream` for about `ms` milliseconds before whatever is queued next."""
+    with torch.cuda.stream(stream):
+        try:
+            torch.cuda._sleep(int(ms * 2.1e6))  # ~2.1 GHz shader clock
+        except (AttributeError, RuntimeError):
+            a = torch.randn(2048, 2048, device="cuda")
+            for _ in range(8):
+                a = a @ a * 1e-3
+
+
+def _busy_task_main(momentum, fault, q):
+    import os
+    # 16 hardware queues give every task stream a queue of its own: at HIP's
+    # default 4 a later stream can share the sync stream's queue, whose
+    # in-order execution would hide a missing wait (DESIGN.md 7)
+    os.environ["GPU_MAX_HW_QUEUES"] = "16"
+    if fault:
+        os.environ["CBX_FAULT_SKIP_TASK_WAIT"] = "1"  # read at context creation
+    try:
+        q.put((_busy_task_loop(momentum), None))
+    except Exception:  # pragma: no cover - reported to the parent
+        import traceback
+        q.put((None, traceback.format_exc()))
+
+
+@pytest.mark.parametrize("momentum", [0.0, 0.9])
+@pytest.mark.parametrize("fault", [False, True])
+def test_clock_loop_on_busy_task_streams_bitexact(momentum, fault):
+    # Each replica's optimiser step on a task stream of its own that is busy
+    # for ~2 ms before it, and the barrier enqueued at once behind them: the
+    # sync stream's wait for every task stream is deferred to the barrier's
+    # entry (flush_task_waits, DESIGN.md 7), so the averaging still reads the
+    # updated w and s, bit for bit.  With the waits dropped
+    # ($CBX_FAULT_SKIP_TASK_WAIT) the same loop must come out wrong: the
+    # check is sensitive to the ordering it relies on.  A fresh process each.
+    import multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_busy_task_main, args=(momentum, fault, q))
+    p.start()
+    bad, err = q.get(timeout=240)
+    p.join(60)
+    assert err is None, err
+    if fault:
+        assert bad, "the race went unseen: the fault switch did nothing"
+    else:
+        assert not bad, bad
+
+
+def _busy_task_loop(momentum):
+    import torch
+
+    from tests.helpers import compare_states, download, upload
+    n, R, clocks, alpha = 1 << 20, 3, 2, 0.1
+    g = _gpu(n, R, momentum, 1e-4, alpha=alpha)
+    streams = [torch.cuda.Stream() for _ in range(R)]
+    try:
+        st = O.make_state(n, 1, R, alpha, momentum)
+        upload(g, st)
+        lasts = [np.zeros(n, np.float32) if momentum > 0 else None for _ in range(R)]
+        grads = [O.fill_normal(n, 7000 + i, 0.01) for i in range(R)]
+        from crossbow_amd import BUF_GRADIENT
+        task = 0
+        for clock in range(1, clocks + 1):
+            for i in range(R):
+                g.replica_write(i, BUF_GRADIENT, grads[i])
+            torch.cuda.synchronize()
+            for i in range(R):
+                _busy(torch, streams[i])
+                g.replica_optimise(i, task, streams[i].cuda_stream)
+                task += 1
+            g.lockAny()
+            g.synchronise(0, clock, 0, False)  # right behind the launches: no host wait, no host work
+            g.unlockAny()
+            for i in range(R):  # the oracle after the enqueue, so the host takes no time in between
+                O.sma_optimise(np.float32(-0.05), momentum, 1e-4, st.w[i], grads[i], lasts[i], st.s[i])
+            O.sma_step(st)
+        g.wait()
+        torch.cuda.synchronize()
+        try:
+            compare_states(download(g, st), st)
+        except AssertionError as e:
+            return str(e)[:300]
+        return None
+    finally:
+        torch.cuda.synchronize()
+        g.free()
+
+
 def test_nesterov_is_unsupported():
     from crossbow_amd import CbxError, TheGPU, _lib
     n = 4096
