@@ -16,7 +16,10 @@ exactly K steps ((12R+8+8m)n per step at G = 1, and
 
 Process forms at N > 1:
   per-rank  one process per GPU, launched by torch.distributed.run (each rank
-            its own RCCL communicator, ncclCommInitRank);
+            its own RCCL communicator, ncclCommInitRank).  RCCL's forms are
+            tuned and timed first; the peer-read form (IPC-mapped buffers)
+            after them, timed too if its best candidate is faster, and the
+            faster timed block sets `value` (the other: `other_form`);
   single    one process over N devices, the form Crossbow itself takes
             (TheGPU.init -> ncclCommInitAll, executioncontext.c:185-201, grouped
             all-reduces from one host thread, synch/common.c:14-54): --gpus N
