@@ -218,3 +218,54 @@ def test_a_later_phase_that_raises_still_prints_the_line():
     inc = d["incomplete_phase"]
     assert inc["phase"] == "peer-read IPC mapping" and "selftest: a later phase raised" in inc["error"], inc
     assert d["config"]["peer_ipc"].startswith("failed: 'peer-read IPC mapping' raised RuntimeError"), d["config"]
+
+
+def test_block_fields_shape_at_two_gpus():
+    # The fields one timed block contributes to the N > 1 line (value, the
+    # kernels' roofline beside the collective, the link rate, the host's
+    # enqueue time), how a block merges into the line and how the other
+    # block is summarised in `other_form`: a fake context's timing records
+    # stand in for the GPU.
+    sys.path.insert(0, ROOT)
+    import argparse
+
+    import bench
+    from crossbow_amd import _lib
+    from crossbow_amd import dist as D
+    n, K = 25_557_032, 4
+
+    class FakeGpu:
+        hist = {_lib.T_KERNEL: [0.30] * K, _lib.T_ALLREDUCE: [0.12] * K, _lib.T_APPLY: [0.07] * K,
+                _lib.T_STEP: [0.45] * K}
+
+        def timing_history(self, which, local=0):
+            return list(self.hist[which])
+
+    args = argparse.Namespace(replicas=8, momentum=0.9, steps=K, model="resnet50",
+                              traffic_json=os.path.join(ROOT, "profiles", "traffic.json"))
+    blk = {"el": K * 0.5e-3, "host_ms": [0.05] * K, "steps_ms": [0.45] * K}
+    calib = {"kernel": [0.43, 0.43], "allreduce": [0.2, 0.2], "apply": [0.08, 0.08], "step": [0.72, 0.72]}
+    chosen = {"algorithm": _lib.ALLREDUCE_RCCL, "buckets": 4, "mode": 1, "stride": 2, "group": 1,
+              "enqueue_threads": None, "bucket_elements": -(-n // 4)}
+
+    class Tune:
+        table = {"4/1/s2": 0.5}
+        errors = {}
+
+    f = bench.block_fields(FakeGpu(), D, args, 1, n, 2, 1, True, blk, chosen, Tune(), calib, False)
+    step_bytes = (12 * 8 + 8) * n + (12 + 8) * n
+    assert f["value"] == round(step_bytes * 2 * K / blk["el"] / 1e9, 2) and f["ms_per_step"] == 0.5
+    r = f["roofline"]
+    assert r["kernel"] == "sma_accumulate_kernel" and r["launch_ms_mean"] == 0.3
+    assert r["apply_kernel"]["kernel"] == "sma_apply_kernel" and r["a_plus_b"]["launch_ms_mean"] == 0.37
+    assert r["collective_busy_ms_mean"] == 0.12 and f["roofline_unpipelined"]["launch_ms_mean"] == 0.43
+    ar = f["allreduce"]
+    assert ar["form"] == "all-reduce" and ar["timed"]["busbw_GBs"] > 0 and ar["timed"]["xgmi_frac"] > 0
+    assert f["config"]["buckets"] == 4 and f["config"]["allreduce_algorithm"] == "all-reduce"
+    assert f["host"] == {"enqueue_ms_per_step_timed": 0.05, "devices_per_process": 1}
+    line = {"metric": bench.METRIC, "config": {"workload": "w", "peer_ipc": "mapped"}}
+    bench.merge_block(line, f)
+    assert line["value"] == f["value"] and line["config"]["peer_ipc"] == "mapped" and line["config"]["buckets"] == 4
+    s = bench.block_summary(f, {"trusted": True})
+    assert s["value"] == f["value"] and s["config"]["allreduce_algorithm"] == "all-reduce"
+    assert s["roofline"]["frac"] == r["frac"] and s["identity"] == {"trusted": True}
