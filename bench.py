@@ -219,15 +219,16 @@ class Watchdog:
         with self.lock:
             self.deadline = None
 
-    def fail_now(self, error: str) -> None:
-        """A phase after the first timed region raised: print the published
-        line (rank 0) naming the phase and the error, and leave with 0, as
-        for a missed deadline.  Before the line exists, re-raise instead."""
+    def fail_now(self, exc: BaseException) -> None:
+        """A phase after the first timed region raised `exc`: print the
+        published line (rank 0) naming the phase and the error, and leave
+        with 0, as for a missed deadline.  Before the line exists, re-raise."""
         with self.lock:
             phase, done, published = self.phase, self.last_done, self.result is not None
             self.deadline = None
         if not published:
-            raise
+            raise exc
+        error = f"{type(exc).__name__}: {exc}"
         sys.stderr.write(f"[bench] rank {self.rank}: phase '{phase}' failed: {error}\n")
         sys.stderr.flush()
         if self.rank == 0:
@@ -910,7 +911,7 @@ def main():
             try:
                 raise RuntimeError("selftest: a later phase raised")
             except Exception as e:  # noqa: BLE001
-                wd.fail_now(f"{type(e).__name__}: {e}")
+                wd.fail_now(e)
         wd.enter("selftest post-timed stall", args.watchdog_selftest_result)
         time.sleep(args.watchdog_selftest_result * 20 + 10)
         raise SystemExit("watchdog did not fire")
@@ -1314,7 +1315,7 @@ def main():
     except Exception as e:  # noqa: BLE001 -- a later phase must not cost the measured line
         import traceback
         traceback.print_exc()
-        wd.fail_now(f"{type(e).__name__}: {e}")
+        wd.fail_now(e)
     wd.stop()
     if rank == 0:
         print(json.dumps(result), file=result_out, flush=True)
