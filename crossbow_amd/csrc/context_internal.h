@@ -787,8 +787,9 @@ inline int probe_device(int hip_id, int *num_cus) {
 // streams (sync, comm, and the two of kernels A) are created together in
 // open_device, before RCCL creates its own, and take the pool's first
 // queues: at HIP's default 4 queues the pipeline then measured within 3 % of
-// 16 (profiles/r04/hw_queues_ab.jsonl); 16 is the recommended deployment
-// setting, which the library does not impose.  (CU-mask
+// 16 (profiles/r04/hw_queues_ab.jsonl).  HIP's default 4 is the recommended
+// deployment setting (beyond 4, a later stream's queue shares
+// a pipe with one of these), which the library does not impose.  (CU-mask
 // streams get queues of their own too, but they synchronise with the null
 // stream; the reference's sync stream is non-blocking.)
 inline int create_stream(hipStream_t *s) {
