@@ -36,6 +36,7 @@ import faulthandler
 import json
 import os
 import re
+import select
 import signal
 import socket
 import statistics
@@ -144,6 +145,8 @@ def parse():
                    help="watchdog deadline (s, times --watchdog-scale) of the peer-read form's IPC mapping")
     p.add_argument("--watchdog-selftest-result", type=float, default=0.0, help=argparse.SUPPRESS)
     p.add_argument("--selftest-raise", action="store_true", help=argparse.SUPPRESS)
+    p.add_argument("--selftest-sigterm", choices=("main", "thread", "unpublished", "launcher"), default=None,
+                   help=argparse.SUPPRESS)
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
                    help="PMC-derived HBM bytes per launch (written by scripts/pmc_traffic.py)")
     return p.parse_args()
@@ -191,15 +194,67 @@ class Watchdog:
     (`publish`), a missed deadline prints that line on rank 0 first, with
     `incomplete_phase` naming what did not finish, and the exit code is 0;
     before that it is 3 and stdout stays empty.  Every phase is one stderr
-    line on rank 0."""
+    line on rank 0.  `catch_sigterm` extends the same to the launcher's
+    SIGTERM.  Exactly one of these endings (or main's own print) prints."""
 
     def __init__(self, scale: float, rank: int):
         self.scale, self.rank = scale, rank
         self.phase, self.deadline, self.seconds, self.last_done = None, None, 0.0, None
         self.result, self.out = None, None
-        self.lock = threading.Lock()
+        self.ending, self.wake = False, None
+        # reentrant: the main thread's SIGTERM handler may run inside a `with self.lock`
+        self.lock = threading.RLock()
         if scale > 0:
             threading.Thread(target=self._watch, name="bench-watchdog", daemon=True).start()
+
+    def catch_sigterm(self) -> None:
+        """torch.distributed.run ends every rank with SIGTERM once one rank
+        fails (SIGKILL after its grace period): on rank 0 that must not cost a
+        line already assembled.  Python's C-level handler writes the signal's
+        number to the wakeup fd in whichever thread the kernel picks, so the
+        watchdog thread prints the line even while the main thread sits in a
+        blocking native call (a HIP synchronize, a collective).  The
+        Python-level handler (main thread, at any bytecode boundary, maybe in
+        the middle of a write to stderr) only keeps the default action away.
+        Before the line exists the rank ends as SIGTERM would (exit 143).
+        Main thread only; needs the watchdog thread (scale > 0)."""
+        if self.scale <= 0:
+            return
+        r, w = socket.socketpair()
+        r.setblocking(False)
+        w.setblocking(False)
+        self.wake = (r, w)
+        signal.set_wakeup_fd(w.fileno(), warn_on_full_buffer=False)
+        signal.signal(signal.SIGTERM, lambda signum, frame: None)
+
+    def _claim_end(self):
+        """(phase, last done, published) for the one ending that prints, else None."""
+        with self.lock:
+            if self.ending:
+                return None
+            self.ending, self.deadline = True, None
+            return self.phase, self.last_done, self.result is not None
+
+    def finish(self) -> bool:
+        """main is about to print the complete line: no other ending may."""
+        return self._claim_end() is not None
+
+    def _terminated(self) -> None:
+        claim = self._claim_end()
+        if claim is None:
+            return  # another ending (or main's print) is already under way
+        phase, done, published = claim
+        sys.stderr.write(f"[bench] rank {self.rank}: SIGTERM in phase '{phase}'; thread states follow\n")
+        sys.stderr.write(thread_states())
+        sys.stderr.flush()
+        if published and self.rank == 0:
+            try:
+                print(self._line(phase, 0.0, done, "SIGTERM", how="was ended by SIGTERM (the launcher ends every "
+                                 "rank once one fails)"), file=self.out, flush=True)
+            except Exception as e:  # noqa: BLE001 -- never let the line itself keep the rank alive
+                sys.stderr.write(f"[bench] could not print the line: {e!r}\n")
+                sys.stderr.flush()
+        os._exit(0 if published else 128 + signal.SIGTERM)
 
     def enter(self, name: str, seconds: float) -> None:
         with self.lock:
@@ -209,25 +264,28 @@ class Watchdog:
             self.deadline = time.monotonic() + self.seconds if self.scale > 0 else None
         if self.rank == 0:
             log(f"[bench] phase {name}" + (f" (deadline {self.seconds:.0f} s)" if self.scale > 0 else ""))
+        kill = os.environ.get("CBX_BENCH_FAULT_KILL")  # test switch "rank:phase": that rank crashes there
+        if kill and kill.partition(":")[0] == str(self.rank) and kill.partition(":")[2] == name:
+            os.kill(os.getpid(), signal.SIGKILL)
 
     def publish(self, result: dict, out) -> None:
         """The line as assembled so far (the main thread keeps adding to it)."""
         with self.lock:
             self.result, self.out = result, out
 
-    def stop(self) -> None:
-        with self.lock:
-            self.deadline = None
-
     def fail_now(self, exc: BaseException) -> None:
         """A phase after the first timed region raised `exc`: print the
         published line (rank 0) naming the phase and the error, and leave
         with 0, as for a missed deadline.  Before the line exists, re-raise."""
         with self.lock:
-            phase, done, published = self.phase, self.last_done, self.result is not None
-            self.deadline = None
+            published = self.result is not None
         if not published:
             raise exc
+        claim = self._claim_end()
+        if claim is None:  # a SIGTERM ending is printing: let it finish the process
+            time.sleep(60)
+            os._exit(0)
+        phase, done, _ = claim
         error = f"{type(exc).__name__}: {exc}"
         sys.stderr.write(f"[bench] rank {self.rank}: phase '{phase}' failed: {error}\n")
         sys.stderr.flush()
@@ -235,8 +293,8 @@ class Watchdog:
             print(self._line(phase, 0.0, done, error), file=self.out, flush=True)
         os._exit(0)
 
-    def _line(self, phase, secs, done, error=None):
-        """The published line with the phase that missed its deadline (or raised)."""
+    def _line(self, phase, secs, done, error=None, how=None):
+        """The published line with the phase that missed its deadline (or raised, or was ended)."""
         import copy
         for _ in range(5):  # the main thread may be adding a key right now
             try:
@@ -246,7 +304,7 @@ class Watchdog:
                 time.sleep(0.05)
         else:
             r = {k: self.result[k] for k in ("metric", "value", "unit") if k in self.result}
-        how = f"raised {error}" if error else f"missed its {secs:.0f} s deadline"
+        how = how or (f"raised {error}" if error else f"missed its {secs:.0f} s deadline")
         r["incomplete_phase"] = {
             "phase": phase, "deadline_s": None if error else round(secs, 1), "error": error, "last_completed": done,
             "note": f"this phase came after the timed region that set `value` and {how}; the run ended here "
@@ -258,12 +316,21 @@ class Watchdog:
 
     def _watch(self) -> None:
         while True:
-            time.sleep(0.2)
+            wake = self.wake
+            if wake is None:
+                time.sleep(0.2)
+            elif select.select([wake[0]], [], [], 0.2)[0]:
+                try:
+                    got = wake[0].recv(256)
+                except BlockingIOError:
+                    got = b""
+                if int(signal.SIGTERM) in got:
+                    self._terminated()
             with self.lock:
                 late = self.deadline is not None and time.monotonic() > self.deadline
                 phase, secs, done = self.phase, self.seconds, self.last_done
                 published = self.result is not None
-            if late:
+            if late and self._claim_end() is not None:
                 sys.stderr.write(f"[bench] WATCHDOG rank {self.rank}: phase '{phase}' missed its {secs:.0f} s "
                                  f"deadline; last completed phase: '{done}'; thread states and stacks follow\n")
                 sys.stderr.write(thread_states())
@@ -915,8 +982,35 @@ def main():
         wd.enter("selftest post-timed stall", args.watchdog_selftest_result)
         time.sleep(args.watchdog_selftest_result * 20 + 10)
         raise SystemExit("watchdog did not fire")
+    if args.selftest_sigterm:
+        # CPU test: the launcher's SIGTERM while the main thread waits (in a
+        # handler-running wait, or -- "thread" -- one that never returns to
+        # Python, as a HIP synchronize or a collective would not).  "launcher":
+        # under torch.distributed.run, rank 1 is killed once rank 0 waits, and
+        # the launcher's SIGTERM ends rank 0.
+        rank = int(os.environ.get("RANK", "0"))
+        mark = os.path.join(tempfile.gettempdir(), f"cbx_sigterm_selftest_{os.environ.get('MASTER_PORT', '0')}")
+        if rank != 0:
+            for _ in range(600):
+                if os.path.exists(mark):
+                    os.kill(os.getpid(), signal.SIGKILL)  # a crash: no handler, no line
+                time.sleep(0.1)
+            raise SystemExit("rank 0 never waited")
+        wd = Watchdog(1.0, 0)
+        wd.catch_sigterm()
+        if args.selftest_sigterm != "unpublished":
+            wd.publish({"metric": METRIC, "value": 1.0, "unit": "GB/s", "config": {}}, result_out)
+        wd.enter("selftest wait for SIGTERM", 600)
+        if args.selftest_sigterm in ("thread", "launcher"):
+            signal.pthread_sigmask(signal.SIG_BLOCK, {signal.SIGTERM})
+        log("[bench] selftest: waiting for SIGTERM")
+        if args.selftest_sigterm == "launcher":
+            open(mark, "w").close()
+        threading.Event().wait(120)
+        raise SystemExit("SIGTERM did not end the run")
     rank0 = int(os.environ.get("RANK", "0"))
     wd = Watchdog(args.watchdog_scale, rank0)
+    wd.catch_sigterm()
     # the first `import torch` on a fresh box can take minutes (image paging)
     wd.enter("init (torch, HIP, communicators)", 900)
     from crossbow_amd import dist as D
@@ -1316,7 +1410,9 @@ def main():
         import traceback
         traceback.print_exc()
         wd.fail_now(e)
-    wd.stop()
+    if not wd.finish():  # a SIGTERM ending is printing the line: let it end the process
+        time.sleep(60)
+        os._exit(0)
     if rank == 0:
         print(json.dumps(result), file=result_out, flush=True)
     D.finalize(world)

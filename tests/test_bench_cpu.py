@@ -5,6 +5,8 @@ import os
 import subprocess
 import sys
 
+import pytest
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
@@ -269,3 +271,76 @@ def test_block_fields_shape_at_two_gpus():
     s = bench.block_summary(f, {"trusted": True})
     assert s["value"] == f["value"] and s["config"]["allreduce_algorithm"] == "all-reduce"
     assert s["roofline"]["frac"] == r["frac"] and s["identity"] == {"trusted": True}
+
+
+def _sigterm_run(variant: str):
+    import signal
+    p = subprocess.Popen([sys.executable, "bench.py", "--selftest-sigterm", variant], cwd=ROOT,
+                         stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+    err = []
+    try:
+        for line in p.stderr:  # the selftest says when it is waiting
+            err.append(line)
+            if "waiting for SIGTERM" in line:
+                break
+        p.send_signal(signal.SIGTERM)
+        out, rest = p.communicate(timeout=60)
+    finally:
+        if p.poll() is None:
+            p.kill()
+            p.wait()
+    return p.returncode, out, "".join(err) + rest
+
+
+@pytest.mark.parametrize("variant", ["main", "thread"])
+def test_launcher_sigterm_still_prints_the_line(variant):
+    # torch.distributed.run sends SIGTERM to every rank once one rank fails:
+    # rank 0 prints the line it already holds, naming the phase that was
+    # ended, and exits 0 -- also when its main thread is in a wait that never
+    # returns to Python ("thread": SIGTERM blocked there, as inside a HIP
+    # synchronize the watchdog thread handles it through the wakeup fd).
+    import json
+    rc, out, err = _sigterm_run(variant)
+    assert rc == 0, (rc, err[-2000:])
+    lines = [ln for ln in out.splitlines() if ln.strip()]
+    assert len(lines) == 1, out
+    inc = json.loads(lines[0])["incomplete_phase"]
+    assert inc["phase"] == "selftest wait for SIGTERM" and inc["error"] == "SIGTERM", inc
+    assert "was ended by SIGTERM" in inc["note"]
+    assert "SIGTERM in phase 'selftest wait for SIGTERM'" in err, err[-2000:]
+
+
+def test_launcher_sigterm_before_the_line_ends_the_rank_as_sigterm_would():
+    rc, out, err = _sigterm_run("unpublished")
+    assert rc == 143 and not out.strip(), (rc, out, err[-2000:])
+
+
+def test_launcher_ending_a_failed_run_keeps_rank_0s_line():
+    # The real launcher: rank 1 dies (SIGKILL, as a crash would) while rank 0
+    # holds a line and waits in a wait that never returns to Python;
+    # torch.distributed.run then SIGTERMs rank 0, which prints that line.
+    import json
+    import socket
+    import tempfile
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    mark = os.path.join(tempfile.gettempdir(), f"cbx_sigterm_selftest_{port}")
+    if os.path.exists(mark):
+        os.unlink(mark)
+    try:
+        # the launcher imports torch: through tests/torch_loader_check.py (a no-op on a healthy install)
+        boot = ("import runpy, sys; from tests.torch_loader_check import ensure_torch_loadable; "
+                "ensure_torch_loadable(); sys.argv = ['torch.distributed.run'] + sys.argv[1:]; "
+                "runpy.run_module('torch.distributed.run', run_name='__main__')")
+        p = subprocess.run([sys.executable, "-c", boot, "--nnodes=1", "--nproc-per-node", "2",
+                            "--master-addr", "127.0.0.1", "--master-port", str(port), "bench.py",
+                            "--selftest-sigterm", "launcher"], cwd=ROOT, capture_output=True, text=True, timeout=180)
+    finally:
+        if os.path.exists(mark):
+            os.unlink(mark)
+    lines = [ln for ln in p.stdout.splitlines() if ln.strip().startswith("{")]
+    assert len(lines) == 1, (p.returncode, p.stdout, p.stderr[-3000:])
+    inc = json.loads(lines[0])["incomplete_phase"]
+    assert inc["error"] == "SIGTERM" and inc["phase"] == "selftest wait for SIGTERM", inc
+    assert p.returncode != 0  # the launcher still reports rank 1's failure
