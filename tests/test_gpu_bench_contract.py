@@ -146,7 +146,9 @@ def test_bench_two_ranks_keeps_the_line_when_another_rank_crashes():
     """A rank that dies after the line exists (here rank 1, SIGKILLed as it
     enters the IPC mapping, $CBX_BENCH_FAULT_KILL) makes torch.distributed.run
     SIGTERM every other rank: rank 0 prints the RCCL block's line naming the
-    phase it was ended in.  The launcher itself still reports rank 1's exit."""
+    phase it was ended in -- by that SIGTERM, or by its gloo collective
+    failing first (connection reset), whichever comes first.  The launcher
+    itself still reports rank 1's exit."""
     env = dict(os.environ, CBX_BENCH_FAULT_KILL="1:peer-read IPC mapping")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", "29679", "bench.py", "--gpus", "2",
@@ -156,9 +158,9 @@ def test_bench_two_ranks_keeps_the_line_when_another_rank_crashes():
     d = _one_line(p.stdout)
     _check(d, 2)
     inc = d["incomplete_phase"]
-    assert inc["error"] == "SIGTERM" and inc["phase"] == "peer-read IPC mapping", inc
+    assert inc["phase"] == "peer-read IPC mapping" and inc["error"], inc
+    assert inc["error"] == "SIGTERM" or "Connection reset" in inc["error"], inc
     assert d["allreduce"]["timed"]["busbw_GBs"] > 0 and d["identity"]["trusted"] is True
-    assert "SIGTERM in phase 'peer-read IPC mapping'" in p.stderr
 
 
 @pytest.mark.timeout(300)
