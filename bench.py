@@ -617,6 +617,45 @@ def base_identity(gpu, world):
                        "across every GPU (every GPU applies the same D, sma.c:168-174)"}
 
 
+def state_max_abs(gpu, world):
+    """max |value| of z and last over every GPU (the fresh state's yardstick
+    for `dynamics`)."""
+    import numpy as np
+    from crossbow_amd import BUF_DATA, BUF_LAST
+    top = 0.0
+    for g in gpu.local_devices():
+        for kind in (BUF_DATA, BUF_LAST):
+            a = gpu.base_read(g, kind)
+            top = max(top, float(np.max(np.abs(a))) if a.size else 0.0)
+    from crossbow_amd import dist as D
+    return D.max_over_ranks(top, world)
+
+
+def sma_dynamics(alpha: float, momentum: float, replicas_total: int) -> dict:
+    """How the bench's values evolve, whatever computes them.  The bench keeps
+    every snapshot s_i fixed between steps (no optimiser runs), so the
+    deviation e = z - mean(s) and the momentum `last` of the SMA step
+    (sma.c:63-174: D = alpha * sum_i (s_i - z) = -alpha N e; last' = mu last +
+    D; z' = z + last') follow the linear map [[1 - alpha N, mu], [-alpha N,
+    mu]] (without momentum, e' = (1 - alpha N) e).  Its spectral radius is
+    the growth per step; it exceeds 1 exactly when alpha N > 2 (1 + mu):
+    3.8 at mu = 0.9.  C3 weak-scaled to 8 GPUs (8 x 8 replicas, alpha 0.1)
+    has alpha N = 6.4 and radius 4.29, so the values grow ~4.3x per step from
+    any start; the reference's own run (8 GPUs x 2, resnet-50.sh:74-102) and
+    C5 (8 x 4) are inside the bound.  Re-snapshotting s_i <- w_i every step
+    does not change the verdict (tests/test_oracle.py).  The arithmetic per
+    element, and so the timing, is the same whatever the values."""
+    import numpy as np
+    aN = alpha * replicas_total
+    if momentum > 0:
+        rho = float(max(abs(np.linalg.eigvals(np.array([[1.0 - aN, momentum], [-aN, momentum]])))))
+    else:
+        rho = abs(1.0 - aN)
+    return {"alpha_times_replicas": round(aN, 4), "stability_bound": round(2 * (1 + max(momentum, 0.0)), 4),
+            "spectral_radius_per_step": round(rho, 4), "bounded": rho <= 1.0 + 1e-9,
+            "model": "fixed snapshots s_i: e = z - mean(s), [e, last]' = [[1 - aN, mu], [-aN, mu]] [e, last]"}
+
+
 def form_agreement(gpu, world, step, chosen, one_bucket, algorithm_name):
     """After the timed region at G > 1, when the measured configuration is not
     the reference's own collective: one more step in that configuration, and
@@ -680,13 +719,20 @@ def form_agreement(gpu, world, step, chosen, one_bucket, algorithm_name):
 AGREEMENT_MAX_ABS = 1e3
 
 
-def block_identity(gpu, world, step, chosen, one_bucket, peer_only, peer_algo, wd):
+def block_identity(gpu, world, step, chosen, one_bucket, peer_only, peer_algo, wd, blk=None, dynamics=None):
     """After a timed block at G > 1: z and last bitwise identical on every GPU
     (base_identity), and, unless the block ran the reference's own in-order
     all-reduce, one step of the block's configuration against one in-order
     all-reduce of the same step from a FRESH synthetic state
-    (form_agreement).  `trusted`: both hold, finitely and not vacuously."""
+    (form_agreement).  `trusted`: both hold, finitely and not vacuously.
+    `dynamics` (sma_dynamics) with the block's fresh-state max |value|: the
+    observed growth per step since the fresh state, beside the predicted one."""
     idn = base_identity(gpu, world)
+    if dynamics is not None and blk is not None and blk.get("fresh_max_abs"):
+        k = blk["steps_since_fresh"]
+        ratio = idn["max_abs_value"] / blk["fresh_max_abs"]
+        idn["dynamics"] = dict(dynamics, fresh_max_abs=blk["fresh_max_abs"], steps_since_fresh=k,
+                               observed_growth_per_step=round(ratio ** (1.0 / k), 4) if ratio > 0 and k > 0 else None)
     if not peer_only and (chosen["algorithm"] != 0 or chosen["buckets"] != 1):
         wd.enter("agreement with the all-reduce", 300)
         gpu.wait()
@@ -771,14 +817,17 @@ def apply_config(gpu, chosen, single):
 def timed_block(gpu, torch, D, args, world, step, wd, refill, label=""):
     """W warm-up steps, then EXACTLY K timed steps bracketed by a barrier and
     a device synchronisation on both sides; the wall time is the max over
-    ranks.  `refill`: fresh synthetic state first (G > 1: the bench never
-    re-snapshots s_i, so hundreds of calibration and tuning steps drive the
-    fixed-snapshot dynamics past fp32's range at G = 8; the
-    arithmetic per element is the same whatever the values)."""
+    ranks.  `refill`: fresh synthetic state first, and its max |value| kept
+    for `dynamics` (G > 1: with the snapshots s_i fixed, alpha N above
+    2 (1 + mu) makes the values grow by sma_dynamics' radius per step, 4.3x
+    at 8 GPUs x 8 replicas; the arithmetic per element is the same whatever
+    the values)."""
     from crossbow_amd import _lib
+    fresh = None
     if refill:
         gpu.wait()
         gpu.fill_synthetic(SEED)
+        fresh = state_max_abs(gpu, world)
     wd.enter("warm-up" + label, 180)
     for _ in range(args.warmup):
         step()
@@ -798,7 +847,8 @@ def timed_block(gpu, torch, D, args, world, step, wd, refill, label=""):
     D.barrier(world)
     el = D.max_over_ranks(el, world)
     wd.enter("timing read-back" + label, 120)
-    return {"el": el, "host_ms": host_ms, "steps_ms": list(gpu.timing_history(_lib.T_STEP)[-args.steps:])}
+    return {"el": el, "host_ms": host_ms, "steps_ms": list(gpu.timing_history(_lib.T_STEP)[-args.steps:]),
+            "fresh_max_abs": fresh, "steps_since_fresh": args.warmup + args.steps}
 
 
 def block_fields(gpu, D, args, world, n, G, nlocal, split, blk, chosen, tuning, calib, rehearse):
@@ -904,11 +954,11 @@ def block_fields(gpu, D, args, world, n, G, nlocal, split, blk, chosen, tuning, 
         # all-reduce (either form) moves 2(G-1)/G x 4n bytes per GPU (busbw);
         # the peer-read reduction reads (G-1)/G x 4n of its shard from the
         # peers (kernel B's remote reads of D sit inside kernel B's span).
-        def link(ms, timed_in):
+        def link(ms, timed_in, algo=ar_algo):
             if not ms or ms <= 0 or G <= 1:
                 return {"ms": round(ms, 4) if ms else ms, "timed_in": timed_in}
             algbw = 4 * n / (ms * 1e-3) / 1e9
-            busbw = algbw * ((G - 1) / G if ar_algo == _lib.ALLREDUCE_PEER else 2 * (G - 1) / G)
+            busbw = algbw * ((G - 1) / G if algo == _lib.ALLREDUCE_PEER else 2 * (G - 1) / G)
             r = {"ms": round(ms, 4), "algbw_GBs": round(algbw, 1), "busbw_GBs": round(busbw, 1),
                  "xgmi_frac": round(busbw / ((G - 1) * XGMI_LINK_GBS), 4), "timed_in": timed_in}
             if rehearse:
@@ -917,7 +967,10 @@ def block_fields(gpu, D, args, world, n, G, nlocal, split, blk, chosen, tuning, 
                 r.update(xgmi_frac=None, note="rehearsal: every rank on one GPU, no xGMI link crossed")
             return r
         ar_ms = statistics.median(calib["allreduce"])
-        unp = link(ar_ms, "calibration steps (one bucket, in order: the collective alone)")
+        # the calibration ran RCCL's all-reduce (one bucket, in order) whatever
+        # form the block ran: its link rate is the all-reduce's
+        unp = link(ar_ms, "calibration steps (one bucket, in order: one RCCL all-reduce alone)", 0)
+        unp["form"] = "all-reduce"
         unp.update(apply_ms_median=round(statistics.median(calib["apply"]), 4),
                    step_ms_median=round(statistics.median(calib["step"]), 4))
         timed = (link(coll_busy, "timed region: per step, the union of the collectives' busy spans (each from the "
@@ -1092,6 +1145,15 @@ def main():
 
     split = G > 1 or args.force_split
     per_rank = G > 1 and not single
+    # G > 1: every tuning candidate starts from the fresh synthetic state
+    # (dist.tune_buckets), as every timed block does (timed_block's refill).
+    dynamics = sma_dynamics(args.alpha, args.momentum, G * args.replicas) if G > 1 else None
+
+    def refresh():
+        gpu.wait()
+        gpu.fill_synthetic(SEED)
+
+    refresh = refresh if G > 1 else None
     # One process per GPU: the peer-read form needs every rank's acc and D
     # mapped through IPC handles first (cbx_peer_export / _import).  An
     # explicit peer-read configuration maps before anything else; otherwise
@@ -1137,7 +1199,7 @@ def main():
                                 ndev=G, peer=single, peer_only=peer_only, threads=single,
                                 steps=max(1, args.tune_steps), passes=max(1, args.tune_passes),
                                 warmup=min(2, max(1, args.tune_steps)),
-                                phase=lambda name: wd.enter(name, 90))
+                                phase=lambda name: wd.enter(name, 90), refresh=refresh)
         chosen.update(bucket_elements=tuning.bucket_elements, buckets=tuning.buckets, mode=tuning.mode,
                       stride=tuning.stride, group=tuning.group, algorithm=tuning.algorithm,
                       enqueue_threads=tuning.enqueue_threads)
@@ -1197,7 +1259,8 @@ def main():
     try:
         if G > 1:
             wd.enter("cross-GPU identity of z and last", 180)
-            result["identity"] = block_identity(gpu, world, step, chosen, one_bucket, peer_only, ALLREDUCE_PEER, wd)
+            result["identity"] = block_identity(gpu, world, step, chosen, one_bucket, peer_only, ALLREDUCE_PEER, wd,
+                                                blk, dynamics)
 
         reported = chosen
         if per_rank and split and not explicit and not args.no_peer_ipc:
@@ -1212,7 +1275,7 @@ def main():
                                          ndev=G, peer=True, peer_only=True, threads=False,
                                          steps=max(1, args.tune_steps), passes=max(1, args.tune_passes),
                                          warmup=min(2, max(1, args.tune_steps)),
-                                         phase=lambda name: wd.enter(name, 90))
+                                         phase=lambda name: wd.enter(name, 90), refresh=refresh)
                 best_rccl, best_peer = min(tuning.table.values()), min(ptuning.table.values())
                 pchosen = dict(chosen, bucket_elements=ptuning.bucket_elements, buckets=ptuning.buckets,
                                mode=ptuning.mode, stride=ptuning.stride, group=ptuning.group,
@@ -1223,7 +1286,8 @@ def main():
                     pfields = block_fields(gpu, D, args, world, n, G, nlocal, split, pblk, pchosen, ptuning, calib,
                                            args.rehearse_one_gpu)
                     wd.enter("cross-GPU identity of z and last (peer-read form)", 180)
-                    pident = block_identity(gpu, world, step, pchosen, one_bucket, False, ALLREDUCE_PEER, wd)
+                    pident = block_identity(gpu, world, step, pchosen, one_bucket, False, ALLREDUCE_PEER, wd,
+                                            pblk, dynamics)
                     if pfields["value"] > result["value"] and pident.get("trusted", False):
                         other = block_summary({k: result[k] for k in pfields}, result["identity"])
                         merge_block(result, pfields)

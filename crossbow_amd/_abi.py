@@ -122,6 +122,7 @@ SIGNATURES = {
     "cbx_replica_host_buffer": (_I, [_P, _I, _I, _PP]),
     "cbx_base_host_buffer": (_I, [_P, _I, _I, _PP]),
     "cbx_wait": (_I, [_P]),
+    "cbx_task_wait_count": (_I, [_P, _I]),
     "cbx_step_event": (_I, [_P, _I, _PP]),
     "cbx_set_timing": (_I, [_P, _I]),
     "cbx_last_timing": (_I, [_P, _I, _FP]),
@@ -137,6 +138,7 @@ SIGNATURES = {
     "cbx_set_allreduce_algorithm": (_I, [_P, _I]),
     "cbx_peer_export": (_I, [_P, _P, _c.POINTER(_S)]),
     "cbx_peer_import": (_I, [_P, _P, _I]),
+    "cbx_resync_base": (_I, [_P, _I]),
     "cbx_set_staging_mode": (_I, [_P, _I]),
     "cbx_set_bucket_elements": (_I, [_P, _c.c_longlong]),
     "cbx_set_force_split": (_I, [_P, _I]),

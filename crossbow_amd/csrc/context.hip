@@ -521,6 +521,8 @@ static int synchronise_impl(cbx_context *c, int first, int clock, int autotune, 
   TRY(check_manager_q(c));
   if (first < 0 || first > c->size) return fail(CBX_ERR_INVALID, "first replica %d out of range", first);
   TRY(flush_task_waits(c));  // the replicas' updates on callers' streams come first
+  // One process per GPU: no collective step of any form once a rank is broken.
+  if (c->G > 1) TRY(peer_guard(c, staged ? "cbx_synchronise_staged" : "cbx_synchronise"));
   // executioncontext.c:2287-2315: SYNCHRONOUSEAMSGD (3) routes to SMA because
   // ELASTIC_AVERAGE is #undef'd; SMA is 7.  The other update models are not
   // this library's path.
@@ -958,11 +960,59 @@ static int replica_optimise_impl(cbx_context *c, int id, int task, void *stream)
 
 namespace cbx::host {
 
+namespace {
+
+// Queues the sync stream's wait for every pending entry (task_mu held).
+int flush_device_waits(Device &d) {
+  for (Device::TaskWait &w : d.task_waits)
+    if (w.pending) {
+      HIP_TRY(hipStreamWaitEvent(d.stream, w.event, 0));
+      w.pending = false;
+    }
+  return CBX_OK;
+}
+
+// Drops the entries whose event has completed: the update behind it is done,
+// so the sync stream has nothing to wait for, whether or not the wait was
+// queued (a queued wait on a completed event is already satisfied; task_mu
+// held).
+void prune_task_waits(Device &d) {
+  auto done = [](const Device::TaskWait &w) { return hipEventQuery(w.event) == hipSuccess; };
+  for (Device::TaskWait &w : d.task_waits)
+    if (done(w)) {
+      (void)hipEventDestroy(w.event);
+      w.event = nullptr;
+    }
+  d.task_waits.erase(std::remove_if(d.task_waits.begin(), d.task_waits.end(),
+                                    [](const Device::TaskWait &w) { return w.event == nullptr; }),
+                     d.task_waits.end());
+}
+
+}  // namespace
+
+// One entry per caller stream with an update not yet known complete.  A
+// stream not in the table first prunes it (entries whose update completed:
+// short-lived task streams leave nothing behind), and at kTaskWaitCap
+// entries the device's pending waits are queued at once and the table is
+// pruned again, the oldest entry's event waited for if that frees nothing.
+// The current device is the caller's (the replica's) throughout.
 int defer_task_wait(Device &d, hipStream_t st) {
   std::lock_guard<std::mutex> l(*d.task_mu);
-  auto it = std::find_if(d.task_waits.begin(), d.task_waits.end(),
-                         [st](const Device::TaskWait &w) { return w.stream == st; });
+  auto find = [&] {
+    return std::find_if(d.task_waits.begin(), d.task_waits.end(),
+                        [st](const Device::TaskWait &w) { return w.stream == st; });
+  };
+  auto it = find();
   if (it == d.task_waits.end()) {
+    prune_task_waits(d);
+    if (d.task_waits.size() >= kTaskWaitCap) {
+      TRY(flush_device_waits(d));
+      prune_task_waits(d);
+      if (d.task_waits.size() >= kTaskWaitCap) {
+        HIP_TRY(hipEventSynchronize(d.task_waits.front().event));
+        prune_task_waits(d);
+      }
+    }
     hipEvent_t e = nullptr;
     HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     d.task_waits.push_back({st, e, false});
@@ -973,17 +1023,31 @@ int defer_task_wait(Device &d, hipStream_t st) {
   return CBX_OK;
 }
 
+// Every device's pending waits; the caller's current device is restored
+// (an optimiser step flushing before its launch must launch on
+// the replica's device).
 int flush_task_waits(cbx_context *c) {
+  int cur = -1;
+  (void)hipGetDevice(&cur);
+  bool moved = false;
+  int rc = CBX_OK;
   for (Device &d : c->devs) {
     std::lock_guard<std::mutex> l(*d.task_mu);
-    for (Device::TaskWait &w : d.task_waits)
-      if (w.pending) {
-        HIP_TRY(hipSetDevice(d.hip_id));
-        HIP_TRY(hipStreamWaitEvent(d.stream, w.event, 0));
-        w.pending = false;
+    if (std::none_of(d.task_waits.begin(), d.task_waits.end(), [](const Device::TaskWait &w) { return w.pending; }))
+      continue;
+    if (d.hip_id != cur) {
+      const hipError_t e = hipSetDevice(d.hip_id);
+      moved = true;
+      if (e != hipSuccess) {
+        rc = fail(CBX_ERR_HIP, "hipSetDevice(%d): %s", d.hip_id, hipGetErrorString(e));
+        break;
       }
+    }
+    rc = flush_device_waits(d);
+    if (rc != CBX_OK) break;
   }
-  return CBX_OK;
+  if (moved && cur >= 0) (void)hipSetDevice(cur);
+  return rc;
 }
 
 int grow_device_buffer(void **p, size_t *have, size_t need) {
@@ -1060,6 +1124,7 @@ int cbx_average_batchnorm_stats(cbx_context *c, int layers, const int *elements,
   // :165-166: nothing to average with one device.
   const bool run = c->G > 1 || c->force_split;
   if (!run) return CBX_OK;
+  TRY(peer_guard(c, "cbx_average_batchnorm_stats"));
   TRY(ensure_comms(c));
   std::vector<BnDevice> devs;
   for (Device &d : c->devs)
@@ -1383,7 +1448,21 @@ int cbx_wait(cbx_context *c) {
     HIP_TRY(hipSetDevice(d.hip_id));
     HIP_TRY(hipStreamSynchronize(d.stream));
   }
-  return CBX_OK;
+  return peer_wait_check(c);
+}
+
+int cbx_resync_base(cbx_context *c, int root) {
+  TraceRange trace("cbx_resync_base");
+  TRY(check_manager_q(c));
+  return resync_base(c, root);
+}
+
+int cbx_task_wait_count(cbx_context *c, int local) {
+  TRY(check_ctx_q(c));
+  if (local < 0 || local >= (int)c->devs.size()) return fail(CBX_ERR_INVALID, "local device %d out of range", local);
+  Device &d = c->devs[local];
+  std::lock_guard<std::mutex> l(*d.task_mu);
+  return (int)d.task_waits.size();
 }
 
 int cbx_step_event(cbx_context *c, int local, void **event) {

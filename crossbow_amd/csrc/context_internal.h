@@ -1048,6 +1048,8 @@ int check_order_pair(const Device::OrderStep &p, const Device::OrderStep &q);
 // A replica update enqueued on a caller's stream `st`: the sync stream must
 // wait for it before the library next uses the replica (defer_task_wait), and
 // does so at its next operation on the device (flush_task_waits).
+// At most kTaskWaitCap entries per device (defer_task_wait).
+constexpr size_t kTaskWaitCap = 64;
 int defer_task_wait(Device &d, hipStream_t st);
 int flush_task_waits(cbx_context *c);
 
@@ -1061,13 +1063,21 @@ void peer_close(cbx_context *c);
 // bucket for "kernel A done", one for "reduction done", and one for "done
 // with the other ranks' memory" (teardown), each holding a step sequence
 // number (monotonic: a waiter waits for >=, so a flag already past it never
-// blocks).  A failed step writes kIpcRelease into its rank's words so no
-// other rank's stream waits forever, and sets its kIpcBroken word, which
-// every rank checks before its next step in this form.
+// blocks).  A failed step sets its kIpcBroken word, then writes kIpcRelease
+// into its rank's words so no other rank's stream waits forever.  A release
+// lets a wait pass on a flag whose data may never have been written, so
+// every kernel B of the form reads all ranks' kIpcBroken words once its own
+// loads have returned, and a wave that finds one set records its step's
+// sequence number in the rank's kIpcPoison word (a consumer may only have
+// read stale data if a release, and so a broken word, came first).  Every
+// rank checks the words before each collective step and in cbx_wait
+// (peer_guard, peer_wait_check); cbx_resync_base clears them.
 constexpr int64_t kIpcMaxBuckets = 4096;
 constexpr size_t kIpcRankWords = 2 * kIpcMaxBuckets + 64;  // a[], r[], done + padding (512 B)
-// kIpcOpened: this rank's imports are done; kIpcBroken: a step of this rank failed part-way
-constexpr int kIpcA = 0, kIpcR = 1, kIpcDone = 2, kIpcOpened = 3, kIpcBroken = 4;
+// kIpcOpened: this rank's imports are done; kIpcBroken: a step of this rank
+// failed part-way or was refused; kIpcPoison: the sequence number of a step
+// whose kernel B on this rank ran after some rank's broken word was set
+constexpr int kIpcA = 0, kIpcR = 1, kIpcDone = 2, kIpcOpened = 3, kIpcBroken = 4, kIpcPoison = 5;
 constexpr uint64_t kIpcRelease = 1ull << 62;
 // The largest buffer the per-rank peer-read form exports.  ROCr 1.18 as
 // shipped with ROCm 7.0 (torch's bundled runtime, which the library shares
@@ -1084,6 +1094,16 @@ inline size_t ipc_word(int rank, int kind, int64_t b) {
   return (size_t)rank * kIpcRankWords +
          (kind >= kIpcDone ? 2 * kIpcMaxBuckets + (size_t)(kind - kIpcDone) : (size_t)kind * kIpcMaxBuckets + b);
 }
-static_assert(2 * kIpcMaxBuckets + (kIpcBroken - kIpcDone) < (int64_t)kIpcRankWords, "flag words per rank");
+static_assert(2 * kIpcMaxBuckets + (kIpcPoison - kIpcDone) < (int64_t)kIpcRankWords, "flag words per rank");
+// Before a collective step of any form (and the batch-norm all-reduce): once
+// any rank's broken or poison word is set, this rank releases its own flags
+// (so no rank's stream waits on them) and refuses with CBX_ERR_STATE until
+// cbx_resync_base.  `what` names the refused call.
+int peer_guard(cbx_context *c, const char *what);
+// cbx_wait, after the streams drained: CBX_ERR_STATE if a kernel B of this
+// rank recorded a poisoned step (its z / last are undefined).
+int peer_wait_check(cbx_context *c);
+// cbx_resync_base: broadcast z and last from `root` and clear the flag page.
+int resync_base(cbx_context *c, int root);
 
 }  // namespace cbx::host

@@ -607,6 +607,23 @@ __global__ __launch_bounds__(256) void sma_peer_apply_kernel(const SmaArgs a, co
       }
     }
   }
+  if (p.broken != nullptr) {
+    // One process per GPU (context_internal.h, kIpcPoison): every load of
+    // this wave has returned, so only now read each rank's broken word, past
+    // the caches.  A flag release that let one of those loads see another
+    // rank's stale acc or D was preceded by a broken word, and shows here.
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const uint32_t lane = threadIdx.x & 63u;
+    uint64_t v = 0;
+    if (lane < (uint32_t)p.G)
+      v = __hip_atomic_load(const_cast<uint64_t *>(p.broken) + (int64_t)lane * p.broken_stride, __ATOMIC_RELAXED,
+                            __HIP_MEMORY_SCOPE_SYSTEM);
+    // The first poisoned step's number is kept: the kernels B of later steps
+    // run after this one's on the same stream, and find the word set.
+    if (__builtin_amdgcn_ballot_w64(v != 0) != 0 && lane == 0 &&
+        __hip_atomic_load(p.poison, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == 0)
+      __hip_atomic_store(p.poison, p.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
 }
 
 // ---------------------------------------------------------------------------

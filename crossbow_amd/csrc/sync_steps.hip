@@ -199,10 +199,12 @@ volatile uint64_t *host_word(cbx_context *c, int rank, int kind, int64_t b) {
 
 // A step that failed part-way, or one refused because another rank's failed:
 // no other rank may wait on this one's flags forever, and none may run
-// another step in this form against it.  The host
-// writes the release value into every flag word of this rank at once (a peer
-// stream waiting on one goes on) and raises the rank's broken word (every
-// rank checks the page before its next step, SplitStep::prepare_common).  The
+// another step against it.  The host raises the rank's broken word (every
+// rank checks the page before its next collective step, peer_guard, and
+// every kernel B of the form checks it after its loads, kIpcPoison), and only
+// then writes the release value into every flag word of this rank (a peer
+// stream waiting on one goes on: whatever such a wait lets a kernel read, the
+// broken word was set before it).  The
 // failed step may have queued writes of its sequence number that land later
 // and would overwrite the release (the GPU runs behind the host), so the
 // release is also queued behind them, on every stream that carries flag
@@ -212,11 +214,12 @@ volatile uint64_t *host_word(cbx_context *c, int rank, int kind, int64_t b) {
 void release_flags(cbx_context *c, int64_t nb) {
   auto &p = c->ipc;
   if (!p.page) return;
+  *host_word(c, p.me, kIpcBroken, 0) = 1;
+  __atomic_thread_fence(__ATOMIC_SEQ_CST);
   for (int64_t b = 0; b < kIpcMaxBuckets; ++b) {
     *host_word(c, p.me, kIpcA, b) = kIpcRelease;
     *host_word(c, p.me, kIpcR, b) = kIpcRelease;
   }
-  *host_word(c, p.me, kIpcBroken, 0) = 1;
   __atomic_thread_fence(__ATOMIC_SEQ_CST);
   p.released = true;
   if (nb <= 0 || !p.dpage) return;
@@ -228,14 +231,128 @@ void release_flags(cbx_context *c, int64_t nb) {
         (void)hipStreamWriteValue64(s, p.dpage + ipc_word(p.me, kind, b), kIpcRelease, 0);
 }
 
-// Whether any rank's step in the per-rank peer-read form failed part-way.
-bool any_rank_broken(cbx_context *c) {
+// The first rank whose broken word is set (a step of it failed part-way or
+// was refused), or -1.
+int first_broken_rank(cbx_context *c) {
   for (int h = 0; h < c->G; ++h)
-    if (*host_word(c, h, kIpcBroken, 0) != 0) return true;
-  return false;
+    if (*host_word(c, h, kIpcBroken, 0) != 0) return h;
+  return -1;
+}
+
+bool any_rank_broken(cbx_context *c) { return first_broken_rank(c) >= 0; }
+
+// Polls every stream of every local device until it drains or `seconds`
+// pass (a stream may wait on a flag of a rank that never arrives).
+bool drain_polled(cbx_context *c, int seconds) {
+  const auto t0 = std::chrono::steady_clock::now();
+  for (Device &d : c->devs) {
+    (void)hipSetDevice(d.hip_id);
+    for (hipStream_t s : {d.stream, d.comm_stream, d.a_stream, d.a_stream2}) {
+      hipError_t e = hipErrorNotReady;
+      while (s && (e = hipStreamQuery(s)) == hipErrorNotReady &&
+             std::chrono::steady_clock::now() - t0 < std::chrono::seconds(seconds))
+        sched_yield();
+      if (s && e == hipErrorNotReady) return false;
+    }
+  }
+  return true;
 }
 
 }  // namespace
+
+int peer_guard(cbx_context *c, const char *what) {
+  auto &p = c->ipc;
+  if (!p.ready) return CBX_OK;
+  const int h = first_broken_rank(c);
+  if (h < 0 && !p.broken) return CBX_OK;
+  // A rank already waiting on this one's flags of a step this rank will now
+  // never run must go on: release them, whatever this call was.
+  if (!p.released) release_flags(c, p.max_nb);
+  p.broken = true;
+  const uint64_t poisoned = *host_word(c, p.me, kIpcPoison, 0);
+  return fail(CBX_ERR_STATE, "%s refused: a per-rank peer-read step failed part-way earlier on this or another rank "
+              "(rank %d's broken word is set; flags released)%s; z / last may differ across ranks, so every "
+              "collective step is refused until cbx_resync_base", what, h < 0 ? p.me : h,
+              poisoned ? fmt_msg(", and this rank's step %llu read released flags",
+                                 (unsigned long long)poisoned).c_str() : "");
+}
+
+int peer_wait_check(cbx_context *c) {
+  auto &p = c->ipc;
+  if (!p.ready) return CBX_OK;
+  const uint64_t poisoned = *host_word(c, p.me, kIpcPoison, 0);
+  if (poisoned == 0) return CBX_OK;
+  if (!p.released) release_flags(c, p.max_nb);
+  p.broken = true;
+  return fail(CBX_ERR_STATE, "peer-read step %llu on rank %d ran after a rank's step failed part-way (its kernel B "
+              "found a broken word once its loads returned): this rank's z / last are undefined from that step on, "
+              "and every collective step is refused until cbx_resync_base", (unsigned long long)poisoned, p.me);
+}
+
+// Every rank calls it (the broadcast and both barriers are collectives).  A
+// rank that knows of a failure releases its flags first, so every rank's
+// queued steps drain; the page is cleared only once every rank has drained
+// (barrier 1), and no rank starts a step before every rank has cleared its
+// words (barrier 2): a step's first wait must not pass on a stale release.
+int resync_base(cbx_context *c, int root) {
+  if (root < 0 || root >= c->G) return fail(CBX_ERR_INVALID, "cbx_resync_base: root %d out of range (G %d)", root, c->G);
+  if (c->G == 1) return CBX_OK;
+  TRY(flush_task_waits(c));
+  auto &p = c->ipc;
+  if (p.ready && !p.released) {
+    bool known = p.broken || any_rank_broken(c);
+    for (int h = 0; h < c->G && !known; ++h) known = *host_word(c, h, kIpcPoison, 0) != 0;
+    if (known) release_flags(c, p.max_nb);
+  }
+  if (!drain_polled(c, 60))
+    return fail(CBX_ERR_STATE, "cbx_resync_base: this rank's streams still wait 60 s on (a rank that never called "
+                "cbx_resync_base?)");
+  TRY(ensure_comms(c));
+  auto barrier = [&]() -> int {
+    NCCL_TRY(ncclGroupStart());
+    for (Device &d : c->devs) {
+      HIP_TRY(hipSetDevice(d.hip_id));
+      float *x = base_ctrl(d, CBX_BUF_DIFF);  // scratch: every step rewrites D's control block
+      NCCL_TRY(ncclAllReduce(x, x, 1, ncclFloat, ncclSum, d.comm, d.stream));
+    }
+    NCCL_TRY(ncclGroupEnd());
+    if (!drain_polled(c, 60))
+      return fail(CBX_ERR_STATE, "cbx_resync_base: a rank never reached the barrier (60 s)");
+    return CBX_OK;
+  };
+  NCCL_TRY(ncclGroupStart());
+  for (Device &d : c->devs) {
+    HIP_TRY(hipSetDevice(d.hip_id));
+    const size_t count = (size_t)c->n4 * 4;
+    float *z = base_dev(c, d, CBX_BUF_DATA);
+    NCCL_TRY(ncclBroadcast(z, z, count, ncclFloat, root, d.comm, d.stream));
+    if (c->has_last) {
+      float *l = base_dev(c, d, CBX_BUF_LAST);
+      NCCL_TRY(ncclBroadcast(l, l, count, ncclFloat, root, d.comm, d.stream));
+    }
+  }
+  NCCL_TRY(ncclGroupEnd());
+  TRY(barrier());
+  if (p.ready) {
+    for (int64_t b = 0; b < kIpcMaxBuckets; ++b) {
+      *host_word(c, p.me, kIpcA, b) = 0;
+      *host_word(c, p.me, kIpcR, b) = 0;
+    }
+    *host_word(c, p.me, kIpcPoison, 0) = 0;
+    *host_word(c, p.me, kIpcBroken, 0) = 0;
+    __atomic_thread_fence(__ATOMIC_SEQ_CST);
+    TRY(barrier());
+    p.seq = 0;  // every rank's next step in the form is number 1 again
+    p.broken = false;
+    p.released = false;
+  }
+  for (Device &d : c->devs) {
+    d.cross_valid = false;
+    d.span_last = -1;
+  }
+  c->foreign_ops.fetch_add(1, std::memory_order_acq_rel);
+  return CBX_OK;
+}
 
 int peer_export(cbx_context *c, void *blob, size_t *bytes) {
   if (!c->manager) return fail(CBX_ERR_STATE, "cbx_peer_export: set the model manager first");
@@ -420,7 +537,10 @@ void peer_close(cbx_context *c) {
     if (!drained) {
       // This rank's streams wait on flags a peer will never write (it died
       // mid-step): write the release into every rank's words on its behalf
-      // (the page is shared), so the waits end and the streams drain.
+      // (the page is shared), so the waits end and the streams drain; the
+      // broken word first, so a kernel B that the release lets run is poisoned.
+      *host_word(c, p.me, kIpcBroken, 0) = 1;
+      __atomic_thread_fence(__ATOMIC_SEQ_CST);
       for (int h = 0; h < c->G; ++h)
         for (int64_t b = 0; b < kIpcMaxBuckets; ++b) {
           *host_word(c, h, kIpcA, b) = kIpcRelease;
@@ -444,7 +564,10 @@ void peer_close(cbx_context *c) {
     // Streams still queued against the others' memory: unmapping it (or the
     // pinned page their waits read) under them would fault the device.  Leak
     // the mappings and the page instead; the process is going down anyway.
+    // The name goes all the same: unlinking a mapped, pinned
+    // object only removes /dev/shm's entry, so no run leaves one behind.
     release_flags(c, 0);
+    if (p.owner) shm_unlink(p.shm_name);
     p.mapped.clear();
     p.page = nullptr;
     p.dpage = nullptr;
@@ -673,19 +796,11 @@ struct SplitStep {
     rsag = c->allreduce_algo == CBX_ALLREDUCE_RSAG;
     peer = c->allreduce_algo == CBX_ALLREDUCE_PEER && c->G > 1;
     ipc = peer && c->per_rank;
-    if (c->ipc.ready && !c->ipc.released && any_rank_broken(c)) {
-      // Another rank's peer-read step failed part-way.  A rank that had
-      // already enqueued its next peer-read step waits on this rank's flags
-      // of it, which this rank will now never write (this step refuses the
-      // form, or takes another): release them, whatever form this step takes.
-      c->ipc.broken = true;
-      release_flags(c, c->ipc.max_nb);
-    }
+    // Any form: refused once a rank is broken (synchronise_impl checked
+    // already; a step that reaches here another way is checked all the same).
+    TRY(peer_guard(c, "the split step"));
     if (ipc) {
-      if (!c->ipc.ready || c->ipc.broken)
-        return fail(CBX_ERR_STATE, c->ipc.broken ? "the per-rank peer-read form failed part-way earlier on this or "
-                                                   "another rank (flags released)"
-                                                 : "the per-rank peer-read form needs cbx_peer_import");
+      if (!c->ipc.ready) return fail(CBX_ERR_STATE, "the per-rank peer-read form needs cbx_peer_import");
       if (nb > kIpcMaxBuckets)
         return fail(CBX_ERR_UNSUPPORTED, "the per-rank peer-read form takes at most %lld buckets (%lld asked)",
                     (long long)kIpcMaxBuckets, (long long)nb);
@@ -1035,6 +1150,12 @@ struct SplitStep {
         p.G = pn();
         p.shard4 = peer_shard4(len_of(b), p.G);
         for (int h = 0; h < p.G; ++h) p.D[h] = p_D(h) + start_of(b);
+        if (ipc) {  // the poison check (context_internal.h, kIpcPoison)
+          p.broken = c->ipc.dpage + ipc_word(0, kIpcBroken, 0);
+          p.broken_stride = (int64_t)kIpcRankWords;
+          p.poison = c->ipc.dpage + ipc_word(c->ipc.me, kIpcPoison, 0);
+          p.seq = seq;
+        }
         HIP_TRY(cbx::launch_sma_peer_apply(a, p, mom, cfg, d.stream, t));
       } else {
         HIP_TRY(cbx::launch_sma_apply(a, mom && !rsag, cfg, d.stream, t));

@@ -120,7 +120,8 @@ def tune_buckets(gpu, n: int, world: int, step: Callable[[], None], candidates=(
                  group_candidates=(2, 4), progress: Optional[Callable[[str], None]] = None,
                  ndev: Optional[int] = None, peer: bool = False, peer_only: bool = False,
                  peer_candidates=(1, 4, 8), threads: bool = False,
-                 phase: Optional[Callable[[str], None]] = None) -> Tuning:
+                 phase: Optional[Callable[[str], None]] = None,
+                 refresh: Optional[Callable[[], None]] = None) -> Tuning:
     """Pick the configuration of the G > 1 pipeline (kernel A / collective /
     kernel B per bucket) by timing each candidate on the live communicator,
     the way a runtime tunes itself in its warm-up.
@@ -163,7 +164,10 @@ def tune_buckets(gpu, n: int, world: int, step: Callable[[], None], candidates=(
     ``Tuning.errors``; the sweep goes on.  ``phase(name)`` (if given) is
     called before each candidate, ``progress`` receives one line per timed
     candidate.  ``ndev`` is the number of GPUs (default ``world``: one
-    process per GPU).
+    process per GPU).  ``refresh()`` (if given) runs before each candidate's
+    warm-up, outside its timing: bench.py puts the fresh synthetic state back
+    there, so no candidate runs on values that many earlier steps drove far
+    from it (a step's arithmetic per element does not depend on them).
 
     Keys: "<buckets>/<mode>" for stride 1, "<buckets>/<mode>/s<stride>", the
     same + "/rsag" or "/peer" for the other forms, "<key of the winner>/g<group>"
@@ -206,6 +210,8 @@ def tune_buckets(gpu, n: int, world: int, step: Callable[[], None], candidates=(
         candidate failed on some rank and is dropped on every rank."""
         if phase:
             phase(f"tune {key}")
+        if refresh:
+            refresh()
         if failed_anywhere(key, run_steps(warmup)):
             return None
         barrier(world)

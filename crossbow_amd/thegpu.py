@@ -246,6 +246,10 @@ class TheGPU:
         """
         check(self._L.cbx_replica_optimise(self._ctx, id, task, ctypes.c_void_p(stream) if stream else None))
 
+    def task_wait_count(self, local: int = 0) -> int:
+        """Entries in the deferred task-stream wait table of a local device (cbx_task_wait_count; at most 64)."""
+        return check(self._L.cbx_task_wait_count(self._ctx, local))
+
     def replica_copy(self, id: int) -> int:
         return check(self._L.cbx_replica_get_copy(self._ctx, id))
 
@@ -440,6 +444,11 @@ class TheGPU:
             raise CbxError(_lib.CBX_ERR_INVALID, "peer_import: every blob must be PEER_BLOB_BYTES long")
         joined = b"".join(blobs)
         check(self._L.cbx_peer_import(self._ctx, joined, len(blobs)))
+
+    def resync_base(self, root: int = 0) -> None:
+        """Every rank: broadcast z and last from `root` and clear the peer-read form's failure state
+        (cbx_resync_base); after a failed step every collective step is refused until this runs."""
+        check(self._L.cbx_resync_base(self._ctx, root))
 
     def set_staging_mode(self, mode: int) -> None:
         """synchronise_staged: STAGING_ZEROCOPY (kernels read / write the pinned mirror) or STAGING_DMA (copies)."""

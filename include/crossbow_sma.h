@@ -247,7 +247,13 @@ int cbx_replica_set_disabled (cbx_context *ctx, int id, int flag);
  * next call that works on the device (synchronise, wait, staging, reads,
  * writes, add / del, free): the wait is queued then, not at once, so it is
  * not pending on another hardware queue while the update runs.
- * Nesterov
+ * The library keeps one event per caller stream with an update whose wait
+ * it has not yet seen complete: a stream it has not seen first drops the
+ * entries whose event has completed (their update is done), so task
+ * streams that come and go leave nothing behind; at 64 entries per device
+ * the pending waits are queued on the sync stream at once (and, if that
+ * frees none, the oldest entry's event is waited for on the host).
+ * cbx_task_wait_count reports the table's size.  Nesterov
  * momentum is CBX_ERR_UNSUPPORTED, as in the reference (sma.cu:46-48).
  * Under update model WORKER the step is crossbowKernelOptimiserSynchronousSGD
  * (synchronoussgd.cu:3-56) instead: weight decay, then the lr-scaled
@@ -257,6 +263,9 @@ int cbx_replica_set_disabled (cbx_context *ctx, int id, int flag);
  * replica and its device's base model take the same step, in one pass on
  * the sync stream (the task stream waits for it).                       */
 int cbx_replica_optimise (cbx_context *ctx, int id, int task, void *stream);
+/* Entries in local device `local`'s table of deferred task-stream waits
+ * (see cbx_replica_optimise; at most 64). */
+int cbx_task_wait_count (cbx_context *ctx, int local);
 /* Global device index a replica lives on (id % G). */
 int cbx_replica_device (cbx_context *ctx, int id);
 /* 1 if the replica lives in this process. */
@@ -285,7 +294,10 @@ int cbx_stage_in (cbx_context *ctx);
 int cbx_stage_out (cbx_context *ctx);
 int cbx_replica_host_buffer (cbx_context *ctx, int id, int kind, void **host_ptr);
 int cbx_base_host_buffer (cbx_context *ctx, int device, int kind, void **host_ptr);
-/* Block until every local sync stream has drained. */
+/* Block until every local sync stream has drained.  One process per GPU
+ * with the peer-read form imported: CBX_ERR_STATE if a drained step's kernel
+ * B on this rank ran after a rank's step failed (cbx_peer_import below):
+ * this rank's z and last are then undefined, until cbx_resync_base. */
 int cbx_wait (cbx_context *ctx);
 /* The event (a hipEvent_t, as void*) recorded on local device `local`'s sync
  * stream at the end of every synchronise(): it stands for the reference's
@@ -445,16 +457,47 @@ int cbx_set_allreduce_algorithm (cbx_context *ctx, int algorithm);
  * 60 s in all, streams polled) until every rank is done with this rank's
  * memory; if a dead peer left this rank's streams waiting, it writes the
  * release into every rank's flags itself.  Every rank calls export, import
- * and free.  A step that fails part-way, on any rank, releases that rank's
- * flags (from the host and behind its queued flag writes) and marks it
- * broken on the page; every rank's next step (in any form) releases its own
- * flags, and further steps in this form are refused (CBX_ERR_STATE), so no
- * stream waits forever
- * and no rank reads a failed rank's stale buffers.  The other collective
- * forms keep working.                                                     */
+ * and free.
+ * Failure (the reference's answer to any failure is exit(1), debug.h:37; the
+ * invariant at stake is that every GPU applies the same D to the same z,
+ * synch/sma.c:168-174):
+ *   - A step that fails part-way on a rank sets that rank's broken word on
+ *     the page, then releases its flags (from the host, and again behind its
+ *     queued flag writes), so no other rank's stream waits forever.
+ *   - A released flag lets a wait pass whether or not the data it guards was
+ *     written, so a step another rank had already enqueued may read the
+ *     failed rank's stale acc or D.  Every kernel B of the form therefore
+ *     reads every rank's broken word once its own loads have returned; a
+ *     wave that finds one set records the step's sequence number on the
+ *     page.  cbx_wait on that rank then returns CBX_ERR_STATE naming the
+ *     step: its z and last are undefined from that step on.  A step whose
+ *     cbx_wait reports nothing read only data that was complete (any stale
+ *     read needs a release, and the broken word comes before it).
+ *   - From the moment any rank's broken word is visible to a rank, that
+ *     rank refuses EVERY collective step (cbx_synchronise and
+ *     cbx_synchronise_staged in every all-reduce form and update model, and
+ *     cbx_average_batchnorm_stats) with CBX_ERR_STATE, releasing its own
+ *     flags first, until cbx_resync_base.  The decision is each rank's own,
+ *     made from the page when it is called: a rank that enqueued an RCCL-
+ *     form step before the failure reached it may wait inside that step's
+ *     collective for a rank that refuses it, so after a failure on any rank
+ *     every rank stops stepping and calls cbx_resync_base.
+ * Same results bit for bit as before whenever no rank fails.              */
 #define CBX_PEER_BLOB_BYTES 256
 int cbx_peer_export (cbx_context *ctx, void *blob, size_t *bytes);
 int cbx_peer_import (cbx_context *ctx, const void *blobs, int nranks);
+/* Re-synchronise the base models after a failure (or at any time): every
+ * rank calls it (a collective over the RCCL communicator).  Releases this
+ * rank's flags if it knows of a failure, waits (up to 60 s, polled) until its
+ * streams drain, broadcasts z and last (device buffers, padded length) from
+ * rank `root`, and, once every rank has drained and received them, clears
+ * this rank's flag words, broken and poison words and restarts the form's
+ * step numbering; a second barrier keeps every rank from starting a step
+ * before every rank's words are clear.  Afterwards z and last are identical
+ * on every rank and every form is accepted again.  Replicas (w_i, s_i) are
+ * left as they are (a Phase-D copy request resets them to z).  No-op at
+ * G = 1.                                                                  */
+int cbx_resync_base (cbx_context *ctx, int root);
 /* How cbx_synchronise_staged moves the model between the pinned host mirror
  * and the device (north_star: the path starts and ends in host memory):
  *   CBX_STAGING_ZEROCOPY (0, default): the SMA kernels read their inputs

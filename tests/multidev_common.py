@@ -488,6 +488,65 @@ def run_autotune_checkpoint(g: Ctx, world: int, local: List[int], ckdir: str, ex
     return bad
 
 
+def _save_npy(d: str, name: str, arr) -> None:
+    tmp = os.path.join(d, name + ".tmp")
+    with open(tmp, "wb") as f:
+        np.save(f, arr)
+    os.replace(tmp, os.path.join(d, name + ".npy"))
+
+
+def save_full_state(g: Ctx, d: str, rank: int, mine: List[int], n: int) -> None:
+    """One rank's whole initial state (z, last, s and w of its replicas) as
+    .npy files under `d`, then its `in_<rank>.ok` marker: the input of
+    full_size_check on every rank."""
+    A = g.A
+    _save_npy(d, f"z_{rank}", g.read("cbx_base_read", rank, A.BUF_DATA, n))
+    _save_npy(d, f"last_{rank}", g.read("cbx_base_read", rank, A.BUF_LAST, n))
+    for i in mine:
+        _save_npy(d, f"s_{i}", g.read("cbx_replica_read", i, A.BUF_DIFF, n))
+        _save_npy(d, f"w_{i}", g.read("cbx_replica_read", i, A.BUF_DATA, n))
+    with open(os.path.join(d, f"in_{rank}.ok"), "w"):
+        pass
+
+
+CHUNK = 1 << 20  # elements per oracle chunk
+
+
+def full_size_check(d: str, world: int, R: int, steps: int, rank: int, z1, l1, w1: Dict[int, np.ndarray],
+                    exact: bool, alpha: float = 0.1, mom: float = 0.9):
+    """Rank `rank`'s z, last and w after `steps` SMA steps against the oracle
+    in EVERY element (no sample).  The oracle runs chunk by chunk
+    over every rank's memory-mapped saved inputs: the step is elementwise
+    (no Phase-D copy in these runs), so a chunk's result is the whole run's.
+    Returns (bad, differs, compared elements)."""
+    O = oracle()
+    n = z1.size
+    size = world * R
+    wait_files([os.path.join(d, f"in_{r}.ok") for r in range(world)], seconds=180)
+    mm = lambda name: np.load(os.path.join(d, name + ".npy"), mmap_mode="r")  # noqa: E731
+    zs = [mm(f"z_{r}") for r in range(world)]
+    ls = [mm(f"last_{r}") for r in range(world)]
+    S = [mm(f"s_{i}") for i in range(size)]
+    W = [mm(f"w_{i}") for i in range(size)]
+    bad = []
+    if any(not np.array_equal(np.asarray(z).view(np.uint32), np.asarray(zs[0]).view(np.uint32)) for z in zs):
+        bad.append("initial z differs across ranks")
+    check = Checker(exact=exact)
+    compared = 0
+    for a in range(0, n, CHUNK):
+        b = min(n, a + CHUNK)
+        cut = lambda arrs: [np.array(x[a:b]) for x in arrs]  # noqa: E731
+        st = O.SmaState(world, size, b - a, alpha, mom, cut(zs), cut(ls), cut(S), cut(W))
+        for _ in range(steps):
+            O.sma_step(st)
+        check(f"z[{a}:{b}]", z1[a:b], st.z[rank])
+        check(f"last[{a}:{b}]", l1[a:b], st.last[rank])
+        for i, w in w1.items():
+            check(f"w[{i}][{a}:{b}]", w[a:b], st.w[i])
+        compared += (2 + len(w1)) * (b - a)
+    return bad + check.bad[:20], check.differs, compared
+
+
 def wait_files(paths, seconds=90.0):
     t0 = time.time()
     while not all(os.path.exists(p) for p in paths):

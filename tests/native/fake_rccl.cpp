@@ -17,7 +17,8 @@
 //    runs the collective for all, the others wait for it (60 s, then
 //    ncclSystemError).
 //
-// Calls: ncclAllReduce, ncclReduceScatter and ncclAllGather (fp32; sum).
+// Calls: ncclAllReduce, ncclReduceScatter, ncclAllGather (fp32; sum) and
+// ncclBroadcast (fp32; cbx_resync_base).
 // Each collective synchronises the stream it was given (so every kernel the
 // library ordered before it has finished), sums the ranks' send buffers on
 // the host, writes the result to every receive buffer with a blocking copy
@@ -169,7 +170,7 @@ void reduce(const std::vector<const float *> &src, size_t count, bool ring, floa
   }
 }
 
-enum OpKind { kAllReduce = 0, kReduceScatter = 1, kAllGather = 2 };
+enum OpKind { kAllReduce = 0, kReduceScatter = 1, kAllGather = 2, kBroadcast = 3 };
 
 // Floats of one rank's send buffer / receive buffer for a call with `count`
 // (the NCCL argument: recvcount for reduce-scatter, sendcount for all-gather).
@@ -180,9 +181,14 @@ size_t recv_elems(int kind, size_t count, int G) { return kind == kAllGather ? c
 // buffers: what rank `rank` receives, into out (recv_elems floats).
 //   all-reduce: the sum;  reduce-scatter: rank's slice of the sum (the ring
 //   order, if on, is that of a ring all-reduce's reduce phase);  all-gather:
-//   the concatenation in rank order.
-void collective(int kind, const std::vector<const float *> &src, size_t count, bool ring, int rank, float *out) {
+//   the concatenation in rank order;  broadcast: root's buffer.
+void collective(int kind, const std::vector<const float *> &src, size_t count, bool ring, int rank, float *out,
+                int root) {
   const int G = (int)src.size();
+  if (kind == kBroadcast) {
+    std::memcpy(out, src[root], count * sizeof(float));
+    return;
+  }
   if (kind == kAllGather) {
     for (int r = 0; r < G; ++r) std::memcpy(out + (size_t)r * count, src[r], count * sizeof(float));
     return;
@@ -201,6 +207,7 @@ struct PendingOp {
   size_t count;
   ncclComm *comm;
   hipStream_t stream;
+  int root;
 };
 
 thread_local int g_depth = 0;
@@ -215,7 +222,7 @@ ncclResult_t run_clique(const std::vector<PendingOp *> &ops) {
   std::vector<std::vector<float>> host(G, std::vector<float>(ns));
   std::vector<const float *> src(G);
   for (int r = 0; r < G; ++r) {
-    if (ops[r]->count != count || ops[r]->kind != kind) return ncclInvalidArgument;
+    if (ops[r]->count != count || ops[r]->kind != kind || ops[r]->root != ops[0]->root) return ncclInvalidArgument;
     if (hipSetDevice(ops[r]->comm->device) != hipSuccess) return ncclSystemError;
     if (hipStreamSynchronize(ops[r]->stream) != hipSuccess) return ncclSystemError;
     if (hipMemcpy(host[r].data(), ops[r]->send, ns * sizeof(float), hipMemcpyDeviceToHost) != hipSuccess)
@@ -224,7 +231,7 @@ ncclResult_t run_clique(const std::vector<PendingOp *> &ops) {
   }
   std::vector<float> out(nr);
   for (int r = 0; r < G; ++r) {
-    collective(kind, src, count, ops[0]->comm->ring, r, out.data());
+    collective(kind, src, count, ops[0]->comm->ring, r, out.data(), ops[0]->root);
     if (hipSetDevice(ops[r]->comm->device) != hipSuccess) return ncclSystemError;
     if (hipMemcpy(ops[r]->recv, out.data(), nr * sizeof(float), hipMemcpyHostToDevice) != hipSuccess)
       return ncclSystemError;
@@ -260,7 +267,8 @@ ncclResult_t rendezvous(const PendingOp &op) {
 }
 
 // The per-rank (multi-process) collective through files.
-ncclResult_t run_ranked(int kind, const void *send, void *recv, size_t count, ncclComm *c, hipStream_t stream) {
+ncclResult_t run_ranked(int kind, const void *send, void *recv, size_t count, ncclComm *c, hipStream_t stream,
+                        int root) {
   if (hipStreamSynchronize(stream) != hipSuccess) return ncclSystemError;
   const size_t ns = send_elems(kind, count, c->nranks), nr = recv_elems(kind, count, c->nranks);
   const size_t bytes = ns * sizeof(float);
@@ -279,7 +287,7 @@ ncclResult_t run_ranked(int kind, const void *send, void *recv, size_t count, nc
     src[r] = host[r].data();
   }
   std::vector<float> out(nr);
-  collective(kind, src, count, c->ring, c->rank, out.data());
+  collective(kind, src, count, c->ring, c->rank, out.data(), root);
   if (hipMemcpy(recv, out.data(), nr * sizeof(float), hipMemcpyHostToDevice) != hipSuccess) return ncclSystemError;
   if (c->nranks > 1) {
     // Every rank acknowledges; a rank removes its data file once all have read it.
@@ -294,15 +302,15 @@ ncclResult_t run_ranked(int kind, const void *send, void *recv, size_t count, nc
 }
 
 ncclResult_t enqueue(int kind, const void *send, void *recv, size_t count, ncclDataType_t type, ncclComm_t c,
-                     hipStream_t stream) {
-  if (!c || type != ncclFloat) return ncclInvalidArgument;
+                     hipStream_t stream, int root = 0) {
+  if (!c || type != ncclFloat || root < 0 || root >= c->nranks) return ncclInvalidArgument;
   if (c->noop) return ncclSuccess;
   if (c->clique) {
     if (g_depth == 0) return ncclInvalidUsage;
-    g_ops.push_back(PendingOp{kind, send, recv, count, c, stream});
+    g_ops.push_back(PendingOp{kind, send, recv, count, c, stream, root});
     return ncclSuccess;
   }
-  return run_ranked(kind, send, recv, count, c, stream);
+  return run_ranked(kind, send, recv, count, c, stream, root);
 }
 
 }  // namespace
@@ -446,6 +454,11 @@ ncclResult_t ncclReduceScatter(const void *send, void *recv, size_t recvcount, n
 ncclResult_t ncclAllGather(const void *send, void *recv, size_t sendcount, ncclDataType_t type, ncclComm_t c,
                            hipStream_t stream) {
   return enqueue(kAllGather, send, recv, sendcount, type, c, stream);
+}
+
+ncclResult_t ncclBroadcast(const void *send, void *recv, size_t count, ncclDataType_t type, int root, ncclComm_t c,
+                           hipStream_t stream) {
+  return enqueue(kBroadcast, send, recv, count, type, c, stream, root);
 }
 
 }  // extern "C"

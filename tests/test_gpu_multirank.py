@@ -161,6 +161,10 @@ N_RESNET50 = 25_557_032
 
 
 def _full_size_main(rank, world, R, steps, mode, order, uid, fake_dir, q):
+    """Every rank saves its whole initial state, steps, and then checks its
+    own z, last and w against the oracle over EVERY element (no
+    sample), the oracle run chunk by chunk over every rank's memory-mapped
+    inputs."""
     os.environ["FAKE_RCCL_DIR"] = fake_dir
     os.environ["FAKE_RCCL_ORDER"] = order
     try:
@@ -174,16 +178,7 @@ def _full_size_main(rank, world, R, steps, mode, order, uid, fake_dir, q):
             g("cbx_fill_synthetic", O.SEED)  # the same generator on every rank
             size = world * R
             mine = [i for i in range(size) if i % world == rank]
-            rng = np.random.default_rng(11)
-            idx = np.unique(np.concatenate([rng.integers(0, n, 60_000), np.arange(4), np.arange(n - 4, n),
-                                            np.arange(3_194_000, 3_196_000)]))  # a dense window across a bucket edge
-            z0 = g.read("cbx_base_read", rank, A.BUF_DATA, n)[idx]
-            l0 = g.read("cbx_base_read", rank, A.BUF_LAST, n)[idx]
-            s0 = np.stack([g.read("cbx_replica_read", i, A.BUF_DIFF, n)[idx] for i in mine])
-            w0 = np.stack([g.read("cbx_replica_read", i, A.BUF_DATA, n)[idx] for i in mine])
-            tmp = os.path.join(fake_dir, f"in_{rank}.tmp.npz")
-            np.savez(tmp, z=z0, last=l0, s=s0, w=w0, ids=np.array(mine))
-            os.replace(tmp, os.path.join(fake_dir, f"in_{rank}.npz"))
+            C.save_full_state(g, fake_dir, rank, mine, n)
             for step in range(steps):
                 g("cbx_lock_any")
                 g("cbx_synchronise", 0, step + 1, 0, 0)
@@ -192,45 +187,34 @@ def _full_size_main(rank, world, R, steps, mode, order, uid, fake_dir, q):
             z1 = g.read("cbx_base_read", rank, A.BUF_DATA, n)
             l1 = g.read("cbx_base_read", rank, A.BUF_LAST, n)
             dig = C.digest(z1, l1)
-            w1 = {i: g.read("cbx_replica_read", i, A.BUF_DATA, n)[idx] for i in mine}
+            w1 = {i: g.read("cbx_replica_read", i, A.BUF_DATA, n) for i in mine}
         finally:
             g.free()
-        # the oracle over every rank's sampled inputs (the step is elementwise)
-        C.wait_files([os.path.join(fake_dir, f"in_{r}.npz") for r in range(world)])
-        ins = [np.load(os.path.join(fake_dir, f"in_{r}.npz")) for r in range(world)]
-        s, w = [None] * size, [None] * size
-        for f in ins:
-            for k, i in enumerate(f["ids"]):
-                s[int(i)], w[int(i)] = f["s"][k].copy(), f["w"][k].copy()
-        bad = []
-        if any(not np.array_equal(f["z"].view(np.uint32), z0.view(np.uint32)) for f in ins):
-            bad.append("initial z differs across ranks")
-        st = O.SmaState(world, size, idx.size, 0.1, 0.9, [f["z"].copy() for f in ins],
-                        [f["last"].copy() for f in ins], s, w)
-        for _ in range(steps):
-            O.sma_step(st)
-        check = C.Checker(exact=order == "rank")
-        check("z sample", z1[idx], st.z[rank])
-        check("last sample", l1[idx], st.last[rank])
-        for i in mine:
-            check(f"w[{i}] sample", w1[i], st.w[i])
-        q.put((rank, {"bad": bad + check.bad, "digest": dig, "differs": check.differs}, None))
+        bad, differs, compared = C.full_size_check(fake_dir, world, R, steps, rank, z1, l1, w1, exact=order == "rank")
+        q.put((rank, {"bad": bad, "digest": dig, "differs": differs, "compared": compared}, None))
     except Exception:  # pragma: no cover - reported to the parent
         import traceback
         q.put((rank, None, traceback.format_exc()))
 
 
+@pytest.mark.timeout(330)
 @pytest.mark.skipif(not os.path.exists(C.VARIANT), reason="run scripts/build_fake_rccl.sh first")
-@pytest.mark.parametrize("world,R,mode,order", [(4, 2, 0, "rank"),   # C4: 2 replicas/GPU x 4, bit for bit
-                                                (8, 4, 1, "ring")])  # C5: 4 replicas/GPU x 8, RCCL's order
+@pytest.mark.parametrize("world,R,mode,order", [(2, 2, 0, "rank"),   # C4's form at 2 ranks, bit for bit
+                                                (4, 2, 0, "rank"),   # C4: 2 replicas/GPU x 4, bit for bit
+                                                (8, 4, 1, "rank"),   # C5: 4 replicas/GPU x 8, bit for bit
+                                                (8, 4, 1, "ring")])  # C5 in RCCL's order: the tolerance
 def test_resnet50_full_size_multirank(world, R, mode, order):
     uid = os.urandom(16) + bytes(112)
     steps = 3
-    with tempfile.TemporaryDirectory(dir=C.loopback_dir(2 << 30)) as fake_dir:
+    need = (2 * world + 2 * world * R) * N_RESNET50 * 4 + (1 << 30)
+    with tempfile.TemporaryDirectory(dir=C.loopback_dir(need)) as fake_dir:
         res = _spawn(world, _full_size_main, lambda r: (r, world, R, steps, mode, order, uid, fake_dir),
-                     timeout=110)
+                     timeout=300)
     for r in range(world):
         assert not res[r]["bad"], f"rank {r}: {res[r]['bad']}"
+        assert res[r]["compared"] == (2 + R) * N_RESNET50, res[r]["compared"]
+    print(f"C{'4' if R == 2 else '5'} full size, {world} ranks x R {R}, order {order}: every rank compared "
+          f"{res[0]['compared']} elements (z, last, {R} w; n = {N_RESNET50} each)")
     assert len({res[r]["digest"] for r in range(world)}) == 1, "z / last differ across ranks at full size"
     if order == "ring":
         assert sum(res[r]["differs"] for r in range(world)) > 0, "ring order never left the oracle's order"

@@ -172,16 +172,7 @@ def _full_size_main(rank, world, R, steps, d, q):
             g("cbx_fill_synthetic", O.SEED)
             size = world * R
             mine = [i for i in range(size) if i % world == rank]
-            rng = np.random.default_rng(12)
-            idx = np.unique(np.concatenate([rng.integers(0, n, 60_000), np.arange(4), np.arange(n - 4, n),
-                                            np.arange(6_389_000, 6_391_000)]))  # across the 4 ranks' shards
-            z0 = g.read("cbx_base_read", rank, A.BUF_DATA, n)[idx]
-            l0 = g.read("cbx_base_read", rank, A.BUF_LAST, n)[idx]
-            s0 = np.stack([g.read("cbx_replica_read", i, A.BUF_DIFF, n)[idx] for i in mine])
-            w0 = np.stack([g.read("cbx_replica_read", i, A.BUF_DATA, n)[idx] for i in mine])
-            tmp = os.path.join(d, f"in_{rank}.tmp.npz")
-            np.savez(tmp, z=z0, last=l0, s=s0, w=w0, ids=np.array(mine))
-            os.replace(tmp, os.path.join(d, f"in_{rank}.npz"))
+            C.save_full_state(g, d, rank, mine, n)
             for step in range(steps):
                 g("cbx_lock_any")
                 g("cbx_synchronise", 0, step + 1, 0, 0)
@@ -190,40 +181,28 @@ def _full_size_main(rank, world, R, steps, d, q):
             z1 = g.read("cbx_base_read", rank, A.BUF_DATA, n)
             l1 = g.read("cbx_base_read", rank, A.BUF_LAST, n)
             dig = C.digest(z1, l1)
-            w1 = {i: g.read("cbx_replica_read", i, A.BUF_DATA, n)[idx] for i in mine}
+            w1 = {i: g.read("cbx_replica_read", i, A.BUF_DATA, n) for i in mine}
         finally:
             g.free()
-        C.wait_files([os.path.join(d, f"in_{r}.npz") for r in range(world)])
-        ins = [np.load(os.path.join(d, f"in_{r}.npz")) for r in range(world)]
-        s, w = [None] * size, [None] * size
-        for f in ins:
-            for k, i in enumerate(f["ids"]):
-                s[int(i)], w[int(i)] = f["s"][k].copy(), f["w"][k].copy()
-        st = O.SmaState(world, size, idx.size, 0.1, 0.9, [f["z"].copy() for f in ins],
-                        [f["last"].copy() for f in ins], s, w)
-        for _ in range(steps):
-            O.sma_step(st)
-        check = C.Checker(exact=True)
-        check("z sample", z1[idx], st.z[rank])
-        check("last sample", l1[idx], st.last[rank])
-        for i in mine:
-            check(f"w[{i}] sample", w1[i], st.w[i])
-        q.put((rank, {"bad": check.bad, "digest": dig}, None))
+        bad, _, compared = C.full_size_check(d, world, R, steps, rank, z1, l1, w1, exact=True)
+        q.put((rank, {"bad": bad, "digest": dig, "compared": compared}, None))
     except Exception:  # pragma: no cover - reported to the parent
         import traceback
         q.put((rank, None, traceback.format_exc()))
 
 
-@pytest.mark.timeout(300)
+@pytest.mark.timeout(330)
 def test_peer_read_one_process_per_gpu_resnet50_c4():
     # C4 (2 replicas/GPU x 4) at the full ResNet-50 size, cross-step pipeline,
-    # 8 buckets (the library default at G > 1): sampled bit for bit, z and
-    # last identical on every rank.
+    # 8 buckets (the library default at G > 1): every element bit for bit, z
+    # and last identical on every rank.
     world, R = 4, 2
-    with tempfile.TemporaryDirectory(dir=C.loopback_dir(1 << 30)) as d:
-        res = _spawn(world, _full_size_main, lambda r: (r, world, R, 3, d), timeout=280)
+    need = (2 * world + 2 * world * R) * N_RESNET50 * 4 + (1 << 30)
+    with tempfile.TemporaryDirectory(dir=C.loopback_dir(need)) as d:
+        res = _spawn(world, _full_size_main, lambda r: (r, world, R, 3, d), timeout=300)
     for r in range(world):
         assert not res[r]["bad"], f"rank {r}: {res[r]['bad']}"
+        assert res[r]["compared"] == (2 + R) * N_RESNET50, res[r]["compared"]
     assert len({res[r]["digest"] for r in range(world)}) == 1, "z / last differ across ranks at full size"
 
 
@@ -244,9 +223,33 @@ def _flag_words(d: str, rank: int, nb: int):
             int(page[base + 2 * IPC_MAX_BUCKETS + 2]))
 
 
+def _save(d: str, name: str, **arrs) -> None:
+    tmp = os.path.join(d, name + ".tmp.npz")
+    np.savez(tmp, **arrs)
+    os.replace(tmp, os.path.join(d, name + ".npz"))
+
+
+def _load_all(d: str, name: str, world: int):
+    C.wait_files([os.path.join(d, f"{name}_{r}.npz") for r in range(world)], seconds=120)
+    return [np.load(os.path.join(d, f"{name}_{r}.npz")) for r in range(world)]
+
+
+def _oracle_state(O, world, size, n, ins, z_from=None):
+    """The job's state from every rank's saved buffers: z / last per rank (or
+    rank `z_from`'s on every rank), s and w per replica."""
+    s, w = [None] * size, [None] * size
+    for f in ins:
+        for k, i in enumerate(f["ids"]):
+            s[int(i)], w[int(i)] = f["s"][k].copy(), f["w"][k].copy()
+    zs = [ins[r if z_from is None else z_from]["z"].copy() for r in range(world)]
+    ls = [ins[r if z_from is None else z_from]["last"].copy() for r in range(world)]
+    return O.SmaState(world, size, n, 0.1, 0.9, zs, ls, s, w)
+
+
 def _failing_main(rank, world, d, q):
     """Rank 1's third peer-read step fails right after it queued its first
-    flag write ($CBX_FAULT_PEER_FAIL="1:3")."""
+    flag write ($CBX_FAULT_PEER_FAIL="1:3").  Every rank then reports what its
+    steps did, is refused in every form, resynchronises, and steps again."""
     import time
     rank_env(rank)
     os.environ["CBX_FAULT_PEER_FAIL"] = "1:3"  # read at context creation
@@ -255,17 +258,38 @@ def _failing_main(rank, world, d, q):
         with open(os.path.join(d, f"progress_{rank}"), "a") as f:
             f.write(f"{time.monotonic():.3f} {what}\n")
 
+    def meet(tag):
+        with open(os.path.join(d, f"{tag}_{rank}"), "w"):
+            pass
+        try:
+            C.wait_files([os.path.join(d, f"{tag}_{r}") for r in range(world)])
+        except TimeoutError as e:
+            report = {r: open(os.path.join(d, f"progress_{r}")).read() if os.path.exists(
+                os.path.join(d, f"progress_{r}")) else "(nothing)" for r in range(world)}
+            raise TimeoutError(f"{e}; progress: {report}") from None
+
     try:
         L, A = load_real()
+        O = C.oracle()
         g = C.init_rank(L, A, rank, world, share_uid(L, rank, os.path.join(d, "uid")))
-        out = {"errors": {}}
+        out = {"errors": {}, "bad": []}
         try:
-            n, nb = 1 << 22, 5
-            C.setup_model(g, A, n, 2, 0.9, 7, A.SYNC_BSP, 2 * world * 2)
+            n, nb, R = 1 << 22, 5, 2
+            size = world * R
+            mine = [i for i in range(size) if i % world == rank]
+            C.setup_model(g, A, n, R, 0.9, 7, A.SYNC_BSP, 2 * world * R)
             exchange(g, rank, world, d, "fail")
             g("cbx_set_allreduce_algorithm", PEER)
             g("cbx_set_bucket_elements", -(-n // nb))
             g("cbx_fill_synthetic", 5)
+
+            def state(tag):  # this rank's whole state, for every rank's oracle
+                _save(d, f"{tag}_{rank}", z=g.read("cbx_base_read", rank, A.BUF_DATA, n),
+                      last=g.read("cbx_base_read", rank, A.BUF_LAST, n),
+                      s=np.stack([g.read("cbx_replica_read", i, A.BUF_DIFF, n) for i in mine]),
+                      w=np.stack([g.read("cbx_replica_read", i, A.BUF_DATA, n) for i in mine]), ids=np.array(mine))
+
+            state("in")
 
             def step(clock):
                 g("cbx_lock_any")
@@ -274,40 +298,77 @@ def _failing_main(rank, world, d, q):
                 finally:
                     g("cbx_unlock_any")
 
+            ok_steps = 0
             for clock in (1, 2, 3):
                 if clock == 3:  # every rank has enqueued steps 1 and 2 before any enqueues step 3
-                    with open(os.path.join(d, f"before3_{rank}"), "w"):
-                        pass
-                    C.wait_files([os.path.join(d, f"before3_{r}") for r in range(world)])
+                    meet("before3")
                 try:
                     step(clock)
+                    ok_steps += 1
                     mark(f"step {clock} enqueued")
                 except RuntimeError as e:
                     out["errors"][clock] = str(e)
                     mark(f"step {clock} refused: {e}")
             t0 = time.monotonic()
-            g("cbx_wait")  # every rank's streams drain: no wait is left on a flag that never comes
+            try:
+                g("cbx_wait")  # every rank's streams drain: no wait is left on a flag that never comes
+                out["wait"] = None
+            except RuntimeError as e:  # a kernel B of this rank ran after a broken word was set
+                out["wait"] = str(e)
             out["drain_s"] = time.monotonic() - t0
-            mark("drained")
+            out["ok_steps"] = ok_steps
+            mark(f"drained: {out['wait']}")
+            if out["wait"] is None:
+                # Nothing reported: every step this rank enqueued must be the
+                # oracle's, bit for bit (rank-order sums), every element.
+                ins = _load_all(d, "in", world)
+                st = _oracle_state(O, world, size, n, ins)
+                for _ in range(ok_steps):
+                    O.sma_step(st)
+                check = C.Checker(exact=True)
+                check(f"z after {ok_steps} steps", g.read("cbx_base_read", rank, A.BUF_DATA, n), st.z[rank])
+                check(f"last after {ok_steps} steps", g.read("cbx_base_read", rank, A.BUF_LAST, n), st.last[rank])
+                if rank != 1:  # rank 1's kernel A of step 3 bucket 0 ran (w moved) before it failed
+                    for i in mine:
+                        check(f"w[{i}] after {ok_steps} steps", g.read("cbx_replica_read", i, A.BUF_DATA, n), st.w[i])
+                out["bad"] += check.bad
             if rank == 1:
                 a, r, broken = _flag_words(d, 1, nb)
                 out["words"] = {"a_min": int(a.min()), "r_min": int(r.min()), "broken": broken}
-            with open(os.path.join(d, f"after3_{rank}"), "w"):
-                pass
-            try:
-                C.wait_files([os.path.join(d, f"after3_{r}") for r in range(world)])
-            except TimeoutError as e:
-                report = {r: open(os.path.join(d, f"progress_{r}")).read() if os.path.exists(
-                    os.path.join(d, f"progress_{r}")) else "(nothing)" for r in range(world)}
-                raise TimeoutError(f"{e}; progress: {report}") from None
-            try:  # the form is unusable on EVERY rank now, not only on the one that failed
-                step(4)
-                out["step4"] = None
-            except RuntimeError as e:
-                out["step4"] = str(e)
-            g("cbx_set_allreduce_algorithm", 0)  # the RCCL form still runs
-            step(5)
+            meet("after3")
+            refused = {}
+            for clock, algo in ((4, PEER), (5, 0)):  # the failure stops EVERY form on EVERY rank
+                g("cbx_set_allreduce_algorithm", algo)
+                try:
+                    step(clock)
+                    refused[clock] = None
+                except RuntimeError as e:
+                    refused[clock] = str(e)
+            out["refused"] = refused
+            meet("before_resync")
+            g("cbx_resync_base", 0)
+            mark("resynced")
+            z = g.read("cbx_base_read", rank, A.BUF_DATA, n)
+            last = g.read("cbx_base_read", rank, A.BUF_LAST, n)
+            out["resync_digest"] = C.digest(z, last)
+            step(5)  # the RCCL form runs again
             g("cbx_wait")
+            out["rccl_digest"] = C.digest(g.read("cbx_base_read", rank, A.BUF_DATA, n),
+                                          g.read("cbx_base_read", rank, A.BUF_LAST, n))
+            state("mid")
+            g("cbx_set_allreduce_algorithm", PEER)  # and so does the peer-read form, from sequence 1
+            step(6)
+            g("cbx_wait")
+            mids = _load_all(d, "mid", world)
+            st = _oracle_state(O, world, size, n, mids)
+            O.sma_step(st)
+            check = C.Checker(exact=True)
+            check("z after the peer step", g.read("cbx_base_read", rank, A.BUF_DATA, n), st.z[rank])
+            check("last after the peer step", g.read("cbx_base_read", rank, A.BUF_LAST, n), st.last[rank])
+            for i in mine:
+                check(f"w[{i}] after the peer step", g.read("cbx_replica_read", i, A.BUF_DATA, n), st.w[i])
+            out["bad"] += check.bad
+            out["compared"] = n
         finally:
             t0 = time.monotonic()
             g.free()
@@ -318,24 +379,35 @@ def _failing_main(rank, world, d, q):
         q.put((rank, None, traceback.format_exc()))
 
 
-@pytest.mark.timeout(200)
+@pytest.mark.timeout(280)
 def test_peer_read_failed_step_releases_and_stops_every_rank():
-    # a rank whose peer-read step fails after queuing flag writes
-    # must leave its words at the release value (the queued writes of the
-    # step's sequence number land BEFORE the queued release), and every other
-    # rank must refuse its next step in the form instead of reading stale
-    # acc / D silently; nobody hangs, the RCCL form still runs, free is bounded.
+    # ADVICE r04 / r05, VERDICT r05: a rank whose peer-read step fails after
+    # queuing flag writes leaves its words at the release value (the queued
+    # writes of the step's sequence number land BEFORE the queued release).
+    # Every step on every rank either equals the oracle (every element) or is
+    # reported: refused when called, or named by cbx_wait because its kernel B
+    # found a broken word.  Then every form is refused on every rank until
+    # cbx_resync_base, after which z / last are identical on every rank and
+    # both the RCCL and the peer-read forms run (the latter bit for bit).
     world = 3
-    with tempfile.TemporaryDirectory(dir=C.loopback_dir()) as d:
-        res = _spawn(world, _failing_main, lambda r: (r, world, d), timeout=180)
+    with tempfile.TemporaryDirectory(dir=C.loopback_dir(1 << 30)) as d:
+        res = _spawn(world, _failing_main, lambda r: (r, world, d), timeout=260)
     assert "fault injection" in res[1]["errors"].get(3, "") and set(res[1]["errors"]) == {3}, res[1]["errors"]
-    for r in (0, 2):
-        # step 3 races rank 1's failure: a rank enqueues it (and its waits on
-        # rank 1 are released) or already refuses it; steps 1 and 2 run
-        errs = res[r]["errors"]
-        assert set(errs) <= {3} and all("failed part-way earlier" in m for m in errs.values()), (r, errs)
+    for r in range(world):
+        errs, wait = res[r]["errors"], res[r]["wait"]
+        assert set(errs) <= {3} and all("failed part-way earlier" in m or "fault injection" in m
+                                        for m in errs.values()), (r, errs)
+        # rank 1 never reduced its shard of step 3: a rank that enqueued step 3
+        # cannot have a correct one, so it must be the one cbx_wait reports
+        if r != 1 and 3 not in errs:
+            assert wait and "ran after a rank's step failed" in wait, (r, wait)
+        assert not res[r]["bad"], (r, res[r]["bad"])
+        assert res[r]["drain_s"] < 30 and res[r]["free_s"] < 70, (r, res[r]["drain_s"], res[r]["free_s"])
+        for clock in (4, 5):
+            m = res[r]["refused"][clock]
+            assert m and "failed part-way earlier" in m and "cbx_resync_base" in m, (r, clock, m)
+        assert res[r]["compared"] == 1 << 22
     w = res[1]["words"]
     assert w["a_min"] >= IPC_RELEASE and w["r_min"] >= IPC_RELEASE and w["broken"] == 1, w
-    for r in range(world):
-        assert res[r]["step4"] and "failed part-way earlier" in res[r]["step4"], (r, res[r]["step4"])
-        assert res[r]["drain_s"] < 30 and res[r]["free_s"] < 70, (r, res[r]["drain_s"], res[r]["free_s"])
+    assert len({res[r]["resync_digest"] for r in range(world)}) == 1, "z / last differ across ranks after the resync"
+    assert len({res[r]["rccl_digest"] for r in range(world)}) == 1, "z / last differ across ranks after the RCCL step"
