@@ -454,11 +454,13 @@ def _hip():
 def test_task_wait_table_stays_bounded_over_1000_task_streams():
     # VERDICT r05 Weak #6: one deferred-wait entry per caller stream, never
     # pruned.  1,000 task streams, each created, given one replica update
-    # (cbx_replica_optimise) and destroyed: first each drained before it goes
-    # (the table must not grow at all), then chained by events and NOT drained
-    # (every entry stays pending: the table must stop at its cap of 64, by
-    # queuing the waits on the sync stream).  The whole sequence, and the
-    # barrier after it, bit for bit against the oracle.
+    # (cbx_replica_optimise) and destroyed: first each drained and destroyed
+    # before the next (the table must not grow at all), then chained by
+    # events behind a ~100 ms head and destroyed only after the barrier (HIP's
+    # hipStreamDestroy drains the stream): every entry stays incomplete, so
+    # the table must stop at its cap of 64, by queuing the waits on the sync
+    # stream.  The whole sequence, and the barrier after it, bit for bit
+    # against the oracle.
     import ctypes
 
     import torch
@@ -477,7 +479,7 @@ def test_task_wait_table_stays_bounded_over_1000_task_streams():
             g.replica_write(i, BUF_GRADIENT, grads[i])
             g.replica_write(i, BUF_LAST, lasts[i])
         g.wait()
-        counts, prev = [], None
+        counts, prev, live = [], None, []
         for k in range(1000):
             chained = k >= 500
             s, e = ctypes.c_void_p(), ctypes.c_void_p()
@@ -495,9 +497,10 @@ def test_task_wait_table_stays_bounded_over_1000_task_streams():
                 if prev is not None:
                     assert hip.hipEventDestroy(prev) == 0
                 prev = e
+                live.append(s)  # hipStreamDestroy would drain it: these go after the barrier
             else:
                 assert hip.hipStreamSynchronize(s) == 0
-            assert hip.hipStreamDestroy(s) == 0
+                assert hip.hipStreamDestroy(s) == 0
             counts.append(g.task_wait_count(0))
         g.lockAny()
         g.synchronise(0, 1, 0, False)  # waits for every update (flush_task_waits)
@@ -506,6 +509,8 @@ def test_task_wait_table_stays_bounded_over_1000_task_streams():
         g.wait()
         if prev is not None:
             assert hip.hipEventDestroy(prev) == 0
+        for s in live:
+            assert hip.hipStreamDestroy(s) == 0
         print(f"task-wait table: max {max(counts[:500])} entries unchained, max {max(counts[500:])} chained")
         assert max(counts[:500]) <= 2, counts[:500]
         assert max(counts[500:]) == 64, max(counts[500:])

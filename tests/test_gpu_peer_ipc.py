@@ -392,6 +392,9 @@ def test_peer_read_failed_step_releases_and_stops_every_rank():
     world = 3
     with tempfile.TemporaryDirectory(dir=C.loopback_dir(1 << 30)) as d:
         res = _spawn(world, _failing_main, lambda r: (r, world, d), timeout=260)
+    for r in range(world):  # what each rank saw (pytest -s)
+        print(f"rank {r}: refused at call {sorted(res[r]['errors'])}, enqueued {res[r]['ok_steps']}, cbx_wait: "
+              f"{(res[r]['wait'] or 'OK (oracle-exact, every element)')[:90]}")
     assert "fault injection" in res[1]["errors"].get(3, "") and set(res[1]["errors"]) == {3}, res[1]["errors"]
     for r in range(world):
         errs, wait = res[r]["errors"], res[r]["wait"]
