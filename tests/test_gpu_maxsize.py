@@ -6,9 +6,9 @@ most 2^31 - 1 bytes: n = 536,870,911 floats, whose last byte offsets reach
 2^31, where signed 32-bit arithmetic would turn negative.  (The kernels'
 own limit is 4 GiB per buffer: unsigned 32-bit byte offsets from a uniform
 base, crossbow_amd/csrc/sma_kernels.hip.)  At that size the step is checked
-bit for bit against the oracle on sampled element positions, with dense
-windows at the head, around byte offset 2^30 and in the ragged tail below
-2^31, and by the size-independent conservation checksum
+bit for bit against the oracle in every element (through byte offset 2^30
+and the ragged tail below 2^31), and by the size-independent conservation
+checksum
 z' + sum_i w_i' = z + sum_i w_i + 0.9 last, summed on the device in fp64.
 Both the fused kernel and the split pipeline (kernel A / one-rank all-reduce /
 kernel B over buckets, i.e. per-bucket base offsets) run.  A size that does
@@ -53,8 +53,13 @@ def test_one_past_the_limit_is_refused():
         g.free()
 
 
+@pytest.mark.timeout(330)
 @pytest.mark.parametrize("split", [False, True])
-def test_max_size_sampled_parity_and_conservation(split):
+def test_max_size_parity_every_element_and_conservation(split):
+    # Every element of z, last and both w against the oracle (no
+    # sample): the inputs are cloned on the device before the step, then
+    # inputs and outputs come down chunk by chunk (the step is elementwise)
+    # and the oracle runs on each chunk.
     import torch
     from crossbow_amd import BUF_DATA, BUF_DIFF, BUF_LAST
     n, R = N_MAX, 2  # ragged: n % 4 == 3
@@ -68,23 +73,12 @@ def test_max_size_sampled_parity_and_conservation(split):
         z, last = _view(g.base_buffer(0, BUF_DATA), n), _view(g.base_buffer(0, BUF_LAST), n)
         s = [_view(g.replica_buffer(i, BUF_DIFF), n) for i in range(R)]
         w = [_view(g.replica_buffer(i, BUF_DATA), n) for i in range(R)]
-        rng = np.random.default_rng(11)
-        windows = [np.arange(a, b) for a, b in (
-            (0, 4096), (2**28 - 2048, 2**28 + 2048),  # byte offset 2^30
-            (n - 8192, n))]                            # the ragged tail, byte offsets up to 2^31
-        idx = np.unique(np.concatenate(windows + [rng.integers(0, n, 200_000)]))
-        idx = idx[idx < n]
-        ti = torch.from_numpy(idx).cuda()
-
-        def sample(t):
-            return t[ti].cpu().numpy()
 
         def total(ts):
             return sum(float(torch.sum(t, dtype=torch.float64)) for t in ts)
 
         torch.cuda.synchronize()
-        z0, l0 = sample(z), sample(last)
-        s0, w0 = [sample(t) for t in s], [sample(t) for t in w]
+        z0, l0, w0 = z.clone(), last.clone(), [t.clone() for t in w]  # s is not written by the step
         before = total([z] + w) + 0.9 * total([last])
         g.lockAny()
         g.synchronise(0, 1, 0, False)
@@ -93,12 +87,21 @@ def test_max_size_sampled_parity_and_conservation(split):
         torch.cuda.synchronize()
         after = total([z] + w)
         assert abs(after - before) <= 1e-6 * max(1.0, abs(before)) + 1e-1, (after, before)
-        st = O.SmaState(1, R, idx.size, 0.1, 0.9, [z0.copy()], [l0.copy()], [x.copy() for x in s0],
-                        [x.copy() for x in w0])
-        O.sma_step(st)
-        assert_bitexact(sample(z), st.z[0], "z sample")
-        assert_bitexact(sample(last), st.last[0], "last sample")
-        for i in range(R):
-            assert_bitexact(sample(w[i]), st.w[i], f"w[{i}] sample")
+        chunk, compared = 1 << 26, 0
+        for a in range(0, n, chunk):
+            b = min(n, a + chunk)
+
+            def host(t):
+                return t[a:b].cpu().numpy()
+
+            st = O.SmaState(1, R, b - a, 0.1, 0.9, [host(z0)], [host(l0)], [host(t) for t in s], [host(t) for t in w0])
+            O.sma_step(st)
+            assert_bitexact(host(z), st.z[0], f"z[{a}:{b}]")
+            assert_bitexact(host(last), st.last[0], f"last[{a}:{b}]")
+            for i in range(R):
+                assert_bitexact(host(w[i]), st.w[i], f"w[{i}][{a}:{b}]")
+            compared += (2 + R) * (b - a)
+        assert compared == (2 + R) * n
+        print(f"max size ({'split' if split else 'fused'}): {compared} elements compared bit for bit (n = {n})")
     finally:
         g.free()

@@ -414,3 +414,96 @@ def test_peer_read_failed_step_releases_and_stops_every_rank():
     assert w["a_min"] >= IPC_RELEASE and w["r_min"] >= IPC_RELEASE and w["broken"] == 1, w
     assert len({res[r]["resync_digest"] for r in range(world)}) == 1, "z / last differ across ranks after the resync"
     assert len({res[r]["rccl_digest"] for r in range(world)}) == 1, "z / last differ across ranks after the RCCL step"
+
+
+# The per-rank form's export limit (kIpcMaxSlotBytes, context_internal.h):
+# ROCm 7.0's IPC keeps an allocation's size in 32 bits, so every exported
+# buffer stays below 2 GiB once hipMalloc has rounded it to 2 MiB.  A slot is
+# round_up(16 n4 + 256, 2 MiB) + 4 KiB bytes, so the reachable slots nearest
+# the limit are 2044 MiB + 4 KiB (accepted: its allocation rounds to 2046 MiB
+# = the limit) and 2046 MiB + 4 KiB (refused).  ADVICE r05: the boundary
+# itself, not 2042 MiB, and the first size past it.
+IPC_MAX_SLOT = (2 << 30) - (2 << 20)
+
+
+def _slot_bytes(n: int) -> int:
+    n4 = -(-(-(-n // 4)) // 1024) * 1024
+    return -(-(16 * n4 + 256) // (2 << 20)) * (2 << 20) + 4096
+
+
+N_SLOT_OK, N_SLOT_REFUSED = 535_818_240, 535_822_336
+assert _slot_bytes(N_SLOT_OK) == (2044 << 20) + 4096 <= IPC_MAX_SLOT
+assert _slot_bytes(N_SLOT_REFUSED) == (2046 << 20) + 4096 > IPC_MAX_SLOT
+
+
+def _boundary_main(rank, world, d, q):
+    rank_env(rank)
+    try:
+        L, A = load_real()
+        O = C.oracle()
+        out = {}
+        g = C.init_rank(L, A, rank, world, share_uid(L, rank, os.path.join(d, "uid_refused")))
+        try:
+            C.setup_model(g, A, N_SLOT_REFUSED, 1, 0.9, 7, A.SYNC_BSP, 2 * world)
+            buf = ctypes.create_string_buffer(A.PEER_BLOB_BYTES)
+            nb = ctypes.c_size_t(0)
+            rc = L.cbx_peer_export(g.c, buf, ctypes.byref(nb))
+            out["refused"] = (rc, L.cbx_last_error().decode())
+        finally:
+            g.free()
+        n = N_SLOT_OK
+        g = C.init_rank(L, A, rank, world, share_uid(L, rank, os.path.join(d, "uid_ok")))
+        try:
+            C.setup_model(g, A, n, 1, 0.9, 7, A.SYNC_BSP, 2 * world)
+            exchange(g, rank, world, d, "edge")  # opens the other rank's 2046 MiB allocations
+            g("cbx_set_allreduce_algorithm", PEER)
+            g("cbx_set_bucket_elements", ctypes.c_longlong(1 << 26))  # 8 buckets
+            g("cbx_fill_synthetic", 3)
+            rng = np.random.default_rng(5)
+            half = n // 2  # around the two ranks' shards of each bucket and the buffer's ends
+            idx = np.unique(np.concatenate([rng.integers(0, n, 100_000), np.arange(4096), np.arange(n - 4096, n),
+                                            np.arange(half - 2048, half + 2048)]))
+            z0 = g.read("cbx_base_read", rank, A.BUF_DATA, n)
+            l0 = g.read("cbx_base_read", rank, A.BUF_LAST, n)
+            s0 = g.read("cbx_replica_read", rank, A.BUF_DIFF, n)[idx]
+            w0 = g.read("cbx_replica_read", rank, A.BUF_DATA, n)[idx]
+            np.savez(os.path.join(d, f"edge_{rank}.tmp.npz"), z=z0[idx], last=l0[idx], s=s0, w=w0)
+            os.replace(os.path.join(d, f"edge_{rank}.tmp.npz"), os.path.join(d, f"edge_{rank}.npz"))
+            del z0, l0
+            g("cbx_lock_any")
+            g("cbx_synchronise", 0, 1, 0, 0)
+            g("cbx_unlock_any")
+            g("cbx_wait")
+            z1 = g.read("cbx_base_read", rank, A.BUF_DATA, n)
+            l1 = g.read("cbx_base_read", rank, A.BUF_LAST, n)
+            out["digest"] = C.digest(z1, l1)
+            z1, l1 = z1[idx], l1[idx]
+            w1 = g.read("cbx_replica_read", rank, A.BUF_DATA, n)[idx]
+        finally:
+            g.free()
+        C.wait_files([os.path.join(d, f"edge_{r}.npz") for r in range(world)], seconds=120)
+        ins = [np.load(os.path.join(d, f"edge_{r}.npz")) for r in range(world)]
+        st = O.SmaState(world, world, idx.size, 0.1, 0.9, [f["z"].copy() for f in ins],
+                        [f["last"].copy() for f in ins], [f["s"].copy() for f in ins], [f["w"].copy() for f in ins])
+        O.sma_step(st)
+        check = C.Checker(exact=True)
+        check("z sample", z1, st.z[rank])
+        check("last sample", l1, st.last[rank])
+        check(f"w[{rank}] sample", w1, st.w[rank])
+        out["bad"] = check.bad
+        q.put((rank, out, None))
+    except Exception:  # pragma: no cover - reported to the parent
+        import traceback
+        q.put((rank, None, traceback.format_exc()))
+
+
+@pytest.mark.timeout(330)
+def test_peer_export_slot_boundary():
+    world = 2
+    with tempfile.TemporaryDirectory(dir=C.loopback_dir()) as d:
+        res = _spawn(world, _boundary_main, lambda r: (r, world, d), timeout=300)
+    for r in range(world):
+        rc, msg = res[r]["refused"]
+        assert rc == -8 and "at most 2046 MiB" in msg, (r, rc, msg)  # CBX_ERR_UNSUPPORTED
+        assert not res[r]["bad"], (r, res[r]["bad"])
+    assert res[0]["digest"] == res[1]["digest"], "z / last differ across ranks at the largest exported slot"
