@@ -439,9 +439,14 @@ assert _slot_bytes(N_SLOT_REFUSED) == (2046 << 20) + 4096 > IPC_MAX_SLOT
 def _boundary_main(rank, world, d, q):
     rank_env(rank)
     try:
+        # torch first, as in bench.py (crossbow_amd/_lib.py): the library then
+        # runs on torch's bundled HIP runtime (7.0), whose IPC keeps the 32-bit
+        # size the limit is for, not on the system ROCm's
+        import torch
+        hip_version = torch.version.hip
         L, A = load_real()
         O = C.oracle()
-        out = {}
+        out = {"hip": hip_version}
         g = C.init_rank(L, A, rank, world, share_uid(L, rank, os.path.join(d, "uid_refused")))
         try:
             C.setup_model(g, A, N_SLOT_REFUSED, 1, 0.9, 7, A.SYNC_BSP, 2 * world)
@@ -507,3 +512,5 @@ def test_peer_export_slot_boundary():
         assert rc == -8 and "at most 2046 MiB" in msg, (r, rc, msg)  # CBX_ERR_UNSUPPORTED
         assert not res[r]["bad"], (r, res[r]["bad"])
     assert res[0]["digest"] == res[1]["digest"], "z / last differ across ranks at the largest exported slot"
+    print(f"largest exported slot {_slot_bytes(N_SLOT_OK)} B opened and stepped, {_slot_bytes(N_SLOT_REFUSED)} B "
+          f"refused, under torch's HIP {res[0]['hip']}")
