@@ -1065,18 +1065,19 @@ void peer_close(cbx_context *c);
 // number (monotonic: a waiter waits for >=, so a flag already past it never
 // blocks).  A failed step sets its kIpcBroken word, then writes kIpcRelease
 // into its rank's words so no other rank's stream waits forever.  A release
-// lets a wait pass on a flag whose data may never have been written, so
-// every kernel B of the form reads all ranks' kIpcBroken words once its own
-// loads have returned, and a wave that finds one set records its step's
-// sequence number in the rank's kIpcPoison word (a consumer may only have
-// read stale data if a release, and so a broken word, came first).  Every
+// lets a wait pass on a flag whose data may never have been written, so a
+// one-wave kernel after each step's last kernel B (same stream: every load
+// of the step's kernels B has returned) reads all ranks' kIpcBroken words
+// and, if one is set, records the step's sequence number in the rank's
+// kIpcPoison word (a consumer may only have read stale data if a release,
+// and so a broken word, came first).  Every
 // rank checks the words before each collective step and in cbx_wait
 // (peer_guard, peer_wait_check); cbx_resync_base clears them.
 constexpr int64_t kIpcMaxBuckets = 4096;
 constexpr size_t kIpcRankWords = 2 * kIpcMaxBuckets + 64;  // a[], r[], done + padding (512 B)
 // kIpcOpened: this rank's imports are done; kIpcBroken: a step of this rank
 // failed part-way or was refused; kIpcPoison: the sequence number of a step
-// whose kernel B on this rank ran after some rank's broken word was set
+// whose kernels B on this rank may have run after some rank's broken word was set
 constexpr int kIpcA = 0, kIpcR = 1, kIpcDone = 2, kIpcOpened = 3, kIpcBroken = 4, kIpcPoison = 5;
 constexpr uint64_t kIpcRelease = 1ull << 62;
 // The largest buffer the per-rank peer-read form exports.  ROCr 1.18 as

@@ -253,22 +253,19 @@ struct PeerArgs {
   int64_t shard4;                     // float4s per shard (a multiple of kPadFloat4)
   int G;
   int pad_;
-  // apply, one process per GPU only (else null): rank 0's kIpcBroken word on
-  // the mapped flag page and the stride between ranks' words, this rank's
-  // kIpcPoison word, and the step's sequence number (context_internal.h)
-  const uint64_t *broken;
-  int64_t broken_stride;
-  uint64_t *poison;
-  uint64_t seq;
 };
 // D[shard] = sum over devices of acc[shard] in device order; the control
 // blocks are summed the same way (block 0).
 hipError_t launch_sma_peer_reduce(const PeerArgs &p, const LaunchConfig &cfg, hipStream_t stream, Timing t = {});
-// Kernel B reading D from each shard's owner: Phase C (+ D on copy).  With
-// p.broken set, each wave reads every rank's broken word after its last load
-// has returned and, if any is set, stores p.seq into *p.poison.
+// Kernel B reading D from each shard's owner: Phase C (+ D on copy).
 hipError_t launch_sma_peer_apply(const SmaArgs &a, const PeerArgs &p, bool momentum, const LaunchConfig &cfg,
                                  hipStream_t stream, Timing t = {});
+// One wave, after a per-rank peer-read step's last kernel B on the same
+// stream: if any of the G broken words (rank h's at broken + h * stride) is
+// set, store seq into *poison unless it already holds a step
+// (context_internal.h, kIpcPoison).
+hipError_t launch_peer_poison_check(const uint64_t *broken, int64_t stride, int G, uint64_t *poison, uint64_t seq,
+                                    hipStream_t stream);
 // The replica's local optimiser step of one task (the producer of s and w,
 // clib-multigpu/kernels/optimisers/sma.cu:3-100), fused into one pass.
 struct OptArgs {

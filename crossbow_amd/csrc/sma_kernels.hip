@@ -607,23 +607,28 @@ __global__ __launch_bounds__(256) void sma_peer_apply_kernel(const SmaArgs a, co
       }
     }
   }
-  if (p.broken != nullptr) {
-    // One process per GPU (context_internal.h, kIpcPoison): every load of
-    // this wave has returned, so only now read each rank's broken word, past
-    // the caches.  A flag release that let one of those loads see another
-    // rank's stale acc or D was preceded by a broken word, and shows here.
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const uint32_t lane = threadIdx.x & 63u;
-    uint64_t v = 0;
-    if (lane < (uint32_t)p.G)
-      v = __hip_atomic_load(const_cast<uint64_t *>(p.broken) + (int64_t)lane * p.broken_stride, __ATOMIC_RELAXED,
-                            __HIP_MEMORY_SCOPE_SYSTEM);
-    // The first poisoned step's number is kept: the kernels B of later steps
-    // run after this one's on the same stream, and find the word set.
-    if (__builtin_amdgcn_ballot_w64(v != 0) != 0 && lane == 0 &&
-        __hip_atomic_load(p.poison, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == 0)
-      __hip_atomic_store(p.poison, p.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  }
+}
+
+// One process per GPU (context_internal.h, kIpcPoison): launched on the sync
+// stream right after a peer-read step's last kernel B, so every load of
+// every kernel B of the step has returned before it reads each rank's broken
+// word, past the caches.  A flag release that let one of those loads see
+// another rank's stale acc or D was preceded by a broken word, and shows
+// here; lane 0 then records the step's sequence number (the first poisoned
+// step's is kept: later steps' checks run after this one on the same stream
+// and find the word set).  One wave per step: the check once per wave of
+// kernel B cost a PCIe read per wave, ~100 k small reads per step, and made
+// kernel B 40x slower (profiles/r06/rehearse_perrank_n2_wave_check.log).
+__global__ __launch_bounds__(64) void peer_poison_check_kernel(const uint64_t *broken, int64_t stride, int G,
+                                                               uint64_t *poison, uint64_t seq) {
+  const uint32_t lane = threadIdx.x & 63u;
+  uint64_t v = 0;
+  if (lane < (uint32_t)G)
+    v = __hip_atomic_load(const_cast<uint64_t *>(broken) + (int64_t)lane * stride, __ATOMIC_RELAXED,
+                          __HIP_MEMORY_SCOPE_SYSTEM);
+  if (__builtin_amdgcn_ballot_w64(v != 0) != 0 && lane == 0 &&
+      __hip_atomic_load(poison, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == 0)
+    __hip_atomic_store(poison, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // ---------------------------------------------------------------------------
@@ -1180,6 +1185,13 @@ hipError_t launch_sma_peer_apply(const SmaArgs &a, const PeerArgs &p, bool momen
   if (cfg.policy == 1)
     return momentum ? peer_apply_u<true, 1>(a, p, cfg, stream, t) : peer_apply_u<false, 1>(a, p, cfg, stream, t);
   return momentum ? peer_apply_u<true, 0>(a, p, cfg, stream, t) : peer_apply_u<false, 0>(a, p, cfg, stream, t);
+}
+
+hipError_t launch_peer_poison_check(const uint64_t *broken, int64_t stride, int G, uint64_t *poison, uint64_t seq,
+                                    hipStream_t stream) {
+  if (!broken || !poison || G < 1 || G > 64) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(peer_poison_check_kernel, dim3(1), dim3(64), 0, stream, broken, stride, G, poison, seq);
+  return hipGetLastError();
 }
 
 hipError_t launch_sma_fused(const SmaArgs &a, bool momentum, bool copy, const LaunchConfig &cfg,

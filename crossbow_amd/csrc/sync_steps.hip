@@ -1150,13 +1150,11 @@ struct SplitStep {
         p.G = pn();
         p.shard4 = peer_shard4(len_of(b), p.G);
         for (int h = 0; h < p.G; ++h) p.D[h] = p_D(h) + start_of(b);
-        if (ipc) {  // the poison check (context_internal.h, kIpcPoison)
-          p.broken = c->ipc.dpage + ipc_word(0, kIpcBroken, 0);
-          p.broken_stride = (int64_t)kIpcRankWords;
-          p.poison = c->ipc.dpage + ipc_word(c->ipc.me, kIpcPoison, 0);
-          p.seq = seq;
-        }
         HIP_TRY(cbx::launch_sma_peer_apply(a, p, mom, cfg, d.stream, t));
+        if (ipc && b == nb - 1)  // every kernel B of the step is done before it (same stream)
+          HIP_TRY(cbx::launch_peer_poison_check(c->ipc.dpage + ipc_word(0, kIpcBroken, 0), (int64_t)kIpcRankWords,
+                                                c->G, c->ipc.dpage + ipc_word(c->ipc.me, kIpcPoison, 0), seq,
+                                                d.stream));
       } else {
         HIP_TRY(cbx::launch_sma_apply(a, mom && !rsag, cfg, d.stream, t));
       }

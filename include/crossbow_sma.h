@@ -466,10 +466,11 @@ int cbx_set_allreduce_algorithm (cbx_context *ctx, int algorithm);
  *     queued flag writes), so no other rank's stream waits forever.
  *   - A released flag lets a wait pass whether or not the data it guards was
  *     written, so a step another rank had already enqueued may read the
- *     failed rank's stale acc or D.  Every kernel B of the form therefore
- *     reads every rank's broken word once its own loads have returned; a
- *     wave that finds one set records the step's sequence number on the
- *     page.  cbx_wait on that rank then returns CBX_ERR_STATE naming the
+ *     failed rank's stale acc or D.  So after each step's last kernel B, on
+ *     the same stream (every load of the step's kernels B has returned), one
+ *     wave reads every rank's broken word and, if one is set, records the
+ *     step's sequence number on the page.  cbx_wait on that rank then
+ *     returns CBX_ERR_STATE naming the
  *     step: its z and last are undefined from that step on.  A step whose
  *     cbx_wait reports nothing read only data that was complete (any stale
  *     read needs a release, and the broken word comes before it).

@@ -29,6 +29,9 @@ case "${1:-a}" in
     step peer_ipc 900 tests/test_gpu_peer_ipc.py -k "not failed_step" ;;
   c)
     step multirank_full 1100 tests/test_gpu_multirank.py -k full_size -s ;;
+  e)
+    step peer_fail 360 tests/test_gpu_peer_ipc.py -k failed_step -s
+    step peer_ipc 900 tests/test_gpu_peer_ipc.py -k "not failed_step and not slot_boundary" ;;
   d)
     step maxsize_full 700 tests/test_gpu_maxsize.py -s
     step ipc_slot_boundary 360 tests/test_gpu_peer_ipc.py -k slot_boundary -s ;;
