@@ -488,6 +488,48 @@ def run_autotune_checkpoint(g: Ctx, world: int, local: List[int], ckdir: str, ex
     return bad
 
 
+def run_resync(g: Ctx, world: int, local: List[int], root: int) -> List[str]:
+    """cbx_resync_base (ADVICE / VERDICT r05 item 1): base models that differ
+    across the devices (as after a failed step) become the root's, bit for
+    bit, on every device; then one step runs and matches the oracle from the
+    resynchronised state (every device's z / last the root's)."""
+    O = oracle()
+    A = g.A
+    n, R, mom = 30_011, 2, 0.9
+    setup_model(g, A, n, R, mom, 7, A.SYNC_BSP, 2 * world * R)
+    st = O.make_state(n, world, R, 0.1, mom)
+    zs = [O.fill_normal(n, 700 + d, 0.05) for d in range(world)]
+    ls = [O.fill_normal(n, 720 + d, 0.001) for d in range(world)]
+    for d in local:
+        g.write("cbx_base_write", d, A.BUF_DATA, zs[d])
+        g.write("cbx_base_write", d, A.BUF_LAST, ls[d])
+    mine = [i for i in range(st.size) if i % world in local]
+    for i in mine:
+        g.write("cbx_replica_write", i, A.BUF_DIFF, st.s[i])
+        g.write("cbx_replica_write", i, A.BUF_DATA, st.w[i])
+    g("cbx_resync_base", root)
+    bad = []
+    check = Checker(exact=True)
+    for d in local:
+        check(f"resync z[{d}]", g.read("cbx_base_read", d, A.BUF_DATA, n), zs[root])
+        check(f"resync last[{d}]", g.read("cbx_base_read", d, A.BUF_LAST, n), ls[root])
+    st.z = [zs[root].copy() for _ in range(world)]
+    st.last = [ls[root].copy() for _ in range(world)]
+    g("cbx_lock_any")
+    g("cbx_synchronise", 0, 1, 0, 0)
+    g("cbx_unlock_any")
+    g("cbx_wait")
+    O.sma_step(st)
+    for d in local:
+        check(f"step z[{d}]", g.read("cbx_base_read", d, A.BUF_DATA, n), st.z[d])
+        check(f"step last[{d}]", g.read("cbx_base_read", d, A.BUF_LAST, n), st.last[d])
+    for i in mine:
+        check(f"step w[{i}]", g.read("cbx_replica_read", i, A.BUF_DATA, n), st.w[i])
+    if g.L.cbx_resync_base(g.c, world) != A.CBX_ERR_INVALID:
+        bad.append("a root out of range was not refused")
+    return bad + check.bad
+
+
 def _save_npy(d: str, name: str, arr) -> None:
     tmp = os.path.join(d, name + ".tmp")
     with open(tmp, "wb") as f:

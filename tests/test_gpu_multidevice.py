@@ -100,7 +100,7 @@ def _jobs(G):
     jobs += [("golden", gc["name"]) for gc in C.golden_cases(G)]
     jobs += [("golden-peer", gc["name"]) for gc in C.golden_cases(G)]
     jobs += [("golden-rsag", gc["name"]) for gc in C.golden_cases(G)]
-    return jobs + [("bn", "bn"), ("autotune", "autotune")]
+    return jobs + [("bn", "bn"), ("autotune", "autotune"), ("resync", "resync")]
 
 
 def _worker(G, jobs, ckdir, q, threads=-1):
@@ -124,6 +124,8 @@ def _worker(G, jobs, ckdir, q, threads=-1):
                     res = {"bad": C.run_golden(g, G, local, goldens[name], algo=algo)}
                 elif kind == "bn":
                     res = {"bad": C.run_bn(g, G, local, poison=True)}
+                elif kind == "resync":
+                    res = {"bad": C.run_resync(g, G, local, root=G - 1)}
                 else:
                     res = {"bad": C.run_autotune_checkpoint(g, G, local, ckdir)}
             finally:

@@ -75,7 +75,7 @@ def _jobs(world):
     jobs = [("case", c.name) for c in _cases(world)]
     jobs += [("golden", gc["name"]) for gc in C.golden_cases(world)]
     jobs += [("golden-rsag", gc["name"]) for gc in C.golden_cases(world)]
-    return jobs + [("bn", "bn"), ("autotune", "autotune")]
+    return jobs + [("bn", "bn"), ("autotune", "autotune"), ("resync", "resync")]
 
 
 def _rank_main(rank, world, jobs, uids, fake_dir, q):
@@ -99,6 +99,8 @@ def _rank_main(rank, world, jobs, uids, fake_dir, q):
                     res = {"bad": C.run_golden(g, world, [rank], goldens[name], algo=2 if kind == "golden-rsag" else 0)}
                 elif kind == "bn":
                     res = {"bad": C.run_bn(g, world, [rank], poison=True)}
+                elif kind == "resync":
+                    res = {"bad": C.run_resync(g, world, [rank], root=world - 1)}
                 else:
                     res = {"bad": C.run_autotune_checkpoint(g, world, [rank], os.path.join(fake_dir, "ckpt"))}
             finally:
