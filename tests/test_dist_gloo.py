@@ -255,9 +255,11 @@ def _tune_main(rank, world, port, q):
         g = _FakeGpu(rank, 1000)
         g.group = 3  # a group left over from an earlier setting must not skew the sweep
         g.algo = 2   # nor an algorithm left over: the sweep runs on the all-reduce
-        t = D.tune_buckets(g, 1000, world, g.step, steps=2, warmup=1)
+        refreshed = []  # bench.py's fresh-state hook: once per candidate, before its warm-up
+        t = D.tune_buckets(g, 1000, world, g.step, steps=2, warmup=1,
+                           refresh=lambda: refreshed.append((g.elems, g.mode, g.stride, g.group, g.algo)))
         q.put((rank, (t.bucket_elements, g.elems, t.mode, g.mode, t.stride, g.stride, t.group, g.group, t.algorithm,
-                      g.algo, sorted(t.table)), None))
+                      g.algo, sorted(t.table), refreshed), None))
         D.finalize(world)
     except Exception:  # pragma: no cover
         import traceback
@@ -287,8 +289,8 @@ def test_bucket_tuning_agrees_across_ranks():
                 p.kill()
     for rank in range(world):
         assert out[rank][1] is None, out[rank][1]
-    (e0, set0, m0, setm0, s0, sets0, g0, setg0, a0, seta0, cands), \
-        (e1, set1, m1, setm1, s1, sets1, g1, setg1, a1, seta1, _) = out[0][0], out[1][0]
+    (e0, set0, m0, setm0, s0, sets0, g0, setg0, a0, seta0, cands, refreshed), \
+        (e1, set1, m1, setm1, s1, sets1, g1, setg1, a1, seta1, _, _) = out[0][0], out[1][0]
     assert e0 == e1 == set0 == set1 == 250, (out[0][0], out[1][0])
     assert m0 == m1 == setm0 == setm1 == 0
     assert s0 == s1 == sets0 == sets1 == 1
@@ -298,6 +300,9 @@ def test_bucket_tuning_agrees_across_ranks():
     want += [k + "/rsag" for k in want]  # every candidate in the reduce-scatter form too
     want += ["4/0/rsag/g2"]  # groups 1 < g < buckets, timed for the winner only
     assert cands == sorted(want)
+    # one fresh state per timed candidate and pass (2 passes), each already in that candidate's setting
+    assert len(refreshed) == 2 * len(want), (len(refreshed), len(want))
+    assert len(set(refreshed)) == len(want)
     assert a0 == a1 == seta0 == seta1 == 2  # faster on both ranks: chosen
 
 
