@@ -30,7 +30,7 @@ PYTEST="python -u -m pytest -m gpu -v -x --timeout 120 --timeout-method thread -
 IFS=',' read -ra STEPS <<< "${1:-tests,bench}"
 for s in "${STEPS[@]}"; do
   case "$s" in
-    tests) run pytest_gpu 900 $PYTEST tests ;;
+    tests) run pytest_gpu 1100 $PYTEST tests ;;
     tests:*) run "pytest_${s#tests:}" 600 $PYTEST tests -k "${s#tests:}" ;;
     bench) run bench 600 python bench.py ${BENCH_ARGS:-} ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as e; e.smoke()" ;;
