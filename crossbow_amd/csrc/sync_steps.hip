@@ -200,8 +200,8 @@ volatile uint64_t *host_word(cbx_context *c, int rank, int kind, int64_t b) {
 // A step that failed part-way, or one refused because another rank's failed:
 // no other rank may wait on this one's flags forever, and none may run
 // another step against it.  The host raises the rank's broken word (every
-// rank checks the page before its next collective step, peer_guard, and
-// every kernel B of the form checks it after its loads, kIpcPoison), and only
+// rank checks the page before its next collective step, peer_guard, and each
+// step's poison check after its last kernel B reads it, kIpcPoison), and only
 // then writes the release value into every flag word of this rank (a peer
 // stream waiting on one goes on: whatever such a wait lets a kernel read, the
 // broken word was set before it).  The
@@ -284,8 +284,8 @@ int peer_wait_check(cbx_context *c) {
   if (poisoned == 0) return CBX_OK;
   if (!p.released) release_flags(c, p.max_nb);
   p.broken = true;
-  return fail(CBX_ERR_STATE, "peer-read step %llu on rank %d ran after a rank's step failed part-way (its kernel B "
-              "found a broken word once its loads returned): this rank's z / last are undefined from that step on, "
+  return fail(CBX_ERR_STATE, "peer-read step %llu on rank %d ran after a rank's step failed part-way (the check "
+              "after its last kernel B found a broken word): this rank's z / last are undefined from that step on, "
               "and every collective step is refused until cbx_resync_base", (unsigned long long)poisoned, p.me);
 }
 
@@ -305,8 +305,8 @@ int resync_base(cbx_context *c, int root) {
     if (known) release_flags(c, p.max_nb);
   }
   if (!drain_polled(c, 60))
-    return fail(CBX_ERR_STATE, "cbx_resync_base: this rank's streams still wait 60 s on (a rank that never called "
-                "cbx_resync_base?)");
+    return fail(CBX_ERR_STATE, "cbx_resync_base: this rank's streams are still busy after 60 s (a rank that never "
+                "called cbx_resync_base?)");
   TRY(ensure_comms(c));
   auto barrier = [&]() -> int {
     NCCL_TRY(ncclGroupStart());
@@ -538,7 +538,8 @@ void peer_close(cbx_context *c) {
       // This rank's streams wait on flags a peer will never write (it died
       // mid-step): write the release into every rank's words on its behalf
       // (the page is shared), so the waits end and the streams drain; the
-      // broken word first, so a kernel B that the release lets run is poisoned.
+      // broken word first, so a step that the release lets run is reported
+      // by its poison check.
       *host_word(c, p.me, kIpcBroken, 0) = 1;
       __atomic_thread_fence(__ATOMIC_SEQ_CST);
       for (int h = 0; h < c->G; ++h)
