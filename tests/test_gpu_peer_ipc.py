@@ -246,7 +246,7 @@ def _oracle_state(O, world, size, n, ins, z_from=None):
     return O.SmaState(world, size, n, 0.1, 0.9, zs, ls, s, w)
 
 
-def _failing_main(rank, world, d, q):
+def _failing_main(rank, world, mode, d, q):
     """Rank 1's third peer-read step fails right after it queued its first
     flag write ($CBX_FAULT_PEER_FAIL="1:3").  Every rank then reports what its
     steps did, is refused in every form, resynchronises, and steps again."""
@@ -281,6 +281,7 @@ def _failing_main(rank, world, d, q):
             exchange(g, rank, world, d, "fail")
             g("cbx_set_allreduce_algorithm", PEER)
             g("cbx_set_bucket_elements", -(-n // nb))
+            g("cbx_set_pipeline_mode", mode)  # 1: kernels A of a step overlap the last one's kernels B
             g("cbx_fill_synthetic", 5)
 
             def state(tag):  # this rank's whole state, for every rank's oracle
@@ -380,7 +381,8 @@ def _failing_main(rank, world, d, q):
 
 
 @pytest.mark.timeout(280)
-def test_peer_read_failed_step_releases_and_stops_every_rank():
+@pytest.mark.parametrize("mode", [0, 1])
+def test_peer_read_failed_step_releases_and_stops_every_rank(mode):
     # ADVICE r04 / r05, VERDICT r05: a rank whose peer-read step fails after
     # queuing flag writes leaves its words at the release value (the queued
     # writes of the step's sequence number land BEFORE the queued release).
@@ -391,7 +393,7 @@ def test_peer_read_failed_step_releases_and_stops_every_rank():
     # both the RCCL and the peer-read forms run (the latter bit for bit).
     world = 3
     with tempfile.TemporaryDirectory(dir=C.loopback_dir(1 << 30)) as d:
-        res = _spawn(world, _failing_main, lambda r: (r, world, d), timeout=260)
+        res = _spawn(world, _failing_main, lambda r: (r, world, mode, d), timeout=260)
     for r in range(world):  # what each rank saw (pytest -s)
         print(f"rank {r}: refused at call {sorted(res[r]['errors'])}, enqueued {res[r]['ok_steps']}, cbx_wait: "
               f"{(res[r]['wait'] or 'OK (oracle-exact, every element)')[:90]}")
