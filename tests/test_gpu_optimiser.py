@@ -456,7 +456,7 @@ def test_task_wait_table_stays_bounded_over_1000_task_streams():
     # pruned.  1,000 task streams, each created, given one replica update
     # (cbx_replica_optimise) and destroyed: first each drained and destroyed
     # before the next (the table must not grow at all), then chained by
-    # events behind a ~100 ms head and destroyed only after the barrier (HIP's
+    # events behind a ~1 s head and destroyed only after the barrier (HIP's
     # hipStreamDestroy drains the stream): every entry stays incomplete, so
     # the table must stop at its cap of 64, by queuing the waits on the sync
     # stream.  The whole sequence, and the barrier after it, bit for bit
@@ -486,8 +486,8 @@ def test_task_wait_table_stays_bounded_over_1000_task_streams():
             assert hip.hipStreamCreateWithFlags(ctypes.byref(s), 1) == 0
             if chained and prev is not None:
                 assert hip.hipStreamWaitEvent(s, prev, 0) == 0
-            elif chained:  # the chain's head holds every later update back ~100 ms: entries pile up
-                _busy(torch, torch.cuda.ExternalStream(s.value), ms=100.0)
+            elif chained:  # the chain's head holds every later update back ~1 s: entries pile up to the cap
+                _busy(torch, torch.cuda.ExternalStream(s.value), ms=1000.0)
             i = k % R
             g.replica_optimise(i, k, s.value)
             O.sma_optimise(np.float32(-0.05), momentum, wd, st.w[i], grads[i], lasts[i], st.s[i])
