@@ -479,10 +479,14 @@ int cbx_set_allreduce_algorithm (cbx_context *ctx, int algorithm);
  *     cbx_synchronise_staged in every all-reduce form and update model, and
  *     cbx_average_batchnorm_stats) with CBX_ERR_STATE, releasing its own
  *     flags first, until cbx_resync_base.  The decision is each rank's own,
- *     made from the page when it is called: a rank that enqueued an RCCL-
- *     form step before the failure reached it may wait inside that step's
- *     collective for a rank that refuses it, so after a failure on any rank
- *     every rank stops stepping and calls cbx_resync_base.
+ *     made from the page when it is called.  A job that keeps the peer-read
+ *     form across steps always recovers (every later step is refused or
+ *     reported).  A job that switches to an RCCL collective while a failure
+ *     is still on its way to some rank can leave that rank inside a
+ *     collective the others refuse; every rank's cbx_resync_base then fails
+ *     within its 60 s bounds and the job must end, as the reference's does.
+ *     After a failure on any rank, every rank stops stepping and calls
+ *     cbx_resync_base.
  * Same results bit for bit as before whenever no rank fails.              */
 #define CBX_PEER_BLOB_BYTES 256
 int cbx_peer_export (cbx_context *ctx, void *blob, size_t *bytes);
