@@ -584,6 +584,10 @@ struct cbx_context {
   // inside hipIpcOpenMemHandle would (no timer of the library reaches it):
   // bench.py must still print its line (VERDICT r04 Next #1).
   int fault_ipc_stall_s = std::getenv("CBX_FAULT_IPC_STALL") ? std::atoi(std::getenv("CBX_FAULT_IPC_STALL")) : 0;
+  // $CBX_FAULT_IPC_OPEN_FAIL=rank (tests only): that rank's opens in
+  // cbx_peer_import fail, so every rank's import must fail with it.
+  int fault_ipc_open_fail = std::getenv("CBX_FAULT_IPC_OPEN_FAIL") ? std::atoi(std::getenv("CBX_FAULT_IPC_OPEN_FAIL"))
+                                                                    : -1;
   // $CBX_FAULT_SKIP_TASK_WAIT (tests only): cbx_replica_optimise on a
   // caller's stream queues no wait for the sync stream at all, so a barrier
   // right behind a busy task stream reads stale replicas (the test proves the

@@ -211,11 +211,15 @@ volatile uint64_t *host_word(cbx_context *c, int rank, int kind, int64_t b) {
 // writes, for the words of the `nb` buckets in use: on each stream the
 // release lands last.  No stream is synchronised here: one may wait on a
 // peer's flag that never comes (then its own earlier writes never land either).
-void release_flags(cbx_context *c, int64_t nb) {
+// `broken` false: teardown (every rank is done with every step) or a failed
+// import (no step ran); the flags go, no rank's steps are refused for it.
+void release_flags(cbx_context *c, int64_t nb, bool broken = true) {
   auto &p = c->ipc;
   if (!p.page) return;
-  *host_word(c, p.me, kIpcBroken, 0) = 1;
-  __atomic_thread_fence(__ATOMIC_SEQ_CST);
+  if (broken) {
+    *host_word(c, p.me, kIpcBroken, 0) = 1;
+    __atomic_thread_fence(__ATOMIC_SEQ_CST);
+  }
   for (int64_t b = 0; b < kIpcMaxBuckets; ++b) {
     *host_word(c, p.me, kIpcA, b) = kIpcRelease;
     *host_word(c, p.me, kIpcR, b) = kIpcRelease;
@@ -480,6 +484,8 @@ int peer_import(cbx_context *c, const void *blobs, int nranks) {
       // hipIpcOpenMemHandle would be (bounded, in 1 s sleeps).
       for (int s = 0; s < c->fault_ipc_stall_s; ++s) std::this_thread::sleep_for(std::chrono::seconds(1));
     }
+    if (c->fault_ipc_open_fail == p.me && err.empty())
+      err = fmt_msg("fault injection: rank %d's opens fail ($CBX_FAULT_IPC_OPEN_FAIL)", p.me);
     for (int h = 0; h < nranks && err.empty(); ++h) {
       char *slot[2] = {d.xslot[0], d.xslot[1]};
       for (int k = 0; k < 2 && h != p.me; ++k) {
@@ -497,12 +503,20 @@ int peer_import(cbx_context *c, const void *blobs, int nranks) {
       p.acc_ctrl[h] = reinterpret_cast<const float *>(slot[0]);
       p.D[h] = reinterpret_cast<const cbx::v4f *>(slot[1] + data);
     }
-    *host_word(c, p.me, kIpcOpened, 0) = 1;  // the next rank's turn, success or not
+    // The next rank's turn, success (1) or not (2): either satisfies its wait.
+    *host_word(c, p.me, kIpcOpened, 0) = err.empty() ? 1 : 2;
     __atomic_thread_fence(__ATOMIC_SEQ_CST);
   }
   finished.store(true, std::memory_order_release);
   timer.join();
   (void)hipStreamDestroy(park);
+  // Every rank's word is final here (this rank waited for each one's turn):
+  // the import succeeds on every rank or on none, so no rank steps in the
+  // form, or has its collective steps refused, because of another's failed
+  // import (cbx_peer_import's contract; dist.setup_peer also agrees).
+  for (int h = 0; h < nranks && err.empty(); ++h)
+    if (*host_word(c, h, kIpcOpened, 0) != 1)
+      err = fmt_msg("rank %d's import failed or timed out", h);
   if (!err.empty()) {
     peer_close(c);
     return fail(CBX_ERR_HIP, "cbx_peer_import: %s", err.c_str());
@@ -554,12 +568,15 @@ void peer_close(cbx_context *c) {
     if (drained) *host_word(c, p.me, kIpcDone, 0) = 1;
     __atomic_thread_fence(__ATOMIC_SEQ_CST);
   }
+  bool met = true;  // every rank said it is done with every step
   if (p.ready && drained) {
     // Every rank's streams must be done with this rank's memory (and this
     // rank with theirs) before any buffer goes: drained above, then meet the
     // others on the page.
-    for (int h = 0; h < c->G; ++h)
+    for (int h = 0; h < c->G; ++h) {
       while (*host_word(c, h, kIpcDone, 0) == 0 && in_time()) sched_yield();
+      met = met && *host_word(c, h, kIpcDone, 0) != 0;
+    }
   }
   if (!drained) {
     // Streams still queued against the others' memory: unmapping it (or the
@@ -579,7 +596,9 @@ void peer_close(cbx_context *c) {
     if (m) (void)hipIpcCloseMemHandle(m);
   p.mapped.clear();
   if (p.page) {
-    release_flags(c, 0);
+    // A rank still stepping when the meeting gave up must not take what it
+    // reads next for a step's data: then the release marks this rank broken.
+    release_flags(c, 0, !met);
     (void)hipHostUnregister(p.page);
     munmap(p.page, p.page_bytes);
     if (p.owner) shm_unlink(p.shm_name);

@@ -447,7 +447,8 @@ int cbx_set_allreduce_algorithm (cbx_context *ctx, int algorithm);
  *      D (hipIpcOpenMemHandle; the ranks open in turn; a rank that has not
  *      opened its handles 120 s into the import fails everyone's import) and
  *      pins the flag page
- *      (hipHostRegister).
+ *      (hipHostRegister).  It succeeds on every rank or on none: a rank
+ *      whose opens failed fails every rank's import.
  * Then CBX_ALLREDUCE_PEER is accepted.  The ranks' streams order each
  * other through the flags: a rank writes the step's sequence number after
  * its kernel A / reduction of a bucket (hipStreamWriteValue64), the others

@@ -516,3 +516,53 @@ def test_peer_export_slot_boundary():
     assert res[0]["digest"] == res[1]["digest"], "z / last differ across ranks at the largest exported slot"
     print(f"largest exported slot {_slot_bytes(N_SLOT_OK)} B opened and stepped, {_slot_bytes(N_SLOT_REFUSED)} B "
           f"refused, under torch's HIP {res[0]['hip']}")
+
+
+def _import_fail_main(rank, world, d, q):
+    """Rank 1's opens fail ($CBX_FAULT_IPC_OPEN_FAIL=1): every rank's import
+    must fail, no rank may take the form, and the RCCL form must still run on
+    every rank (a failed import refuses no collective step)."""
+    rank_env(rank)
+    os.environ["CBX_FAULT_IPC_OPEN_FAIL"] = "1"  # read at context creation
+    try:
+        L, A = load_real()
+        g = C.init_rank(L, A, rank, world, share_uid(L, rank, os.path.join(d, "uid")))
+        out = {}
+        try:
+            n = 1 << 20
+            C.setup_model(g, A, n, 2, 0.9, 7, A.SYNC_BSP, 2 * world * 2)
+            try:
+                exchange(g, rank, world, d, "impfail")
+                out["import"] = None
+            except RuntimeError as e:
+                out["import"] = str(e)
+            out["peer"] = L.cbx_set_allreduce_algorithm(g.c, PEER)
+            g("cbx_set_allreduce_algorithm", 0)
+            g("cbx_set_bucket_elements", ctypes.c_longlong(1 << 18))
+            g("cbx_fill_synthetic", 9)
+            for clock in (1, 2):
+                g("cbx_lock_any")
+                g("cbx_synchronise", 0, clock, 0, 0)
+                g("cbx_unlock_any")
+            g("cbx_wait")
+            out["digest"] = C.digest(g.read("cbx_base_read", rank, A.BUF_DATA, n),
+                                     g.read("cbx_base_read", rank, A.BUF_LAST, n))
+        finally:
+            g.free()
+        q.put((rank, out, None))
+    except Exception:  # pragma: no cover - reported to the parent
+        import traceback
+        q.put((rank, None, traceback.format_exc()))
+
+
+@pytest.mark.timeout(200)
+def test_peer_import_fails_on_every_rank_or_none():
+    world = 3
+    with tempfile.TemporaryDirectory(dir=C.loopback_dir()) as d:
+        res = _spawn(world, _import_fail_main, lambda r: (r, world, d), timeout=180)
+    assert "fault injection" in (res[1]["import"] or ""), res[1]["import"]
+    for r in (0, 2):
+        assert res[r]["import"] and "rank 1's import failed" in res[r]["import"], (r, res[r]["import"])
+    for r in range(world):
+        assert res[r]["peer"] == -2, (r, res[r]["peer"])  # CBX_ERR_STATE: the form needs a successful import
+    assert len({res[r]["digest"] for r in range(world)}) == 1, "the RCCL form after a failed import"
