@@ -573,12 +573,15 @@ struct cbx_context {
   // idle kernel ahead of each kernel A, so rank 0 reads acc before it is
   // written (results are then wrong: the test proves the waits matter).
   bool fault_skip_peer_wait = std::getenv("CBX_FAULT_SKIP_PEER_WAIT") != nullptr;
-  // $CBX_FAULT_PEER_FAIL="rank:seq" (tests only): that rank's per-rank
-  // peer-read step with sequence number seq fails right after it queued its
-  // first flag write (kernel A of bucket 0), the failure the release path
-  // must survive (queued flag writes vs the host release).
+  // $CBX_FAULT_PEER_FAIL="rank:seq[:bucket]" (tests only): that rank's
+  // per-rank peer-read step with sequence number seq fails right after it
+  // queued the flag write of kernel A of `bucket` (default 0; later buckets
+  // leave earlier buckets' collectives and kernels B queued too), the
+  // failure the release path must survive (queued flag writes vs
+  // the host release).
   int fault_peer_fail_rank = fault_pair(std::getenv("CBX_FAULT_PEER_FAIL"), 0);
   int fault_peer_fail_seq = fault_pair(std::getenv("CBX_FAULT_PEER_FAIL"), 1);
+  int fault_peer_fail_bucket = std::max(0, fault_pair(std::getenv("CBX_FAULT_PEER_FAIL"), 2));
   // $CBX_FAULT_IPC_STALL=seconds (tests only): rank 0's cbx_peer_import sleeps
   // that long where it would open the others' handles, as a thread stuck
   // inside hipIpcOpenMemHandle would (no timer of the library reaches it):
@@ -595,8 +598,8 @@ struct cbx_context {
   bool fault_skip_task_wait = std::getenv("CBX_FAULT_SKIP_TASK_WAIT") != nullptr;
 
   static int fault_pair(const char *s, int which) {
-    int v[2] = {-1, -1};
-    if (s && std::sscanf(s, "%d:%d", &v[0], &v[1]) == 2) return v[which];
+    int v[3] = {-1, -1, -1};
+    if (s && std::sscanf(s, "%d:%d:%d", &v[0], &v[1], &v[2]) >= 2) return v[which];
     return -1;
   }
 };

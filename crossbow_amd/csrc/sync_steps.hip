@@ -959,9 +959,12 @@ struct SplitStep {
       HIP_TRY(cbx::launch_sma_accumulate(offset_args(args[k], start_of(b), len_of(b)), b == 0, cfg, st, t));
       if (peer && !pipelined && !ipc) HIP_TRY(hipEventRecord(d.peer_a, st));  // the other devices' R waits on it
       TRY(put_flag(st, kIpcA, b));  // one process per GPU: the other ranks' R waits on it
-      if (ipc && b == 0 && c->fault_peer_fail_rank == c->ipc.me && (int64_t)c->fault_peer_fail_seq == (int64_t)seq)
-        return fail(CBX_ERR_STATE, "fault injection: rank %d's peer-read step %llu fails after its first flag write "
-                    "($CBX_FAULT_PEER_FAIL)", c->ipc.me, (unsigned long long)seq);
+      if (ipc && b == std::min<int64_t>(c->fault_peer_fail_bucket, nb - 1) && c->fault_peer_fail_rank == c->ipc.me &&
+          (int64_t)c->fault_peer_fail_seq == (int64_t)seq) {
+        c->fault_peer_fail_seq = -1;  // once: numbering restarts after cbx_resync_base
+        return fail(CBX_ERR_STATE, "fault injection: rank %d's peer-read step %llu fails after kernel A of bucket "
+                    "%lld ($CBX_FAULT_PEER_FAIL)", c->ipc.me, (unsigned long long)seq, (long long)b);
+      }
       if (spans) tr[k].slot->a_used[b] = t.stop;
       note_dispatch(k, si, Device::SPAN_A, t.stop, b == 0 ? t.start : nullptr);
       publish(a_seq, k, b);

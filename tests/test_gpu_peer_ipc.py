@@ -246,13 +246,14 @@ def _oracle_state(O, world, size, n, ins, z_from=None):
     return O.SmaState(world, size, n, 0.1, 0.9, zs, ls, s, w)
 
 
-def _failing_main(rank, world, mode, d, q):
-    """Rank 1's third peer-read step fails right after it queued its first
-    flag write ($CBX_FAULT_PEER_FAIL="1:3").  Every rank then reports what its
-    steps did, is refused in every form, resynchronises, and steps again."""
+def _failing_main(rank, world, mode, fail_seq, bucket, d, q):
+    """Rank 1's peer-read step `fail_seq` fails right after it queued kernel
+    A of `bucket` ($CBX_FAULT_PEER_FAIL="1:seq:bucket").  Every rank then
+    reports what its steps did, is refused in every form, resynchronises, and
+    steps again."""
     import time
     rank_env(rank)
-    os.environ["CBX_FAULT_PEER_FAIL"] = "1:3"  # read at context creation
+    os.environ["CBX_FAULT_PEER_FAIL"] = f"1:{fail_seq}:{bucket}"  # read at context creation
 
     def mark(what):  # each rank's progress, for the report if a rank never arrives
         with open(os.path.join(d, f"progress_{rank}"), "a") as f:
@@ -301,8 +302,8 @@ def _failing_main(rank, world, mode, d, q):
 
             ok_steps = 0
             for clock in (1, 2, 3):
-                if clock == 3:  # every rank has enqueued steps 1 and 2 before any enqueues step 3
-                    meet("before3")
+                if clock == fail_seq:  # every rank has enqueued the steps before it before any enqueues it
+                    meet("before_fail")
                 try:
                     step(clock)
                     ok_steps += 1
@@ -381,8 +382,8 @@ def _failing_main(rank, world, mode, d, q):
 
 
 @pytest.mark.timeout(280)
-@pytest.mark.parametrize("mode", [0, 1])
-def test_peer_read_failed_step_releases_and_stops_every_rank(mode):
+@pytest.mark.parametrize("mode,fail_seq,bucket", [(0, 3, 0), (1, 3, 0), (0, 2, 3), (1, 1, 4)])
+def test_peer_read_failed_step_releases_and_stops_every_rank(mode, fail_seq, bucket):
     # ADVICE r04 / r05, VERDICT r05: a rank whose peer-read step fails after
     # queuing flag writes leaves its words at the release value (the queued
     # writes of the step's sequence number land BEFORE the queued release).
@@ -393,18 +394,21 @@ def test_peer_read_failed_step_releases_and_stops_every_rank(mode):
     # both the RCCL and the peer-read forms run (the latter bit for bit).
     world = 3
     with tempfile.TemporaryDirectory(dir=C.loopback_dir(1 << 30)) as d:
-        res = _spawn(world, _failing_main, lambda r: (r, world, mode, d), timeout=260)
+        res = _spawn(world, _failing_main, lambda r: (r, world, mode, fail_seq, bucket, d), timeout=260)
     for r in range(world):  # what each rank saw (pytest -s)
         print(f"rank {r}: refused at call {sorted(res[r]['errors'])}, enqueued {res[r]['ok_steps']}, cbx_wait: "
               f"{(res[r]['wait'] or 'OK (oracle-exact, every element)')[:90]}")
-    assert "fault injection" in res[1]["errors"].get(3, "") and set(res[1]["errors"]) == {3}, res[1]["errors"]
+    later = set(range(fail_seq, 4))  # the failed step and every step after it
+    assert "fault injection" in res[1]["errors"].get(fail_seq, "") and set(res[1]["errors"]) == later, \
+        res[1]["errors"]
     for r in range(world):
         errs, wait = res[r]["errors"], res[r]["wait"]
-        assert set(errs) <= {3} and all("failed part-way earlier" in m or "fault injection" in m
-                                        for m in errs.values()), (r, errs)
-        # rank 1 never reduced its shard of step 3: a rank that enqueued step 3
-        # cannot have a correct one, so it must be the one cbx_wait reports
-        if r != 1 and 3 not in errs:
+        assert set(errs) <= later and all("failed part-way earlier" in m or "fault injection" in m
+                                          for m in errs.values()), (r, errs)
+        # rank 1 never reduced its shard of the failed step: a rank that
+        # enqueued that step (or a later one) cannot have a correct one, so
+        # cbx_wait must report it
+        if r != 1 and later - set(errs):
             assert wait and "ran after a rank's step failed" in wait, (r, wait)
         assert not res[r]["bad"], (r, res[r]["bad"])
         assert res[r]["drain_s"] < 30 and res[r]["free_s"] < 70, (r, res[r]["drain_s"], res[r]["free_s"])
