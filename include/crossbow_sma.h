@@ -462,9 +462,11 @@ int cbx_set_allreduce_algorithm (cbx_context *ctx, int algorithm);
  * Failure (the reference's answer to any failure is exit(1), debug.h:37; the
  * invariant at stake is that every GPU applies the same D to the same z,
  * synch/sma.c:168-174):
- *   - A step that fails part-way on a rank sets that rank's broken word on
- *     the page, then releases its flags (from the host, and again behind its
- *     queued flag writes), so no other rank's stream waits forever.
+ *   - A step that fails part-way on a rank (its call returns the error; that
+ *     rank's z, last and replicas are undefined from it on, as for a
+ *     poisoned step) sets that rank's broken word on the page, then releases
+ *     its flags (from the host, and again behind its queued flag writes), so
+ *     no other rank's stream waits forever.
  *   - A released flag lets a wait pass whether or not the data it guards was
  *     written, so a step another rank had already enqueued may read the
  *     failed rank's stale acc or D.  So after each step's last kernel B, on

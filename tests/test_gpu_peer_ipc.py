@@ -320,7 +320,11 @@ def _failing_main(rank, world, mode, fail_seq, bucket, d, q):
             out["drain_s"] = time.monotonic() - t0
             out["ok_steps"] = ok_steps
             mark(f"drained: {out['wait']}")
-            if out["wait"] is None:
+            # A step that failed part-way (the injected fault) reported itself
+            # when called and left this rank's z / last undefined: its
+            # kernels B of the buckets before the fault may have run.
+            partial = out["partial"] = any("fault injection" in m for m in out["errors"].values())
+            if out["wait"] is None and not partial:
                 # Nothing reported: every step this rank enqueued must be the
                 # oracle's, bit for bit (rank-order sums), every element.
                 ins = _load_all(d, "in", world)
@@ -330,9 +334,8 @@ def _failing_main(rank, world, mode, fail_seq, bucket, d, q):
                 check = C.Checker(exact=True)
                 check(f"z after {ok_steps} steps", g.read("cbx_base_read", rank, A.BUF_DATA, n), st.z[rank])
                 check(f"last after {ok_steps} steps", g.read("cbx_base_read", rank, A.BUF_LAST, n), st.last[rank])
-                if rank != 1:  # rank 1's kernel A of step 3 bucket 0 ran (w moved) before it failed
-                    for i in mine:
-                        check(f"w[{i}] after {ok_steps} steps", g.read("cbx_replica_read", i, A.BUF_DATA, n), st.w[i])
+                for i in mine:
+                    check(f"w[{i}] after {ok_steps} steps", g.read("cbx_replica_read", i, A.BUF_DATA, n), st.w[i])
                 out["bad"] += check.bad
             if rank == 1:
                 a, r, broken = _flag_words(d, 1, nb)
@@ -396,8 +399,10 @@ def test_peer_read_failed_step_releases_and_stops_every_rank(mode, fail_seq, buc
     with tempfile.TemporaryDirectory(dir=C.loopback_dir(1 << 30)) as d:
         res = _spawn(world, _failing_main, lambda r: (r, world, mode, fail_seq, bucket, d), timeout=260)
     for r in range(world):  # what each rank saw (pytest -s)
-        print(f"rank {r}: refused at call {sorted(res[r]['errors'])}, enqueued {res[r]['ok_steps']}, cbx_wait: "
-              f"{(res[r]['wait'] or 'OK (oracle-exact, every element)')[:90]}")
+        ok = "OK (its own step failed part-way: state undefined, not compared)" if res[r]["partial"] else \
+            "OK (oracle-exact, every element)"
+        print(f"rank {r}: failed or refused at call {sorted(res[r]['errors'])}, enqueued {res[r]['ok_steps']}, "
+              f"cbx_wait: {(res[r]['wait'] or ok)[:90]}")
     later = set(range(fail_seq, 4))  # the failed step and every step after it
     assert "fault injection" in res[1]["errors"].get(fail_seq, "") and set(res[1]["errors"]) == later, \
         res[1]["errors"]
