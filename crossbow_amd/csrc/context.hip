@@ -578,6 +578,7 @@ int cbx_unlock_any(cbx_context *c) {
 
 // ---- checkpoint -----------------------------------------------------------
 static int batchnorm_checkpoint(cbx_context *c, const std::string &dir, bool store);
+static int wait_streams(cbx_context *c);  // cbx_wait without the peer-read poison check
 
 int cbx_checkpoint_model(cbx_context *c, const char *dir) {
   TraceRange trace("cbx_checkpoint_model");
@@ -610,7 +611,7 @@ int cbx_override_model_data(cbx_context *c, const char *dir) {
   TraceRange trace("cbx_override_model_data");
   TRY(check_manager(c));
   if (!dir) return CBX_OK;  // GPU.c:1169: a null directory is a no-op
-  TRY(cbx_wait(c));
+  TRY(wait_streams(c));  // no poison check: loading a checkpoint is a way back
   std::vector<char> tmp;
   const size_t bytes = (size_t)c->n * 4;
   for (Device &d : c->devs) {
@@ -1441,13 +1442,18 @@ int cbx_base_host_buffer(cbx_context *c, int g, int kind, void **host_ptr) {
   return CBX_OK;
 }
 
-int cbx_wait(cbx_context *c) {
-  TRY(check_ctx_q(c));
+static int wait_streams(cbx_context *c) {
   TRY(flush_task_waits(c));
   for (Device &d : c->devs) {
     HIP_TRY(hipSetDevice(d.hip_id));
     HIP_TRY(hipStreamSynchronize(d.stream));
   }
+  return CBX_OK;
+}
+
+int cbx_wait(cbx_context *c) {
+  TRY(check_ctx_q(c));
+  TRY(wait_streams(c));
   return peer_wait_check(c);
 }
 

@@ -152,9 +152,12 @@ int cbx_synchronise_staged (cbx_context *ctx, int first, int clock, int autotune
 int cbx_unlock_any (cbx_context *ctx);
 
 /* ---- checkpoint / resume ---------------------------------------------- */
-/* TheGPU.checkpointModel(String)   GPU.c:1151-1163 -> executioncontext.c:2340-2367 */
+/* TheGPU.checkpointModel(String)   GPU.c:1151-1163 -> executioncontext.c:2340-2367.
+ * Waits as cbx_wait does, so it refuses (CBX_ERR_STATE) to store a model a
+ * poisoned peer-read step left undefined (cbx_peer_import below). */
 int cbx_checkpoint_model (cbx_context *ctx, const char *dir);
-/* TheGPU.overrideModelData(String) GPU.c:1165-1176 -> executioncontext.c:2369-2388 */
+/* TheGPU.overrideModelData(String) GPU.c:1165-1176 -> executioncontext.c:2369-2388.
+ * Drains the streams without that check: loading a checkpoint is a way back. */
 int cbx_override_model_data (cbx_context *ctx, const char *dir);
 /* Batch-norm running statistics in the checkpoint.  After the model files,
  * executioncontext.c:2352-2364 / 2375-2386 walk the dataflow's BATCHNORM

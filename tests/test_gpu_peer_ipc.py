@@ -319,6 +319,9 @@ def _failing_main(rank, world, mode, fail_seq, bucket, d, q):
                 out["wait"] = str(e)
             out["drain_s"] = time.monotonic() - t0
             out["ok_steps"] = ok_steps
+            if out["wait"] is not None:  # an undefined model is not checkpointed
+                os.makedirs(os.path.join(d, f"ck_{rank}"), exist_ok=True)
+                out["ckpt_rc"] = L.cbx_checkpoint_model(g.c, os.path.join(d, f"ck_{rank}").encode())
             mark(f"drained: {out['wait']}")
             # A step that failed part-way (the injected fault) reported itself
             # when called and left this rank's z / last undefined: its
@@ -415,6 +418,8 @@ def test_peer_read_failed_step_releases_and_stops_every_rank(mode, fail_seq, buc
         # cbx_wait must report it
         if r != 1 and later - set(errs):
             assert wait and "ran after a rank's step failed" in wait, (r, wait)
+        if wait:
+            assert res[r]["ckpt_rc"] == -2, (r, res[r]["ckpt_rc"])  # CBX_ERR_STATE
         assert not res[r]["bad"], (r, res[r]["bad"])
         assert res[r]["drain_s"] < 30 and res[r]["free_s"] < 70, (r, res[r]["drain_s"], res[r]["free_s"])
         for clock in (4, 5):
