@@ -643,7 +643,7 @@ def sma_dynamics(alpha: float, momentum: float, replicas_total: int) -> dict:
     has alpha N = 6.4 and radius 4.29, so the values grow ~4.3x per step from
     any start; the reference's own run (8 GPUs x 2, resnet-50.sh:74-102) and
     C5 (8 x 4) are inside the bound.  Re-snapshotting s_i <- w_i every step
-    does not change the verdict (tests/test_oracle.py).  The arithmetic per
+    does not change the verdict (tests/test_bench_cpu.py).  The arithmetic per
     element, and so the timing, is the same whatever the values."""
     import numpy as np
     aN = alpha * replicas_total
