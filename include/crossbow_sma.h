@@ -298,9 +298,10 @@ int cbx_stage_out (cbx_context *ctx);
 int cbx_replica_host_buffer (cbx_context *ctx, int id, int kind, void **host_ptr);
 int cbx_base_host_buffer (cbx_context *ctx, int device, int kind, void **host_ptr);
 /* Block until every local sync stream has drained.  One process per GPU
- * with the peer-read form imported: CBX_ERR_STATE if a drained step's kernel
- * B on this rank ran after a rank's step failed (cbx_peer_import below):
- * this rank's z and last are then undefined, until cbx_resync_base. */
+ * with the peer-read form imported: CBX_ERR_STATE if a drained step on this
+ * rank may have read a failed rank's buffers (its poison check found a
+ * broken word, cbx_peer_import below): this rank's z and last are then
+ * undefined, until cbx_resync_base. */
 int cbx_wait (cbx_context *ctx);
 /* The event (a hipEvent_t, as void*) recorded on local device `local`'s sync
  * stream at the end of every synchronise(): it stands for the reference's
