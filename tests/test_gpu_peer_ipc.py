@@ -580,3 +580,58 @@ def test_peer_import_fails_on_every_rank_or_none():
     for r in range(world):
         assert res[r]["peer"] == -2, (r, res[r]["peer"])  # CBX_ERR_STATE: the form needs a successful import
     assert len({res[r]["digest"] for r in range(world)}) == 1, "the RCCL form after a failed import"
+
+
+def _healthy_resync_main(rank, world, d, q):
+    """No failure: two peer-read steps, cbx_resync_base (a no-op for z / last,
+    which are already identical, but it clears the page and restarts the step
+    numbering), two more peer-read steps; every element against the oracle."""
+    rank_env(rank)
+    try:
+        L, A = load_real()
+        O = C.oracle()
+        g = C.init_rank(L, A, rank, world, share_uid(L, rank, os.path.join(d, "uid")))
+        try:
+            n, R = 1 << 20, 2
+            size = world * R
+            mine = [i for i in range(size) if i % world == rank]
+            C.setup_model(g, A, n, R, 0.9, 7, A.SYNC_BSP, 2 * world * R)
+            exchange(g, rank, world, d, "healthy")
+            g("cbx_set_allreduce_algorithm", PEER)
+            g("cbx_set_bucket_elements", ctypes.c_longlong(1 << 18))
+            g("cbx_set_pipeline_mode", 1)
+            g("cbx_fill_synthetic", 4)
+            _save(d, f"in_{rank}", z=g.read("cbx_base_read", rank, A.BUF_DATA, n),
+                  last=g.read("cbx_base_read", rank, A.BUF_LAST, n),
+                  s=np.stack([g.read("cbx_replica_read", i, A.BUF_DIFF, n) for i in mine]),
+                  w=np.stack([g.read("cbx_replica_read", i, A.BUF_DATA, n) for i in mine]), ids=np.array(mine))
+            for clock in (1, 2, 3, 4):
+                if clock == 3:
+                    g("cbx_resync_base", 0)
+                g("cbx_lock_any")
+                g("cbx_synchronise", 0, clock, 0, 0)
+                g("cbx_unlock_any")
+            g("cbx_wait")
+            st = _oracle_state(O, world, size, n, _load_all(d, "in", world))
+            for _ in range(4):
+                O.sma_step(st)
+            check = C.Checker(exact=True)
+            check("z", g.read("cbx_base_read", rank, A.BUF_DATA, n), st.z[rank])
+            check("last", g.read("cbx_base_read", rank, A.BUF_LAST, n), st.last[rank])
+            for i in mine:
+                check(f"w[{i}]", g.read("cbx_replica_read", i, A.BUF_DATA, n), st.w[i])
+        finally:
+            g.free()
+        q.put((rank, {"bad": check.bad}, None))
+    except Exception:  # pragma: no cover - reported to the parent
+        import traceback
+        q.put((rank, None, traceback.format_exc()))
+
+
+@pytest.mark.timeout(200)
+def test_peer_resync_without_failure_keeps_the_form_exact():
+    world = 2
+    with tempfile.TemporaryDirectory(dir=C.loopback_dir()) as d:
+        res = _spawn(world, _healthy_resync_main, lambda r: (r, world, d), timeout=180)
+    for r in range(world):
+        assert not res[r]["bad"], (r, res[r]["bad"])
